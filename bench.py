@@ -1,0 +1,187 @@
+"""Headline benchmark: whole-job training throughput (samples/s) of the MLP regression step.
+
+Config (BASELINE.json / BASELINE.md): the reference algorithm's 512-wide proxy — MLP
+512 -> 512 -> 512 -> 512 -> 1 (ReLU, MSE), 8192 rows per GPU, full-shard batch (one optimizer
+step per epoch, as the reference's DataLoader does, ref.py:146), SGD momentum 0.9, bf16 compute
+with fp32 master weights; synthetic make_regression-style data generated on device, random
+init.  Weak scaling: every GPU keeps 8192 rows (plus one extra row on the first N-1 ranks so the
+split is uneven, BASELINE config 3), gradients are all-reduced over RCCL (xGMI) every step.
+
+    python bench.py [--gpus N] [--steps K] [--warmup W]
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Rank 0 prints ONE JSON line.  The timed region is exactly K full training steps (forward,
+loss, backward, gradient all-reduce, optimizer update), bracketed by barrier + device sync on
+both sides; the reported time is the max over ranks.
+"""
+from __future__ import annotations
+
+import argparse
+import json
+import os
+import sys
+import time
+
+sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+
+# Reference numbers (reference algorithm on the 512-wide proxy, CPU, samples/s)
+BASELINE_SAMPLES_PER_S = {1: 32190.0, 2: 61546.0, 4: 88657.0, 8: 105377.0}
+
+CONFIGS = {
+    "proxy512": dict(widths=[512, 512, 512, 512, 1], loss="mse", rows=8192,
+                     model="mlp_512x4_regression(512-512-512-512-1)"),
+    "mlp512x3": dict(widths=[512, 512, 512, 1], loss="mse", rows=8192,
+                     model="mlp_512x3_regression(512-512-512-1)"),
+    "wide8192": dict(widths=[8192] * 5 + [1], loss="mse", rows=4096,
+                     model="mlp_8192x4_regression(8192x4-1)"),
+    "mnist": dict(widths=[784, 1024, 1024, 10], loss="xent", rows=8192,
+                  model="mlp_mnist_shape(784-1024-1024-10,xent)"),
+    "ref": dict(widths=[2, 3, 1], loss="mse", rows=16, model="mlp_reference(2-3-1)"),
+}
+
+
+def parse():
+    p = argparse.ArgumentParser()
+    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--steps", type=int, default=200)
+    p.add_argument("--warmup", type=int, default=20)
+    p.add_argument("--config", default="proxy512", choices=sorted(CONFIGS))
+    p.add_argument("--rows", type=int, default=None, help="rows per GPU (weak scaling)")
+    p.add_argument("--scaling", choices=["weak", "strong"], default="weak")
+    p.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
+    p.add_argument("--comm", choices=["native", "torch"], default="native")
+    p.add_argument("--bucket_mb", type=float, default=25.0)
+    p.add_argument("--no_graph", action="store_true")
+    p.add_argument("--even", action="store_true", help="no uneven extra rows")
+    return p.parse_args()
+
+
+def main():
+    a = parse()
+    import torch
+    import torch.distributed as dist
+    import nnmpi_amd  # noqa: F401
+    from nnmpi_amd.data import synth
+    from nnmpi_amd.data.partition import partition_rows
+    from nnmpi_amd.engine.arena import Arena
+    from nnmpi_amd.engine.engine import MLPEngine
+    from nnmpi_amd.engine.trainer import loss_scales
+    from nnmpi_amd.models.mlp import MLPSpec, reference_init
+    from nnmpi_amd.ops.hip_ops import HipOps
+    from nnmpi_amd.parallel import dist as pdist
+    from nnmpi_amd.parallel.sync import NativeRcclSync, NoSync, TorchDistSync
+    from nnmpi_amd.utils.config import TrainConfig
+    from nnmpi_amd import native
+
+    job = pdist.detect_job()
+    rank, world = job.rank, job.world
+    torch.cuda.set_device(job.local_rank % torch.cuda.device_count())
+    dev = torch.device("cuda", torch.cuda.current_device())
+    pg = pdist.ProcessGroupContext(job, 600.0, want_nccl=(a.comm == "torch" and world > 1))
+    c = CONFIGS[a.config]
+    widths = c["widths"]
+    spec = MLPSpec(tuple(widths), "relu", c["loss"])
+    rows_pg = a.rows or c["rows"]
+    if a.scaling == "weak":
+        n_global = rows_pg * world + (0 if a.even else world - 1)
+    else:
+        n_global = rows_pg
+    part = partition_rows(n_global, world)
+    rows = part.rows(rank)
+    dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
+
+    # data (device-generated, partition-independent rows)
+    if c["loss"] == "xent":
+        X, labels = synth.chunked_classification(part.start(rank), rows, widths[0], widths[-1],
+                                                 device=dev)
+        Y = None
+    else:
+        X, Y = synth.chunked_regression(part.start(rank), rows, widths[0], device=dev)
+        labels = None
+    # model: same seed everywhere + broadcast from rank 0 (reference ref.py:87)
+    big = spec.n_params > 20_000_000
+    model = reference_init(widths, "relu", seed=0, device=dev if big else None)
+    arena = Arena([spec.layer_shape(i) for i in range(spec.n_layers)], dev,
+                  shadow_dtype=torch.bfloat16 if dtype == torch.bfloat16 else None,
+                  bucket_bytes=a.bucket_mb * 2 ** 20)
+    arena.bind_model(model)
+    del model
+    native_comm = None
+    if world > 1 and a.comm == "native":
+        lib = native.lib()
+        uid = pg.broadcast_object(lib.rccl_unique_id() if rank == 0 else None, 0)
+        native_comm = lib.RcclComm(uid, world, rank, dev.index)
+        s = torch.cuda.current_stream()
+        native_comm.broadcast(arena.master.data_ptr(), arena.numel, 0, 0, int(s.cuda_stream))
+        s.synchronize()
+        arena.sync_shadow()
+        sync = NativeRcclSync(arena, native_comm, world)
+    elif world > 1:
+        dist.broadcast(arena.master, src=0, group=pg.nccl)
+        arena.sync_shadow()
+        sync = TorchDistSync(arena, pg.nccl, world)
+    else:
+        sync = NoSync(arena)
+    ops = HipOps(dev)
+    eng = MLPEngine(spec, arena, ops, sync, device=dev, dtype=dtype, rows_capacity=rows,
+                    lr=1e-3, momentum=0.9, use_graph=not a.no_graph)
+    eng.load_batch(X.to(dtype), Y, labels)
+    del X
+    cfg = TrainConfig(widths=list(widths), loss=c["loss"], n_features=widths[0])
+    inv, lsc, gsc = loss_scales(cfg, rows, list(part.counts), widths[-1])
+    eng.set_scales(inv, lsc, gsc)
+
+    def barrier():
+        torch.cuda.synchronize()
+        pg.barrier()
+        torch.cuda.synchronize()
+
+    for _ in range(a.warmup):
+        eng.step()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(a.steps):
+        eng.step()
+    eng.synchronize()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    pg.barrier()
+    elapsed = t1 - t0
+    if world > 1:
+        el = torch.tensor([elapsed], dtype=torch.float64)
+        pg.allreduce_cpu(el, op=dist.ReduceOp.MAX)
+        elapsed = float(el.item())
+    loss = eng.loss()
+    ms = elapsed / a.steps * 1e3
+    samples = n_global
+    value = samples * a.steps / elapsed
+    base = BASELINE_SAMPLES_PER_S.get(world) if a.config == "proxy512" else None
+    tflops = spec.flops_per_sample() * samples / (ms * 1e-3) / 1e12
+    if rank == 0:
+        out = {
+            "metric": "samples_per_sec_whole_node",
+            "value": round(value, 1),
+            "unit": "samples/s",
+            "n_gpus": world,
+            "steps": a.steps,
+            "warmup": a.warmup,
+            "ms_per_step": round(ms, 5),
+            "higher_is_better": True,
+            "scaling": a.scaling,
+            "vs_baseline": (round(value / base, 2) if base else None),
+            "dtype": a.dtype,
+            "data": "synthetic (device-generated make_regression-style rows), random init",
+            "config": {"model": c["model"], "global_batch": samples, "seq_len": None,
+                       "parallelism": f"dp{world}", "rows_per_gpu": rows_pg,
+                       "uneven_split": (not a.even and world > 1), "comm": a.comm if world > 1 else "none",
+                       "graph": not a.no_graph},
+            "model_tflops_per_s": round(tflops, 2),
+            "final_loss": loss,
+        }
+        print(json.dumps(out), flush=True)
+    native_comm = None
+    pg.destroy()
+
+
+if __name__ == "__main__":
+    main()

@@ -1,0 +1,190 @@
+// pybind11 bindings of the native runtime (kernels, RCCL communicator, gradient synchroniser,
+// graph runner).  Tensors cross the boundary as raw device addresses + the caller's HIP stream
+// (torch owns the memory; this library owns the compute/comm schedule).
+#include <pybind11/pybind11.h>
+#include <pybind11/stl.h>
+
+#include <stdexcept>
+#include <string>
+
+#include "comm/rccl_comm.h"
+#include "kernels/kernels.h"
+
+namespace py = pybind11;
+using namespace nnmpi;
+
+typedef uintptr_t uptr;
+
+static void check(hipError_t e, const char* what) {
+  if (e != hipSuccess) throw std::runtime_error(std::string(what) + ": " + hipGetErrorString(e));
+}
+
+template <typename T>
+static T* P(uptr p) { return reinterpret_cast<T*>(p); }
+static hipStream_t S(uptr s) { return reinterpret_cast<hipStream_t>(s); }
+
+PYBIND11_MODULE(_nnmpi_hip, m) {
+  m.doc() = "MI355X-native kernels and RCCL runtime for nnmpi_amd";
+
+  m.def("arch", []() {
+    int dev = 0;
+    check(hipGetDevice(&dev), "hipGetDevice");
+    hipDeviceProp_t prop;
+    check(hipGetDeviceProperties(&prop, dev), "hipGetDeviceProperties");
+    return std::string(prop.gcnArchName);
+  });
+  m.def("cu_count", []() {
+    int dev = 0, n = 0;
+    check(hipGetDevice(&dev), "hipGetDevice");
+    check(hipDeviceGetAttribute(&n, hipDeviceAttributeMultiprocessorCount, dev), "attr");
+    return n;
+  });
+  m.def("rccl_version", []() {
+    int v = 0;
+    ncclGetVersion(&v);
+    return v;
+  });
+
+  // ---- GEMMs ----
+  m.def("linear_fwd_bf16", [](uptr X, int ldx, uptr W, int ldw, uptr bias, uptr Y, int ldy, int M,
+                              int N, int K, int act, uptr s) {
+    check(linear_fwd_bf16(P<const bf16>(X), ldx, P<const bf16>(W), ldw, P<const float>(bias),
+                          P<bf16>(Y), ldy, M, N, K, act, S(s)), "linear_fwd_bf16");
+  });
+  m.def("linear_dgrad_bf16", [](uptr dZ, int lddz, uptr W, int ldw, uptr Ap, int ldap, uptr dX,
+                                int lddx, int M, int N, int K, int act, uptr s) {
+    check(linear_dgrad_bf16(P<const bf16>(dZ), lddz, P<const bf16>(W), ldw, P<const bf16>(Ap), ldap,
+                            P<bf16>(dX), lddx, M, N, K, act, S(s)), "linear_dgrad_bf16");
+  });
+  m.def("wgrad_workspace_bytes", &wgrad_workspace_bytes);
+  m.def("wgrad_splits", &wgrad_splits);
+  m.def("linear_wgrad_bf16", [](uptr dZ, int lddz, uptr X, int ldx, uptr dW, uptr db, int M, int N,
+                                int K, uptr ws, uptr s) {
+    check(linear_wgrad_bf16(P<const bf16>(dZ), lddz, P<const bf16>(X), ldx, P<float>(dW), P<float>(db),
+                            M, N, K, P<float>(ws), S(s)), "linear_wgrad_bf16");
+  });
+  m.def("gemm_bf16", [](uptr A, int lda, int la, uptr B, int ldb, int lb, int M, int N, int K, uptr C,
+                        int ldc, uptr s) {
+    check(gemm_bf16_generic(P<const bf16>(A), lda, la, P<const bf16>(B), ldb, lb, M, N, K, P<float>(C),
+                            ldc, S(s)), "gemm_bf16");
+  });
+  m.def("linear_fwd_f32", [](uptr X, int ldx, uptr W, int ldw, uptr bias, uptr Y, int ldy, int M,
+                             int N, int K, int act, uptr s) {
+    check(linear_fwd_f32(P<const float>(X), ldx, P<const float>(W), ldw, P<const float>(bias),
+                         P<float>(Y), ldy, M, N, K, act, S(s)), "linear_fwd_f32");
+  });
+  m.def("linear_dgrad_f32", [](uptr dZ, int lddz, uptr W, int ldw, uptr Ap, int ldap, uptr dX,
+                               int lddx, int M, int N, int K, int act, uptr s) {
+    check(linear_dgrad_f32(P<const float>(dZ), lddz, P<const float>(W), ldw, P<const float>(Ap), ldap,
+                           P<float>(dX), lddx, M, N, K, act, S(s)), "linear_dgrad_f32");
+  });
+  m.def("wgrad_f32_workspace_bytes", &wgrad_f32_workspace_bytes);
+  m.def("linear_wgrad_f32", [](uptr dZ, int lddz, uptr X, int ldx, uptr dW, uptr db, int M, int N,
+                               int K, uptr ws, uptr s) {
+    check(linear_wgrad_f32(P<const float>(dZ), lddz, P<const float>(X), ldx, P<float>(dW), P<float>(db),
+                           M, N, K, P<float>(ws), S(s)), "linear_wgrad_f32");
+  });
+  m.def("splitk_reduce", [](uptr ws, int S_, long long stride, int M, int N, uptr out, int ldo,
+                            uptr bws, long long bstride, uptr bout, uptr lp, int nlp, float lscale,
+                            uptr lout, uptr s) {
+    check(splitk_reduce(P<const float>(ws), S_, stride, M, N, P<float>(out), ldo, P<const float>(bws),
+                        bstride, P<float>(bout), P<const float>(lp), nlp, lscale, P<float>(lout), S(s)),
+          "splitk_reduce");
+  });
+
+  // ---- head ----
+  m.def("head_fwd_parts", &head_fwd_parts);
+  m.def("head_fwd", [](uptr a, int a_bf16, int rows, int in, uptr W, uptr b, int out, uptr y,
+                       uptr labels, int loss, float inv_count, int act_prev, uptr dz, uptr dl,
+                       uptr lp, uptr s) {
+    check(head_fwd(P<const void>(a), a_bf16, rows, in, P<const float>(W), P<const float>(b), out,
+                   P<const float>(y), P<const int64_t>(labels), loss, inv_count, act_prev, P<void>(dz),
+                   P<float>(dl), P<float>(lp), S(s)), "head_fwd");
+  });
+  m.def("head_wgrad_workspace_bytes", &head_wgrad_workspace_bytes);
+  m.def("head_wgrad", [](uptr a, int a_bf16, int rows, int in, uptr dl, int out, uptr gW, uptr gb,
+                         uptr ws, uptr lp, int nlp, float lscale, uptr lout, uptr s) {
+    check(head_wgrad(P<const void>(a), a_bf16, rows, in, P<const float>(dl), out, P<float>(gW),
+                     P<float>(gb), P<float>(ws), P<const float>(lp), nlp, lscale, P<float>(lout), S(s)),
+          "head_wgrad");
+  });
+
+  // ---- tiny fused MLP ----
+  m.def("tiny_mlp_workspace_bytes", &tiny_mlp_workspace_bytes);
+  m.def("tiny_mlp_step", [](std::vector<int> widths, std::vector<int> w_off, std::vector<int> b_off,
+                            int act, int loss, uptr params, uptr X, uptr y, uptr labels, int rows,
+                            float inv_count, uptr grad, int numel, uptr ws, uptr lout, uptr s) {
+    TinyMLPDesc d{};
+    d.n_layers = (int)widths.size() - 1;
+    if (d.n_layers < 1 || d.n_layers > 4 || (int)w_off.size() != d.n_layers || (int)b_off.size() != d.n_layers)
+      throw std::runtime_error("tiny_mlp_step: bad layer description");
+    for (size_t i = 0; i < widths.size(); ++i) d.widths[i] = widths[i];
+    for (int i = 0; i < d.n_layers; ++i) { d.w_off[i] = w_off[i]; d.b_off[i] = b_off[i]; }
+    d.act = act;
+    d.loss = loss;
+    check(tiny_mlp_step(d, P<const float>(params), P<const float>(X), P<const float>(y),
+                        P<const int64_t>(labels), rows, inv_count, P<float>(grad), numel, P<float>(ws),
+                        P<float>(lout), S(s)), "tiny_mlp_step");
+  });
+
+  // ---- optimizer / elementwise ----
+  m.def("sgd_momentum", [](uptr p, uptr g, uptr buf, uptr shadow, long long n, uptr hp, int nesterov,
+                           int first, int zero_grad, uptr s) {
+    check(sgd_momentum(P<float>(p), P<float>(g), P<float>(buf), P<bf16>(shadow), n, P<const float>(hp),
+                       nesterov, first, zero_grad, S(s)), "sgd_momentum");
+  });
+  m.def("cast_f32_bf16", [](uptr x, uptr y, long long n, uptr s) {
+    check(cast_f32_bf16(P<const float>(x), P<bf16>(y), n, S(s)), "cast_f32_bf16");
+  });
+  m.def("cast_bf16_f32", [](uptr x, uptr y, long long n, uptr s) {
+    check(cast_bf16_f32(P<const bf16>(x), P<float>(y), n, S(s)), "cast_bf16_f32");
+  });
+  m.def("scale_f32", [](uptr x, long long n, float a, uptr s) {
+    check(scale_f32(P<float>(x), n, a, S(s)), "scale_f32");
+  });
+  m.def("checksum_f32", [](uptr x, long long n, uptr out, uptr s) {
+    check(checksum_f32(P<const float>(x), n, P<double>(out), S(s)), "checksum_f32");
+  });
+
+  // ---- RCCL runtime ----
+  m.def("rccl_unique_id", []() { return py::bytes(RcclComm::get_unique_id()); });
+  py::class_<RcclComm>(m, "RcclComm")
+      .def(py::init([](py::bytes uid, int nranks, int rank, int device) {
+             return new RcclComm(std::string(uid), nranks, rank, device);
+           }), py::call_guard<py::gil_scoped_release>())
+      .def_property_readonly("rank", &RcclComm::rank)
+      .def_property_readonly("size", &RcclComm::size)
+      .def("allreduce", [](RcclComm& c, uptr buf, size_t n, int dt, int op, uptr s) {
+        c.allreduce(P<void>(buf), n, dt, op, S(s));
+      })
+      .def("broadcast", [](RcclComm& c, uptr buf, size_t n, int dt, int root, uptr s) {
+        c.broadcast(P<void>(buf), n, dt, root, S(s));
+      })
+      .def("reduce", [](RcclComm& c, uptr buf, size_t n, int dt, int op, int root, uptr s) {
+        c.reduce(P<void>(buf), n, dt, op, root, S(s));
+      })
+      .def("allgather", [](RcclComm& c, uptr sb, uptr rb, size_t n, int dt, uptr s) {
+        c.allgather(P<const void>(sb), P<void>(rb), n, dt, S(s));
+      })
+      .def("scatterv", [](RcclComm& c, uptr sb, std::vector<long long> counts,
+                          std::vector<long long> displs, uptr rb, int dt, int root, uptr s) {
+        c.scatterv(P<const void>(sb), counts, displs, P<void>(rb), dt, root, S(s));
+      })
+      .def("poll_error", &RcclComm::poll_error, py::arg("abort_on_error") = true)
+      .def("abort", &RcclComm::abort);
+  py::class_<GradSync>(m, "GradSync")
+      .def(py::init([](RcclComm* c, int nb, int prio) { return new GradSync(c, nb, prio); }),
+           py::keep_alive<1, 2>())
+      .def("bucket_ready", [](GradSync& g, int b, uptr ptr, size_t n, int dt, uptr s) {
+        g.bucket_ready(b, P<void>(ptr), n, dt, S(s));
+      })
+      .def("join", [](GradSync& g, uptr s) { g.join(S(s)); })
+      .def_property_readonly("comm_stream", [](GradSync& g) { return (uptr)g.comm_stream(); });
+  py::class_<GraphRunner>(m, "GraphRunner")
+      .def(py::init<>())
+      .def("begin", [](GraphRunner& g, uptr s) { g.begin(S(s)); })
+      .def("end", &GraphRunner::end)
+      .def("launch", [](GraphRunner& g, uptr s) { g.launch(S(s)); })
+      .def_property_readonly("ready", &GraphRunner::ready)
+      .def_property_readonly("num_nodes", &GraphRunner::num_nodes);
+}

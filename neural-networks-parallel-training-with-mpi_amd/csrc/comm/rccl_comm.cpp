@@ -1,0 +1,188 @@
+#include "rccl_comm.h"
+
+#include <cstring>
+#include <stdexcept>
+
+namespace nnmpi {
+
+#define HIP_THROW(x)                                                                     \
+  do {                                                                                   \
+    hipError_t e_ = (x);                                                                 \
+    if (e_ != hipSuccess)                                                                \
+      throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e_) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__));               \
+  } while (0)
+
+#define NCCL_THROW(x)                                                                    \
+  do {                                                                                   \
+    ncclResult_t r_ = (x);                                                               \
+    if (r_ != ncclSuccess)                                                               \
+      throw std::runtime_error(std::string("RCCL error: ") + ncclGetErrorString(r_) + " at " + \
+                               __FILE__ + ":" + std::to_string(__LINE__));               \
+  } while (0)
+
+static ncclDataType_t to_nccl(int dtype) {
+  switch (dtype) {
+    case 0: return ncclFloat32;
+    case 1: return ncclBfloat16;
+    case 2: return ncclFloat64;
+    case 3: return ncclInt64;
+    case 4: return ncclInt32;
+    case 5: return ncclUint8;
+    default: throw std::runtime_error("unsupported dtype code");
+  }
+}
+
+static size_t dtype_size(int dtype) {
+  switch (dtype) {
+    case 0: return 4;
+    case 1: return 2;
+    case 2: return 8;
+    case 3: return 8;
+    case 4: return 4;
+    case 5: return 1;
+    default: return 0;
+  }
+}
+
+static ncclRedOp_t to_op(int op) {
+  switch (op) {
+    case 0: return ncclSum;
+    case 1: return ncclAvg;
+    case 2: return ncclMax;
+    case 3: return ncclMin;
+    default: throw std::runtime_error("unsupported reduction op");
+  }
+}
+
+std::string RcclComm::get_unique_id() {
+  ncclUniqueId id;
+  NCCL_THROW(ncclGetUniqueId(&id));
+  return std::string(id.internal, sizeof(id.internal));
+}
+
+RcclComm::RcclComm(const std::string& uid, int nranks, int rank, int device)
+    : nranks_(nranks), rank_(rank), device_(device) {
+  if (uid.size() != sizeof(ncclUniqueId)) throw std::runtime_error("bad ncclUniqueId size");
+  ncclUniqueId id;
+  std::memcpy(id.internal, uid.data(), sizeof(id.internal));
+  HIP_THROW(hipSetDevice(device));
+  NCCL_THROW(ncclCommInitRank(&comm_, nranks, id, rank));
+}
+
+RcclComm::~RcclComm() {
+  if (comm_ && !aborted_) ncclCommDestroy(comm_);
+}
+
+void RcclComm::allreduce(void* buf, size_t count, int dtype, int op, hipStream_t s) {
+  NCCL_THROW(ncclAllReduce(buf, buf, count, to_nccl(dtype), to_op(op), comm_, s));
+}
+
+void RcclComm::broadcast(void* buf, size_t count, int dtype, int root, hipStream_t s) {
+  NCCL_THROW(ncclBroadcast(buf, buf, count, to_nccl(dtype), root, comm_, s));
+}
+
+void RcclComm::reduce(void* buf, size_t count, int dtype, int op, int root, hipStream_t s) {
+  NCCL_THROW(ncclReduce(buf, buf, count, to_nccl(dtype), to_op(op), root, comm_, s));
+}
+
+void RcclComm::allgather(const void* sendbuf, void* recvbuf, size_t count, int dtype, hipStream_t s) {
+  NCCL_THROW(ncclAllGather(sendbuf, recvbuf, count, to_nccl(dtype), comm_, s));
+}
+
+void RcclComm::scatterv(const void* sendbuf, const std::vector<long long>& counts,
+                        const std::vector<long long>& displs, void* recvbuf, int dtype, int root,
+                        hipStream_t s) {
+  if ((int)counts.size() != nranks_ || (int)displs.size() != nranks_)
+    throw std::runtime_error("scatterv: counts/displs must have one entry per rank");
+  const size_t es = dtype_size(dtype);
+  const ncclDataType_t dt = to_nccl(dtype);
+  NCCL_THROW(ncclGroupStart());
+  if (rank_ == root) {
+    for (int r = 0; r < nranks_; ++r) {
+      if (counts[r] == 0) continue;
+      const char* src = static_cast<const char*>(sendbuf) + displs[r] * es;
+      if (r == root) {
+        HIP_THROW(hipMemcpyAsync(recvbuf, src, counts[r] * es, hipMemcpyDeviceToDevice, s));
+      } else {
+        NCCL_THROW(ncclSend(src, counts[r], dt, r, comm_, s));
+      }
+    }
+  } else if (counts[rank_] > 0) {
+    NCCL_THROW(ncclRecv(recvbuf, counts[rank_], dt, root, comm_, s));
+  }
+  NCCL_THROW(ncclGroupEnd());
+}
+
+int RcclComm::poll_error(bool abort_on_error) {
+  if (aborted_) return (int)ncclInvalidUsage;
+  ncclResult_t r = ncclSuccess;
+  ncclCommGetAsyncError(comm_, &r);
+  if (r != ncclSuccess && r != ncclInProgress && abort_on_error) abort();
+  return r == ncclInProgress ? 0 : (int)r;
+}
+
+void RcclComm::abort() {
+  if (comm_ && !aborted_) {
+    ncclCommAbort(comm_);
+    aborted_ = true;
+  }
+}
+
+// ---------------------------------------------------------------------------------------------
+GradSync::GradSync(RcclComm* comm, int n_buckets, int priority) : comm_(comm) {
+  HIP_THROW(hipStreamCreateWithPriority(&comm_stream_, hipStreamNonBlocking, priority));
+  ready_.resize(n_buckets);
+  for (auto& e : ready_) HIP_THROW(hipEventCreateWithFlags(&e, hipEventDisableTiming));
+  HIP_THROW(hipEventCreateWithFlags(&done_, hipEventDisableTiming));
+}
+
+GradSync::~GradSync() {
+  for (auto& e : ready_) hipEventDestroy(e);
+  if (done_) hipEventDestroy(done_);
+  if (comm_stream_) hipStreamDestroy(comm_stream_);
+}
+
+void GradSync::bucket_ready(int b, void* ptr, size_t count, int dtype, hipStream_t compute) {
+  if (b < 0 || b >= (int)ready_.size()) throw std::runtime_error("bucket index out of range");
+  HIP_THROW(hipEventRecord(ready_[b], compute));
+  HIP_THROW(hipStreamWaitEvent(comm_stream_, ready_[b], 0));
+  comm_->allreduce(ptr, count, dtype, 0, comm_stream_);
+}
+
+void GradSync::join(hipStream_t compute) {
+  HIP_THROW(hipEventRecord(done_, comm_stream_));
+  HIP_THROW(hipStreamWaitEvent(compute, done_, 0));
+}
+
+// ---------------------------------------------------------------------------------------------
+GraphRunner::~GraphRunner() {
+  if (exec_) hipGraphExecDestroy(exec_);
+  if (graph_) hipGraphDestroy(graph_);
+}
+
+void GraphRunner::begin(hipStream_t s) {
+  if (exec_) { hipGraphExecDestroy(exec_); exec_ = nullptr; }
+  if (graph_) { hipGraphDestroy(graph_); graph_ = nullptr; }
+  cap_ = s;
+  HIP_THROW(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+}
+
+void GraphRunner::end() {
+  HIP_THROW(hipStreamEndCapture(cap_, &graph_));
+  HIP_THROW(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
+}
+
+void GraphRunner::launch(hipStream_t s) {
+  if (!exec_) throw std::runtime_error("graph not captured");
+  HIP_THROW(hipGraphLaunch(exec_, s));
+}
+
+size_t GraphRunner::num_nodes() const {
+  if (!graph_) return 0;
+  size_t n = 0;
+  hipGraphGetNodes(graph_, nullptr, &n);
+  return n;
+}
+
+}  // namespace nnmpi

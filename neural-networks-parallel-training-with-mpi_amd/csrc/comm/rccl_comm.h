@@ -1,0 +1,87 @@
+// Native communication runtime: one RCCL communicator per process/GPU plus a bucketed,
+// stream-overlapped gradient synchroniser.
+//
+// Replaces the reference's pickle-over-MPI star exchange (ref.py:185 comm.gather of the gradient
+// list, ref.py:190-197 root averaging, ref.py:199/203 serial send/recv) and the init
+// broadcasts (ref.py:87,97) / row scatter (ref.py:108,138):
+//   * allreduce  — ncclAllReduce(SUM) per contiguous gradient bucket on a dedicated comm stream,
+//                  gated by a "bucket ready" event recorded on the compute stream after that
+//                  layer's wgrad, joined back before the optimizer;
+//   * broadcast  — initial parameters from rank 0 (ncclBroadcast);
+//   * scatterv   — grouped ncclSend/ncclRecv with per-rank counts (uneven splits, fixes D1-D3).
+// Every call is asynchronous and hipGraph-capturable (no host sync inside).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <rccl/rccl.h>
+
+#include <string>
+#include <vector>
+
+namespace nnmpi {
+
+class RcclComm {
+ public:
+  static std::string get_unique_id();
+  RcclComm(const std::string& uid, int nranks, int rank, int device);
+  ~RcclComm();
+  RcclComm(const RcclComm&) = delete;
+  RcclComm& operator=(const RcclComm&) = delete;
+
+  int rank() const { return rank_; }
+  int size() const { return nranks_; }
+  ncclComm_t handle() const { return comm_; }
+
+  void allreduce(void* buf, size_t count, int dtype, int op, hipStream_t s);
+  void broadcast(void* buf, size_t count, int dtype, int root, hipStream_t s);
+  void reduce(void* buf, size_t count, int dtype, int op, int root, hipStream_t s);
+  // root sends counts[r] elements starting at displs[r] of sendbuf to rank r (recvbuf on r)
+  void scatterv(const void* sendbuf, const std::vector<long long>& counts,
+                const std::vector<long long>& displs, void* recvbuf, int dtype, int root,
+                hipStream_t s);
+  void allgather(const void* sendbuf, void* recvbuf, size_t count, int dtype, hipStream_t s);
+  // Returns the RCCL async error code (0 = ok); aborts the communicator on error if asked.
+  int poll_error(bool abort_on_error);
+  void abort();
+
+ private:
+  ncclComm_t comm_ = nullptr;
+  int nranks_ = 0, rank_ = 0, device_ = 0;
+  bool aborted_ = false;
+};
+
+// Bucketed gradient all-reduce overlapped with backward on a side stream.
+class GradSync {
+ public:
+  GradSync(RcclComm* comm, int n_buckets, int priority);
+  ~GradSync();
+  // compute stream -> (event) -> comm stream: all-reduce [ptr, ptr+count) of bucket b.
+  void bucket_ready(int b, void* ptr, size_t count, int dtype, hipStream_t compute);
+  // comm stream -> (event) -> compute stream: everything launched so far is complete.
+  void join(hipStream_t compute);
+  hipStream_t comm_stream() const { return comm_stream_; }
+
+ private:
+  RcclComm* comm_;
+  hipStream_t comm_stream_ = nullptr;
+  std::vector<hipEvent_t> ready_;
+  hipEvent_t done_ = nullptr;
+};
+
+// Minimal native stream-capture graph runner (hipStreamBeginCapture / hipGraphInstantiate).
+class GraphRunner {
+ public:
+  GraphRunner() = default;
+  ~GraphRunner();
+  void begin(hipStream_t s);
+  void end();
+  void launch(hipStream_t s);
+  bool ready() const { return exec_ != nullptr; }
+  size_t num_nodes() const;
+
+ private:
+  hipStream_t cap_ = nullptr;
+  hipGraph_t graph_ = nullptr;
+  hipGraphExec_t exec_ = nullptr;
+};
+
+}  // namespace nnmpi

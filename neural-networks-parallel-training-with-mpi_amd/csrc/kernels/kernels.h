@@ -1,0 +1,78 @@
+// Host-side launch API of the gfx950 kernels (all launches are asynchronous on `stream`, make
+// no allocation and no host synchronisation, so every one of them is hipGraph-capturable).
+#pragma once
+#include <hip/hip_runtime.h>
+#include <stddef.h>
+#include <stdint.h>
+
+namespace nnmpi {
+
+typedef __bf16 bf16;
+
+enum Epi : int { EPI_BIAS_ACT = 0, EPI_DACT = 1, EPI_F32 = 2 };
+enum Loss : int { LOSS_MSE = 0, LOSS_XENT = 1 };
+
+// ---- GEMM (gemm_bf16.hip) ----
+hipError_t linear_fwd_bf16(const bf16* X, int ldx, const bf16* W, int ldw, const float* bias,
+                           bf16* Y, int ldy, int M, int N, int K, int act, hipStream_t s);
+hipError_t linear_dgrad_bf16(const bf16* dZ, int lddz, const bf16* W, int ldw, const bf16* Aprev,
+                             int lda_prev, bf16* dX, int lddx, int M, int N, int K, int act,
+                             hipStream_t s);
+int wgrad_splits(int M, int N, int K);
+size_t wgrad_workspace_bytes(int M, int N, int K);
+hipError_t linear_wgrad_bf16(const bf16* dZ, int lddz, const bf16* X, int ldx, float* dW,
+                             float* db, int M, int N, int K, float* ws, hipStream_t s);
+hipError_t gemm_bf16_generic(const bf16* A, int lda, int la, const bf16* B, int ldb, int lb,
+                             int M, int N, int K, float* C, int ldc, hipStream_t s);
+hipError_t splitk_reduce(const float* ws, int S, long long stride, int M, int N, float* out,
+                         int ldo, const float* bws, long long bstride, float* bout,
+                         const float* loss_part, int n_loss_part, float loss_scale,
+                         float* loss_out, hipStream_t s);
+
+// ---- fp32 GEMM (gemm_f32.hip) ----
+hipError_t linear_fwd_f32(const float* X, int ldx, const float* W, int ldw, const float* bias,
+                          float* Y, int ldy, int M, int N, int K, int act, hipStream_t s);
+hipError_t linear_dgrad_f32(const float* dZ, int lddz, const float* W, int ldw,
+                            const float* Aprev, int lda_prev, float* dX, int lddx, int M, int N,
+                            int K, int act, hipStream_t s);
+size_t wgrad_f32_workspace_bytes(int M, int N, int K);
+hipError_t linear_wgrad_f32(const float* dZ, int lddz, const float* X, int ldx, float* dW,
+                            float* db, int M, int N, int K, float* ws, hipStream_t s);
+
+// ---- output layer + loss (head.hip) ----
+// a: [rows][in] activations (bf16 if a_bf16 else fp32); W: [out][in] fp32; y: [rows][out] fp32
+// (MSE) or labels int64 (XENT).  Writes dlogits [rows][out] fp32, dz_prev [rows][in] (same dtype
+// as a; may be null), loss partials [n_part].
+int head_fwd_parts(int rows);
+hipError_t head_fwd(const void* a, int a_bf16, int rows, int in, const float* W, const float* b,
+                    int out, const float* y, const int64_t* labels, int loss, float inv_count,
+                    int act_prev, void* dz_prev, float* dlogits, float* loss_part, hipStream_t s);
+size_t head_wgrad_workspace_bytes(int rows, int in, int out);
+hipError_t head_wgrad(const void* a, int a_bf16, int rows, int in, const float* dlogits, int out,
+                      float* gW, float* gb, float* ws, const float* loss_part, int n_loss_part,
+                      float loss_scale, float* loss_out, hipStream_t s);
+
+// ---- whole tiny MLP in one launch (tiny_mlp.hip), fp32, widths <= 16, layers <= 4 ----
+struct TinyMLPDesc {
+  int n_layers;
+  int widths[5];
+  int w_off[4];   // arena offsets of W_l
+  int b_off[4];   // arena offsets of b_l
+  int act;
+  int loss;
+};
+size_t tiny_mlp_workspace_bytes(int rows, int arena_numel);
+hipError_t tiny_mlp_step(const TinyMLPDesc& d, const float* params, const float* X,
+                         const float* y, const int64_t* labels, int rows, float inv_count,
+                         float* grad, int arena_numel, float* ws, float* loss_out, hipStream_t s);
+
+// ---- optimizer / elementwise (optim.hip) ----
+// hp = {lr, momentum, dampening, weight_decay, grad_scale}
+hipError_t sgd_momentum(float* p, float* g, float* buf, bf16* shadow, long long n,
+                        const float* hp, int nesterov, int first, int zero_grad, hipStream_t s);
+hipError_t cast_f32_bf16(const float* x, bf16* y, long long n, hipStream_t s);
+hipError_t scale_f32(float* x, long long n, float a, hipStream_t s);
+hipError_t cast_bf16_f32(const bf16* x, float* y, long long n, hipStream_t s);
+hipError_t checksum_f32(const float* x, long long n, double* out, hipStream_t s);
+
+}  // namespace nnmpi

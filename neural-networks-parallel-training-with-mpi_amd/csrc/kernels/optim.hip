@@ -1,0 +1,121 @@
+// Fused optimizer and elementwise kernels over the flat arena.
+//
+// sgd_momentum replaces torch.optim.SGD's per-tensor `_single_tensor_sgd` loop (ref.py:91,211;
+// torch/optim/sgd.py) with ONE memory-bound pass over the whole arena: it folds the gradient
+// average (1/P of the all-reduced SUM; ref.py:197's /nprocs), weight decay, momentum with
+// dampening / Nesterov, the update of the fp32 master weights, the refresh of the bf16 compute
+// shadow, and zeroes the gradient for the next step.  16-byte vector accesses, grid-stride.
+// Hyper-parameters are read from device memory so a captured hipGraph picks up LR changes.
+#include "common.h"
+#include "kernels.h"
+
+#include <algorithm>
+
+namespace nnmpi {
+
+__global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* __restrict__ g,
+                                                  float* __restrict__ buf, bf16* __restrict__ shadow,
+                                                  long long n4, const float* __restrict__ hp,
+                                                  int nesterov, int first, int zero_grad) {
+  const float lr = hp[0], mom = hp[1], damp = hp[2], wd = hp[3], gs = hp[4];
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
+    f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
+    f32x4 gv = reinterpret_cast<f32x4*>(g)[i];
+    f32x4 d = gv * gs;
+    if (wd != 0.f) d += wd * pv;
+    if (mom != 0.f) {
+      f32x4 b;
+      if (first) b = d;
+      else b = mom * reinterpret_cast<f32x4*>(buf)[i] + (1.f - damp) * d;
+      reinterpret_cast<f32x4*>(buf)[i] = b;
+      d = nesterov ? d + mom * b : b;
+    }
+    pv -= lr * d;
+    reinterpret_cast<f32x4*>(p)[i] = pv;
+    if (shadow) {
+      bf16x4 s;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) s[r] = (bf16)pv[r];
+      reinterpret_cast<bf16x4*>(shadow)[i] = s;
+    }
+    if (zero_grad) reinterpret_cast<f32x4*>(g)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+}
+
+static int grid_for(long long n, int per_thread = 1) {
+  const long long b = (n / per_thread + 255) / 256;
+  return (int)std::max<long long>(1, std::min<long long>(b, 2048));
+}
+
+hipError_t sgd_momentum(float* p, float* g, float* buf, bf16* shadow, long long n,
+                        const float* hp, int nesterov, int first, int zero_grad, hipStream_t s) {
+  if (n % 4 != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n / 4)), dim3(256), 0, s, p, g, buf, shadow, n / 4,
+                     hp, nesterov, first, zero_grad);
+  return hipGetLastError();
+}
+
+__global__ void cast_f32_bf16_kernel(const float* __restrict__ x, bf16* __restrict__ y, long long n) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = (bf16)x[i];
+}
+
+__global__ void cast_bf16_f32_kernel(const bf16* __restrict__ x, float* __restrict__ y, long long n) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) y[i] = (float)x[i];
+}
+
+__global__ void scale_kernel(float* __restrict__ x, long long n, float a) {
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride) x[i] *= a;
+}
+
+// Order-fixed fp64 checksum (replica-consistency check): per-block partial sums in LDS, then a
+// single block combines them in block order.
+__global__ void checksum_kernel(const float* __restrict__ x, long long n, double* __restrict__ part) {
+  __shared__ double red[256];
+  double s = 0.0;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    s += (double)x[i] * (double)((i % 7) + 1);
+  red[threadIdx.x] = s;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void checksum_final(double* part, int nb, double* out) {
+  if (threadIdx.x == 0 && blockIdx.x == 0) {
+    double s = 0.0;
+    for (int i = 0; i < nb; ++i) s += part[i];
+    *out = s;
+  }
+}
+
+hipError_t cast_f32_bf16(const float* x, bf16* y, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(cast_f32_bf16_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, y, n);
+  return hipGetLastError();
+}
+
+hipError_t cast_bf16_f32(const bf16* x, float* y, long long n, hipStream_t s) {
+  hipLaunchKernelGGL(cast_bf16_f32_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, y, n);
+  return hipGetLastError();
+}
+
+hipError_t scale_f32(float* x, long long n, float a, hipStream_t s) {
+  hipLaunchKernelGGL(scale_kernel, dim3(grid_for(n)), dim3(256), 0, s, x, n, a);
+  return hipGetLastError();
+}
+
+// out must hold 65 doubles (64 partials + the result at out[64]).
+hipError_t checksum_f32(const float* x, long long n, double* out, hipStream_t s) {
+  hipLaunchKernelGGL(checksum_kernel, dim3(64), dim3(256), 0, s, x, n, out);
+  hipLaunchKernelGGL(checksum_final, dim3(1), dim3(64), 0, s, out, 64, out + 64);
+  return hipGetLastError();
+}
+
+}  // namespace nnmpi

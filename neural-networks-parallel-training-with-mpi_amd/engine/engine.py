@@ -1,0 +1,246 @@
+"""Explicit data-parallel MLP training engine.
+
+One step (per rank), replacing the reference's hot loop ``ref.py:155-211`` (DataLoader ->
+``.float()`` -> forward -> MSELoss -> autograd backward -> gather/average/send -> SGD):
+
+    forward   h_i = act(h_{i-1} W_i^T + b_i)                  hidden layers (GEMM + epilogue)
+    head      logits, loss, dlogits, dZ_{L-2}, dW_{L-1}, db   fused output layer + loss
+              -> grad bucket(s) of layer L-1 ready -> all-reduce starts on the comm stream
+    backward  for i = L-2 .. 0:
+                 dW_i, db_i = dZ_i^T h_{i-1}, sum(dZ_i)       wgrad (+ fused bias grad)
+                 -> bucket ready -> all-reduce overlaps the rest of backward
+                 dZ_{i-1} = (dZ_i W_i) * act'(h_{i-1})        dgrad + activation backward
+    join      compute stream waits for the comm stream
+    update    fused SGD-momentum over the whole arena (1/P folded in, bf16 shadow refreshed,
+              gradients zeroed for the next step)
+
+All buffers are allocated once (rows capacity), so on the GPU the steady-state step is
+allocation-free and is captured into ONE hipGraph (kernels + RCCL + cross-stream events) that
+is replayed every step.  The same schedule runs with :class:`~nnmpi_amd.ops.torch_ops.TorchOps`
+on the CPU (gloo) — that is the reference-semantics path and the test oracle.
+"""
+from __future__ import annotations
+
+import math
+from typing import Dict, Optional
+
+import torch
+
+from ..models.mlp import MLPSpec
+from .arena import Arena
+
+TINY_MAX_WIDTH = 16
+TINY_MAX_LAYERS = 4
+
+
+class MLPEngine:
+    def __init__(self, spec: MLPSpec, arena: Arena, ops, sync, *, device, dtype: torch.dtype,
+                 rows_capacity: int, lr: float, momentum: float, dampening: float = 0.0,
+                 weight_decay: float = 0.0, nesterov: bool = False, use_graph: bool = True,
+                 use_tiny: Optional[bool] = None):
+        self.spec = spec
+        self.arena = arena
+        self.ops = ops
+        self.sync = sync
+        self.device = torch.device(device)
+        self.dtype = dtype
+        self.R = max(1, int(rows_capacity))
+        self.nesterov = bool(nesterov)
+        self.is_cuda = self.device.type == "cuda"
+        L = spec.n_layers
+        w = spec.widths
+        self.L = L
+        self.act = spec.activation
+        self.loss_kind = spec.loss
+        if use_tiny is None:
+            use_tiny = (self.is_cuda and dtype == torch.float32 and L <= TINY_MAX_LAYERS
+                        and max(w) <= TINY_MAX_WIDTH)
+        self.use_tiny = bool(use_tiny)
+        self.use_graph = bool(use_graph) and self.is_cuda
+        self._validate()
+        dev, R = self.device, self.R
+        self.stream = torch.cuda.Stream(device=dev) if self.is_cuda else None
+        # persistent buffers
+        self.X = torch.zeros(R, w[0], dtype=dtype, device=dev)
+        if spec.loss == "mse":
+            self.Y = torch.zeros(R, w[-1], dtype=torch.float32, device=dev)
+            self.labels = None
+        else:
+            self.Y = None
+            self.labels = torch.zeros(R, dtype=torch.int64, device=dev)
+        self.acts = [torch.zeros(R, w[i + 1], dtype=dtype, device=dev) for i in range(L - 1)]
+        maxw = max(w[1:-1]) if L > 1 else 1
+        self.dzbuf = [torch.zeros(R * maxw, dtype=dtype, device=dev) for _ in range(2)]
+        self.dlogits = torch.zeros(R, w[-1], dtype=torch.float32, device=dev)
+        self.loss_out = torch.zeros(4, dtype=torch.float32, device=dev)
+        self.hp = torch.tensor([lr, momentum, dampening, weight_decay, 1.0, 0, 0, 0],
+                               dtype=torch.float32, device=dev)
+        self.ws = torch.zeros(max(1, self._workspace_bytes() // 4 + 64), dtype=torch.float32,
+                              device=dev)
+        self.rows = 0
+        self.steps_done = 0
+        self._graphs: Dict[tuple, object] = {}
+        self.inv_count = 1.0
+        self.loss_scale = 1.0
+
+    # ------------------------------------------------------------------------------------
+    def _validate(self):
+        w = self.spec.widths
+        if self.is_cuda and not self.use_tiny:
+            if self.dtype == torch.bfloat16:
+                for i in range(self.L - 1):
+                    if w[i] % 8 or w[i + 1] % 8:
+                        raise ValueError(f"bf16 GPU path needs hidden/input widths % 8 == 0: {w}")
+            if w[-1] > 16 or w[-2] % 8:
+                raise ValueError(f"GPU head needs out <= 16 and in % 8 == 0: {w}")
+            if w[-1] * w[-2] * 4 > 65536:
+                raise ValueError("GPU head weight must fit 64 KiB of LDS")
+
+    def _workspace_bytes(self) -> int:
+        ops, R, w = self.ops, self.R, self.spec.widths
+        need = 0
+        if self.use_tiny:
+            return ops.tiny_workspace_bytes(R, self.arena.numel) if hasattr(ops, "tiny_workspace_bytes") else 0
+        if hasattr(ops, "wgrad_workspace_bytes"):
+            for i in range(self.L - 1):
+                need = max(need, ops.wgrad_workspace_bytes(R, w[i + 1], w[i], self.dtype))
+        if hasattr(ops, "head_workspace_bytes"):
+            need = max(need, ops.head_workspace_bytes(R, w[-2], w[-1]))
+        return need
+
+    # ------------------------------------------------------------------------------------
+    def set_hparams(self, lr=None, momentum=None, grad_scale=None):
+        with torch.no_grad():
+            if lr is not None:
+                self.hp[0] = lr
+            if momentum is not None:
+                self.hp[1] = momentum
+            if grad_scale is not None:
+                self.hp[4] = grad_scale
+
+    def set_scales(self, inv_count: float, loss_scale: float, grad_scale: float):
+        """Loss-gradient scale (1/count), reported-loss scale, optimizer gradient scale (1/P)."""
+        self.inv_count, self.loss_scale = float(inv_count), float(loss_scale)
+        self.set_hparams(grad_scale=grad_scale)
+
+    def load_batch(self, X: torch.Tensor, Y: Optional[torch.Tensor] = None,
+                   labels: Optional[torch.Tensor] = None):
+        """Copy a batch into the persistent (graph-stable) input buffers."""
+        n = X.shape[0]
+        if n > self.R:
+            raise ValueError(f"batch of {n} rows exceeds capacity {self.R}")
+        ctx = torch.cuda.stream(self.stream) if self.is_cuda else _nullctx()
+        with ctx, torch.no_grad():
+            self.X[:n].copy_(X, non_blocking=True)
+            if self.Y is not None and Y is not None:
+                self.Y[:n].copy_(Y.reshape(n, -1), non_blocking=True)
+            if self.labels is not None and labels is not None:
+                self.labels[:n].copy_(labels, non_blocking=True)
+        self.rows = n
+
+    # ------------------------------------------------------------------------------------
+    def _dz(self, k: int, rows: int, width: int) -> torch.Tensor:
+        return self.dzbuf[k][: rows * width].view(rows, width)
+
+    def forward_backward(self):
+        rows, ops, ar, L = self.rows, self.ops, self.arena, self.L
+        if rows == 0:  # empty shard: contributes a zero gradient, still joins every collective
+            self.loss_out.zero_()
+            for i in reversed(range(L)):
+                self.sync.ready(i)
+            return
+        if self.use_tiny:
+            ops.tiny_step(self.spec, ar, self.X[:rows], self.Y[:rows] if self.Y is not None else None,
+                          self.labels[:rows] if self.labels is not None else None,
+                          self.inv_count, self.loss_out, self.ws)
+            for i in reversed(range(L)):
+                self.sync.ready(i)
+            return
+        x = self.X[:rows]
+        h = x
+        for i in range(L - 1):
+            out = self.acts[i][:rows]
+            ops.linear_act(h, ar.compute_weight(i), ar.bias(i), self.act, out)
+            h = out
+        last = L - 1
+        dz = self._dz(0, rows, self.spec.widths[last]) if L > 1 else None
+        ops.head(h, ar.weight(last), ar.bias(last),
+                 self.Y[:rows] if self.Y is not None else None,
+                 self.labels[:rows] if self.labels is not None else None,
+                 self.loss_kind, self.inv_count, self.act if L > 1 else "none", dz,
+                 ar.grad_weight(last), ar.grad_bias(last), self.dlogits[:rows], self.loss_out,
+                 self.loss_scale, ws=self.ws)
+        self.sync.ready(last)
+        k = 0
+        for i in range(L - 2, -1, -1):
+            x_in = self.acts[i - 1][:rows] if i > 0 else x
+            ops.linear_wgrad(dz, x_in, ar.grad_weight(i), ar.grad_bias(i), ws=self.ws)
+            self.sync.ready(i)
+            if i > 0:
+                k ^= 1
+                dz_next = self._dz(k, rows, self.spec.widths[i])
+                ops.linear_dgrad(dz, ar.compute_weight(i), self.acts[i - 1][:rows], self.act, dz_next)
+                dz = dz_next
+
+    def _step_body(self, first: bool):
+        self.sync.begin()
+        self.forward_backward()
+        self.sync.finish()
+        self.ops.sgd(self.arena, self.hp, self.nesterov, first)
+
+    def step(self):
+        """One optimizer step on the loaded batch.  Asynchronous on the GPU."""
+        first = self.steps_done == 0
+        if not self.is_cuda:
+            self._step_body(first)
+        else:
+            with torch.cuda.stream(self.stream):
+                if first or not self.use_graph:
+                    self._step_body(first)
+                else:
+                    # scales are baked into the captured launches -> part of the key
+                    key = (self.rows, self.inv_count, self.loss_scale)
+                    g = self._graphs.get(key)
+                    if g is None:
+                        g = self._capture()
+                        self._graphs[key] = g
+                    g.launch(int(self.stream.cuda_stream))
+        self.steps_done += 1
+
+    def _capture(self):
+        from .. import native
+        g = native.lib().GraphRunner()
+        s = int(self.stream.cuda_stream)
+        g.begin(s)
+        try:
+            self._step_body(False)
+        except Exception:
+            try:
+                g.end()
+            except Exception:
+                pass
+            raise
+        g.end()
+        return g
+
+    def loss(self) -> float:
+        """Local (this rank's) mean loss of the last step (host sync)."""
+        if self.is_cuda:
+            self.stream.synchronize()
+        return float(self.loss_out[0].item())
+
+    def synchronize(self):
+        if self.is_cuda:
+            self.stream.synchronize()
+
+    @property
+    def flops_per_step(self) -> float:
+        return float(self.spec.flops_per_sample()) * self.rows
+
+
+class _nullctx:
+    def __enter__(self):
+        return self
+
+    def __exit__(self, *a):
+        return False

@@ -1,0 +1,341 @@
+"""``dist_train`` — the end-to-end training job (reference ``ref.py:56-236``).
+
+Per rank:
+  1. discover rank/world from the launcher environment, rendezvous (gloo control plane);
+  2. build the dataset and distribute rows (reference: rank 0 ``make_regression`` +
+     ``Scatter``/``Scatterv``, ref.py:66-143) — here with int64 counts, any world size, empty
+     shards allowed (D1-D3 fixed); per-shard (reference) or global feature scaling;
+  3. initialise the model on rank 0 with ``torch.manual_seed(0)`` (ref.py:69,84) and broadcast it
+     (ref.py:87-88) into the flat arena that backs the model's parameters;
+  4. run the epoch loop: one optimizer step per batch (full shard by default, ref.py:146),
+     gradients synchronised by bucketed all-reduce, fused SGD-momentum; print the reference's
+     two log lines (ref.py:152,224);
+  5. optionally checkpoint (reference-format state_dict) / resume, emit JSON metrics.
+"""
+from __future__ import annotations
+
+import dataclasses
+import json
+import math
+import os
+import time
+from dataclasses import dataclass, field
+from typing import List, Optional
+
+import numpy as np
+import torch
+
+from ..data import synth
+from ..data.dataset import RegressionDataset, scale_features
+from ..data.partition import partition_rows
+from ..models.mlp import MLP, MLPSpec, reference_init
+from ..parallel import dist as pdist
+from ..parallel.sync import NativeRcclSync, NoSync, TorchDistSync
+from ..utils import checkpoint as ckpt
+from ..utils.config import TrainConfig, config_from_args
+from ..utils.metrics import MetricsWriter
+from ..utils.seqcheck import SequenceChecker
+from ..utils.watchdog import Watchdog
+from .arena import Arena
+from .engine import MLPEngine
+
+SKLEARN_MAX_ELEMS = 4_000_000
+HOST_INIT_MAX_PARAMS = 20_000_000
+
+
+@dataclass
+class TrainResult:
+    rank: int
+    world: int
+    losses: List[float] = field(default_factory=list)        # local loss per epoch (printed)
+    global_losses: List[float] = field(default_factory=list)
+    final_params: Optional[torch.Tensor] = None               # forward-order flat, fp32 CPU
+    state_dict: Optional[dict] = None
+    rows: int = 0
+    epoch_times: List[float] = field(default_factory=list)
+    steps: int = 0
+
+
+def dist_train(args) -> Optional[TrainResult]:
+    cfg = config_from_args(args)
+    if cfg.nprocs and cfg.nprocs > 1 and not pdist.under_launcher():
+        pdist.spawn(_spawn_worker, cfg.nprocs, cfg)
+        return None
+    return run_worker(cfg)
+
+
+def _spawn_worker(cfg: TrainConfig):
+    run_worker(cfg)
+
+
+# --------------------------------------------------------------------------------------------
+class Job:
+    """Everything a rank needs for the run (built by :func:`setup`)."""
+
+    def __init__(self, cfg: TrainConfig):
+        self.cfg = cfg
+        self.job = pdist.detect_job()
+        self.rank, self.world = self.job.rank, self.job.world
+        self.device = torch.device("cpu")
+        if cfg.device == "cuda":
+            if not torch.cuda.is_available():
+                raise RuntimeError("--device cuda requested but no GPU is visible")
+            ndev = torch.cuda.device_count()
+            torch.cuda.set_device(self.job.local_rank % ndev)
+            self.device = torch.device("cuda", torch.cuda.current_device())
+        comm = cfg.comm
+        if comm == "auto":
+            comm = "native" if self.device.type == "cuda" else "torch"
+        if self.world == 1:
+            comm = "none"
+        self.comm_kind = comm
+        self.pg = pdist.ProcessGroupContext(self.job, cfg.timeout_s,
+                                            want_nccl=(comm == "torch" and self.device.type == "cuda"))
+        self.native_comm = None
+        if comm == "native":
+            from .. import native
+            lib = native.lib()
+            uid = lib.rccl_unique_id() if self.rank == 0 else None
+            uid = self.pg.broadcast_object(uid, 0)
+            self.native_comm = lib.RcclComm(uid, self.world, self.rank, self.device.index)
+
+    def close(self):
+        self.native_comm = None
+        self.pg.destroy()
+
+
+def _compute_dtype(cfg: TrainConfig):
+    return torch.bfloat16 if cfg.dtype == "bf16" else torch.float32
+
+
+def build_shard(j: Job):
+    """Return (X fp32 [rows, in] on device, Y fp32 [rows, out] or labels int64, partition)."""
+    cfg, rank, world = j.cfg, j.rank, j.world
+    part = partition_rows(cfg.n_samples, world)
+    rows = part.rows(rank)
+    start = part.start(rank)
+    out_f = cfg.widths[-1]
+    small = cfg.n_samples * cfg.n_features <= SKLEARN_MAX_ELEMS
+    use_sklearn = cfg.loss == "mse" and out_f == 1 and (
+        cfg.data_gen == "sklearn" or (cfg.data_gen == "auto" and small))
+    labels = None
+    if use_sklearn:
+        if cfg.data_dist == "scatter" and world > 1:
+            XY = None
+            if rank == 0:
+                X, y = synth.reference_regression(cfg.n_samples, cfg.n_features, cfg.noise, cfg.data_seed)
+                XY = synth.as_xy_matrix(X, y)
+            shard = _scatter_rows(j, XY, part, cfg.n_features + 1)
+        else:
+            X, y = synth.reference_regression(cfg.n_samples, cfg.n_features, cfg.noise, cfg.data_seed)
+            shard = synth.as_xy_matrix(X, y)[part.slice(rank)]
+        Xs, ys = shard[:, :cfg.n_features], shard[:, cfg.n_features]
+        # RegressionDataset semantics (ref.py:145): per-shard StandardScaler on float64
+        if cfg.scaling == "per_shard":
+            ds = RegressionDataset(Xs, ys, scale_data=True)
+            Xt = ds.X
+        else:
+            Xt = scale_features(torch.from_numpy(np.ascontiguousarray(Xs)), cfg.scaling,
+                                allreduce=lambda t: j.pg.allreduce_cpu(t))
+        Xt = Xt.to(torch.float32)                       # the reference's .float() (ref.py:159)
+        Yt = torch.from_numpy(np.ascontiguousarray(ys)).to(torch.float32).reshape(-1, 1)
+        return Xt.to(j.device), Yt.to(j.device), None, part
+    gen_dev = j.device
+    if cfg.loss == "xent":
+        X, labels = synth.chunked_classification(start, rows, cfg.n_features, out_f,
+                                                 seed=cfg.data_seed, device=gen_dev)
+        Y = None
+    else:
+        X, Y = synth.chunked_regression(start, rows, cfg.n_features, cfg.noise,
+                                        seed=cfg.data_seed, out=out_f, device=gen_dev)
+    if cfg.scaling != "none":
+        def ar(t):
+            tc = t.cpu()
+            j.pg.allreduce_cpu(tc)
+            t.copy_(tc)
+        X = scale_features(X, cfg.scaling, allreduce=ar)
+    return X, Y, labels, part
+
+
+def _scatter_rows(j: Job, XY, part, width: int) -> np.ndarray:
+    """Reference Scatter/Scatterv (ref.py:108,138) over gloo: padded equal chunks, trimmed."""
+    import torch.distributed as dist
+    mx = max(1, part.max_rows)
+    recv = torch.zeros(mx, width, dtype=torch.float64)
+    chunks = None
+    if j.rank == 0:
+        t = torch.from_numpy(np.ascontiguousarray(XY))
+        chunks = []
+        for r in range(j.world):
+            c = torch.zeros(mx, width, dtype=torch.float64)
+            n = part.rows(r)
+            if n:
+                c[:n] = t[part.slice(r)]
+            chunks.append(c)
+    dist.scatter(recv, chunks, src=0, group=j.pg.gloo)
+    return recv[: part.rows(j.rank)].numpy()
+
+
+def init_model(j: Job, spec: MLPSpec) -> MLP:
+    cfg = j.cfg
+    big = spec.n_params > HOST_INIT_MAX_PARAMS and j.device.type == "cuda"
+    model = reference_init(spec.widths, spec.activation, seed=cfg.seed,
+                           device=j.device if big else None)
+    return model
+
+
+def broadcast_params(j: Job, arena: Arena):
+    """Rank 0's parameters to every rank (reference ref.py:87-88 bcast(state_dict))."""
+    if j.world == 1:
+        return
+    if j.native_comm is not None:
+        from .. import native
+        s = torch.cuda.current_stream()
+        j.native_comm.broadcast(arena.master.data_ptr(), arena.numel, 0, 0, int(s.cuda_stream))
+        s.synchronize()
+    elif j.device.type == "cuda" and j.pg.nccl is not None:
+        import torch.distributed as dist
+        dist.broadcast(arena.master, src=0, group=j.pg.nccl)
+    else:
+        import torch.distributed as dist
+        t = arena.master.cpu() if j.device.type != "cpu" else arena.master
+        dist.broadcast(t, src=0, group=j.pg.gloo)
+        if t is not arena.master:
+            arena.master.copy_(t)
+    arena.sync_shadow()
+
+
+def make_sync(j: Job, arena: Arena):
+    cfg = j.cfg
+    if j.world == 1 or j.comm_kind == "none":
+        return NoSync(arena)
+    if j.comm_kind == "native":
+        if cfg.sync == "root":
+            raise ValueError("--sync root is only provided on the torch.distributed path")
+        return NativeRcclSync(arena, j.native_comm, j.world)
+    group = j.pg.nccl if (j.device.type == "cuda" and j.pg.nccl is not None) else j.pg.gloo
+    return TorchDistSync(arena, group, j.world, mode=cfg.sync, overlap=cfg.overlap)
+
+
+def make_ops(j: Job):
+    if j.device.type == "cuda":
+        from ..ops.hip_ops import HipOps
+        return HipOps(j.device)
+    from ..ops.torch_ops import TorchOps
+    return TorchOps(j.device)
+
+
+def loss_scales(cfg: TrainConfig, rows_local: int, rows_all: List[int], out_f: int):
+    """(inv_count, loss_scale, grad_scale) for one step."""
+    per = out_f if cfg.loss == "mse" else 1
+    loss_scale = 1.0 / (max(rows_local, 1) * per)
+    nonempty = sum(1 for r in rows_all if r > 0) or 1
+    if cfg.averaging == "weighted":
+        tot = sum(rows_all)
+        return 1.0 / (max(tot, 1) * per), loss_scale, 1.0
+    return loss_scale, loss_scale, 1.0 / nonempty
+
+
+def _print(cfg: TrainConfig, rank: int, msg: str):
+    if cfg.print_rank == "all" or (cfg.print_rank == "0" and rank == 0):
+        print(msg, flush=True)
+
+
+def run_worker(cfg: TrainConfig) -> TrainResult:
+    j = Job(cfg)
+    try:
+        return _run(j)
+    finally:
+        j.close()
+
+
+def _run(j: Job) -> TrainResult:
+    cfg, rank, world = j.cfg, j.rank, j.world
+    spec = MLPSpec(tuple(cfg.widths), cfg.activation, cfg.loss)
+    X, Y, labels, part = build_shard(j)
+    rows_local = X.shape[0]
+    model = init_model(j, spec)
+    dtype = _compute_dtype(cfg)
+    arena = Arena([spec.layer_shape(i) for i in range(spec.n_layers)], j.device,
+                  shadow_dtype=torch.bfloat16 if dtype == torch.bfloat16 else None,
+                  bucket_bytes=cfg.bucket_mb * 2 ** 20)
+    arena.bind_model(model)
+    broadcast_params(j, arena)
+    start_epoch, steps_done = 0, 0
+    if cfg.resume:
+        start_epoch, steps_done = ckpt.load_training_state(cfg.resume, arena)
+    sync = make_sync(j, arena)
+    ops = make_ops(j)
+    bs = cfg.batch_size
+    max_rows = part.max_rows
+    cap = min(bs, max_rows) if bs else max_rows
+    eng = MLPEngine(spec, arena, ops, sync, device=j.device, dtype=dtype,
+                    rows_capacity=max(cap, 1), lr=cfg.lr, momentum=cfg.momentum,
+                    dampening=cfg.dampening, weight_decay=cfg.weight_decay,
+                    nesterov=cfg.nesterov, use_graph=cfg.graph)
+    eng.steps_done = steps_done
+    Xc = X.to(dtype)
+    metrics = MetricsWriter(cfg.metrics_json if rank == 0 else None)
+    seqchk = SequenceChecker(j.pg) if cfg.seqcheck else None
+    wd = Watchdog(cfg.timeout_s, j.native_comm) if world > 1 else None
+    res = TrainResult(rank, world, rows=rows_local)
+    steps_per_epoch = 1 if not bs else max(1, math.ceil(max_rows / bs))
+    gen = torch.Generator(device="cpu")
+    full_loaded = False
+    try:
+        for epoch in range(start_epoch, cfg.nepochs):
+            _print(cfg, rank, "[ = = = = = Epoch {} = = = = = ]".format(epoch))
+            t0 = time.perf_counter()
+            if bs and cfg.shuffle:
+                gen.manual_seed(cfg.seed * 1000003 + rank * 7919 + epoch)
+                perm = torch.randperm(rows_local, generator=gen).to(j.device)
+            else:
+                perm = None
+            for s in range(steps_per_epoch):
+                if not bs:
+                    if not full_loaded:  # full-shard batch: order-irrelevant, uploaded once (D10)
+                        eng.load_batch(Xc, Y, labels)
+                        full_loaded = True
+                    rows_all = list(part.counts)
+                else:
+                    lo, hi = s * bs, min((s + 1) * bs, rows_local)
+                    idx = perm[lo:hi] if perm is not None else torch.arange(lo, max(lo, hi), device=j.device)
+                    eng.load_batch(Xc[idx], Y[idx] if Y is not None else None,
+                                   labels[idx] if labels is not None else None)
+                    rows_all = [max(0, min(bs, c - s * bs)) for c in part.counts]
+                inv, lsc, gsc = loss_scales(cfg, eng.rows, rows_all, cfg.widths[-1])
+                eng.set_scales(inv, lsc, gsc)
+                eng.step()
+                if wd:
+                    wd.kick()
+            loss = eng.loss()
+            dt = time.perf_counter() - t0
+            res.losses.append(loss)
+            res.epoch_times.append(dt)
+            _print(cfg, rank, f"loss in worker {rank}: {loss}")
+            if cfg.global_loss and world > 1:
+                t = torch.tensor([loss * eng.rows, float(eng.rows)], dtype=torch.float64)
+                j.pg.allreduce_cpu(t)
+                gl = float(t[0] / max(t[1], 1.0))
+                res.global_losses.append(gl)
+                _print(cfg, rank, f"global loss: {gl}") if rank == 0 else None
+            if seqchk:
+                seqchk.check(epoch, sync.seq)
+            metrics.write(epoch=epoch, loss=loss, epoch_s=dt, steps=steps_per_epoch,
+                          samples_per_s=sum(part.counts) / dt if dt > 0 else None, world=world)
+            if cfg.checkpoint and cfg.checkpoint_every and (epoch + 1) % cfg.checkpoint_every == 0:
+                if rank == 0:
+                    ckpt.save(cfg.checkpoint, arena, epoch + 1, eng.steps_done, cfg)
+                j.pg.barrier()
+        eng.synchronize()
+        res.steps = eng.steps_done
+        if cfg.checkpoint and rank == 0:
+            ckpt.save(cfg.checkpoint, arena, cfg.nepochs, eng.steps_done, cfg)
+        res.final_params = arena.flat_params_forward_order().detach().cpu().clone()
+        res.state_dict = {k: v.cpu() for k, v in arena.state_dict().items()}
+        j.pg.barrier()
+    finally:
+        if wd:
+            wd.stop()
+        metrics.close()
+    return res

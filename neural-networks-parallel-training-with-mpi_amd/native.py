@@ -1,0 +1,61 @@
+"""Loader for the native extension ``_nnmpi_hip`` (HIP kernels + RCCL runtime).
+
+torch is imported first so the extension's ``libamdhip64.so.7`` / ``librccl.so.1``
+dependencies resolve (by SONAME) to the copies torch already mapped: one HIP runtime, one
+device context, shared streams and pointers.  If the library is missing it is built in-tree
+(hipcc, gfx950).  There is no silent fallback: on a GPU device every op goes through this
+library and raises if it cannot be loaded.
+"""
+from __future__ import annotations
+
+import importlib
+import importlib.machinery
+import importlib.util
+import os
+import sys
+
+import torch  # noqa: F401  (must precede the extension import)
+
+from . import _build
+
+_lib = None
+
+
+def _load():
+    path = _build.ext_path()
+    if not os.path.exists(path):
+        _build.build(verbose=True)
+    name = __package__ + "._nnmpi_hip"
+    if name in sys.modules:
+        return sys.modules[name]
+    loader = importlib.machinery.ExtensionFileLoader(name, path)
+    spec = importlib.util.spec_from_file_location(name, path, loader=loader)
+    mod = importlib.util.module_from_spec(spec)
+    loader.exec_module(mod)
+    sys.modules[name] = mod
+    return mod
+
+
+def lib():
+    """The loaded extension module (raises if it cannot be built/loaded)."""
+    global _lib
+    if _lib is None:
+        _lib = _load()
+    return _lib
+
+
+def available() -> bool:
+    try:
+        lib()
+        return True
+    except Exception:  # pragma: no cover - diagnostic helper
+        return False
+
+
+def stream_handle(stream=None) -> int:
+    s = torch.cuda.current_stream() if stream is None else stream
+    return int(s.cuda_stream)
+
+
+def ptr(t) -> int:
+    return 0 if t is None else int(t.data_ptr())

@@ -1,0 +1,122 @@
+"""HIP (gfx950) implementation of the engine's op set — thin wrappers over ``_nnmpi_hip``.
+
+Every method launches hand-written CDNA4 kernels on the current HIP stream; none of them
+allocates, synchronises or falls back to PyTorch compute (so a step built from them can be
+captured into a hipGraph).  Workspaces are provided by the caller (the engine sizes them once).
+"""
+from __future__ import annotations
+
+import torch
+
+from .. import native
+from .torch_ops import ACT_CODES
+
+LOSS_CODES = {"mse": 0, "xent": 1}
+
+
+def _p(t):
+    return native.ptr(t)
+
+
+def _check(cond, msg):
+    if not cond:
+        raise ValueError(msg)
+
+
+class HipOps:
+    name = "hip"
+
+    def __init__(self, device="cuda"):
+        self.device = torch.device(device)
+        self.lib = native.lib()
+
+    @property
+    def stream(self) -> int:
+        return native.stream_handle()
+
+    # ---------------- hidden layers ----------------
+    def linear_act(self, x, W, b, act: str, out):
+        M, K = x.shape
+        N = W.shape[0]
+        if x.dtype == torch.bfloat16:
+            _check(K % 8 == 0 and N % 4 == 0, f"bf16 linear needs K%8==0, N%4==0 (K={K}, N={N})")
+            self.lib.linear_fwd_bf16(_p(x), x.stride(0), _p(W), W.stride(0), _p(b), _p(out),
+                                     out.stride(0), M, N, K, ACT_CODES[act], self.stream)
+        else:
+            self.lib.linear_fwd_f32(_p(x), x.stride(0), _p(W), W.stride(0), _p(b), _p(out),
+                                    out.stride(0), M, N, K, ACT_CODES[act], self.stream)
+
+    def linear_dgrad(self, dz, W, a_prev, act: str, out):
+        M, K = dz.shape          # K = out features of this layer
+        N = W.shape[1]           # in features
+        if dz.dtype == torch.bfloat16:
+            _check(K % 8 == 0 and N % 8 == 0, f"bf16 dgrad needs K%8==0, N%8==0 (K={K}, N={N})")
+            self.lib.linear_dgrad_bf16(_p(dz), dz.stride(0), _p(W), W.stride(0), _p(a_prev),
+                                       a_prev.stride(0), _p(out), out.stride(0), M, N, K,
+                                       ACT_CODES[act], self.stream)
+        else:
+            self.lib.linear_dgrad_f32(_p(dz), dz.stride(0), _p(W), W.stride(0), _p(a_prev),
+                                      a_prev.stride(0), _p(out), out.stride(0), M, N, K,
+                                      ACT_CODES[act], self.stream)
+
+    def wgrad_workspace_bytes(self, rows, out_f, in_f, dtype) -> int:
+        if dtype == torch.bfloat16:
+            return int(self.lib.wgrad_workspace_bytes(out_f, in_f, rows))
+        return int(self.lib.wgrad_f32_workspace_bytes(out_f, in_f, rows))
+
+    def linear_wgrad(self, dz, x, gW, gb, ws=None):
+        rows, M = dz.shape
+        N = x.shape[1]
+        if dz.dtype == torch.bfloat16:
+            _check(M % 8 == 0 and N % 8 == 0, f"bf16 wgrad needs out%8==0, in%8==0 ({M}, {N})")
+            self.lib.linear_wgrad_bf16(_p(dz), dz.stride(0), _p(x), x.stride(0), _p(gW), _p(gb),
+                                       M, N, rows, _p(ws), self.stream)
+        else:
+            self.lib.linear_wgrad_f32(_p(dz), dz.stride(0), _p(x), x.stride(0), _p(gW), _p(gb),
+                                      M, N, rows, _p(ws), self.stream)
+
+    # ---------------- head ----------------
+    def head_parts(self, rows: int) -> int:
+        return int(self.lib.head_fwd_parts(rows))
+
+    def _head_split(self, rows):
+        parts = self.head_parts(rows)
+        return parts, (parts + 3) // 4 * 4 + 4   # keep the slab region 16-byte aligned
+
+    def head_workspace_bytes(self, rows, in_f, out_f) -> int:
+        _, off = self._head_split(rows)
+        return int(self.lib.head_wgrad_workspace_bytes(rows, in_f, out_f)) + 4 * off
+
+    def head(self, a, W, b, y, labels, loss: str, inv_count: float, act_prev: str, dz_out,
+             gW, gb, dlogits, loss_out, loss_scale: float, ws=None):
+        rows, in_f = a.shape
+        out_f = W.shape[0]
+        _check(in_f % 8 == 0, f"head needs in%8==0 (in={in_f})")
+        parts, off = self._head_split(rows)
+        lp = ws[:parts]
+        wws = ws[off:]
+        a_bf16 = 1 if a.dtype == torch.bfloat16 else 0
+        self.lib.head_fwd(_p(a), a_bf16, rows, in_f, _p(W), _p(b), out_f, _p(y), _p(labels),
+                          LOSS_CODES[loss], float(inv_count), ACT_CODES[act_prev], _p(dz_out),
+                          _p(dlogits), _p(lp), self.stream)
+        self.lib.head_wgrad(_p(a), a_bf16, rows, in_f, _p(dlogits), out_f, _p(gW), _p(gb),
+                            _p(wws), _p(lp), parts, float(loss_scale), _p(loss_out), self.stream)
+
+    # ---------------- tiny fused MLP ----------------
+    def tiny_workspace_bytes(self, rows, numel) -> int:
+        return int(self.lib.tiny_mlp_workspace_bytes(rows, numel))
+
+    def tiny_step(self, spec, arena, X, y, labels, inv_count, loss_out, ws):
+        L = spec.n_layers
+        w_off = [arena.by_name[f"layers.{2 * i}.weight"].offset for i in range(L)]
+        b_off = [arena.by_name[f"layers.{2 * i}.bias"].offset for i in range(L)]
+        self.lib.tiny_mlp_step(list(spec.widths), w_off, b_off, ACT_CODES[spec.activation],
+                               LOSS_CODES[spec.loss], _p(arena.master), _p(X), _p(y), _p(labels),
+                               X.shape[0], float(inv_count), _p(arena.grad), arena.numel,
+                               _p(ws), _p(loss_out), self.stream)
+
+    # ---------------- optimizer ----------------
+    def sgd(self, arena, hp, nesterov: bool, first: bool, zero_grad: bool = True):
+        self.lib.sgd_momentum(_p(arena.master), _p(arena.grad), _p(arena.momentum),
+                              _p(arena.shadow), arena.numel, _p(hp), int(nesterov), int(first),
+                              int(zero_grad), self.stream)

@@ -1,0 +1,107 @@
+"""Gradient synchronisation strategies (the data-parallel core).
+
+The reference averages gradients by pickling every rank's gradient list to rank 0
+(``comm.gather``, ref.py:185), summing them there in rank order, dividing by P (ref.py:190-197)
+and sending the mean back with P-1 serial ``comm.send`` calls (ref.py:199, recv ref.py:203):
+2(P-1)·G bytes through the root every step, fully blocking.
+
+Here the flat gradient arena is split into contiguous buckets in backward order
+(:mod:`nnmpi_amd.engine.arena`); the engine calls :meth:`GradSync.ready` after each layer's
+weight gradient, a bucket's all-reduce (SUM) is launched as soon as its last layer is ready and
+overlaps the remaining backward, and :meth:`GradSync.finish` joins before the optimizer, which
+folds the 1/P (or per-rank weighted) scale into the SGD kernel.
+
+Implementations
+* :class:`NoSync` — world size 1.
+* :class:`TorchDistSync` — ``torch.distributed`` (gloo on CPU, nccl = RCCL on GPU), async work
+  handles per bucket.  ``mode="root"`` reproduces the reference's centralised pattern (reduce to
+  rank 0 + broadcast) for comparison.
+* :class:`NativeRcclSync` — the C++ runtime: ncclAllReduce per bucket on a dedicated HIP comm
+  stream gated by per-bucket events (capturable in the step's hipGraph).
+"""
+from __future__ import annotations
+
+from typing import List, Optional
+
+import torch
+import torch.distributed as dist
+
+
+class GradSync:
+    world = 1
+
+    def __init__(self, arena):
+        self.arena = arena
+        self._pending_layers = set()
+        self.seq = 0  # collective sequence number (for the sequence checker)
+
+    def begin(self):
+        self._done_buckets = set()
+
+    def ready(self, layer: int):
+        b = self.arena.bucket_of_layer(layer)
+        if b.index in self._done_buckets:
+            return
+        if layer == min(b.layers):
+            self._done_buckets.add(b.index)
+            self._launch(b)
+
+    def _launch(self, bucket):
+        pass
+
+    def finish(self):
+        pass
+
+
+class NoSync(GradSync):
+    world = 1
+
+
+class TorchDistSync(GradSync):
+    def __init__(self, arena, group, world: int, mode: str = "allreduce", overlap: bool = True):
+        super().__init__(arena)
+        self.group = group
+        self.world = world
+        self.mode = mode
+        self.overlap = overlap
+        self._works: List = []
+
+    def _launch(self, bucket):
+        view = self.arena.grad[bucket.offset:bucket.offset + bucket.numel]
+        self.seq += 1
+        if self.mode == "root":
+            # reference pattern: everything through rank 0 (reduce to root, then fan out)
+            dist.reduce(view, dst=0, group=self.group)
+            dist.broadcast(view, src=0, group=self.group)
+            return
+        w = dist.all_reduce(view, group=self.group, async_op=self.overlap)
+        if w is not None:
+            self._works.append(w)
+
+    def finish(self):
+        for w in self._works:
+            w.wait()
+        self._works.clear()
+
+
+class NativeRcclSync(GradSync):
+    def __init__(self, arena, native_comm, world: int, priority: int = -1):
+        super().__init__(arena)
+        from .. import native
+        self.native = native
+        self.comm = native_comm
+        self.world = world
+        self.gs = native.lib().GradSync(native_comm, len(arena.buckets), priority)
+        self._launched = False
+
+    def _launch(self, bucket):
+        view = self.arena.grad[bucket.offset:bucket.offset + bucket.numel]
+        self.seq += 1
+        self.gs.bucket_ready(bucket.index, view.data_ptr(), bucket.numel, 0,
+                             self.native.stream_handle())
+        self._launched = True
+
+    def finish(self):
+        if self._launched:
+            self.gs.join(self.native.stream_handle())
+        self._launched = False

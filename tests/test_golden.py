@@ -1,0 +1,62 @@
+"""Golden-value parity with the unmodified reference, CPU fp32 + gloo.
+
+Values were captured by running the reference under real MPICH with defaults (lr 0.001,
+momentum 0.9, 3 epochs).  The all-reduce sums in a different order than the reference's
+rank-ordered root loop, so comparisons use fp32 reorder tolerance (rtol 1e-5)."""
+import pytest
+import torch
+
+from _mp import run_ranks
+
+import nnmpi_amd
+import nnmpi_amd.engine.trainer
+from nnmpi_amd.utils.config import TrainConfig
+
+GOLDEN_LOSSES = {
+    1: [[2530.8323, 2526.6860, 2518.3696]],
+    2: [[2230.0779, 2227.2249, 2221.5249], [2835.1191, 2831.0088, 2822.7886]],
+    4: [[3436.1426, 3432.5225, 3425.3755], [1024.9196, 1023.7071, 1021.2964],
+        [5564.9150, 5559.6724, 5549.2437], [109.8141, 108.9418, 107.2274]],
+    8: [[3440.1406, 3442.4292, 3446.6699], [3444.0632, 3439.1643, 3429.6243],
+        [477.4702, 475.5150, 471.7312], [1578.2849, 1579.4331, 1581.6400],
+        [3591.8452, 3587.8357, 3580.0391], [7551.7095, 7550.1221, 7546.6318],
+        [212.0440, 210.7312, 208.1876], [7.3952, 7.4497, 7.5500]],
+}
+GOLDEN_PARAMS = {
+    1: [0.044477, 0.394547, -0.650854, -0.533515, -0.308854, 0.178998, -0.015673, 0.611135,
+        -0.047008, 0.190303, -0.512300, -0.172305, -0.616148],
+    2: [0.037285, 0.379001, -0.646043, -0.524991, -0.309168, 0.185970, -0.015641, 0.609327,
+        -0.044659, 0.152463, -0.481531, -0.181779, -0.616241],
+    4: [0.028263, 0.379533, -0.631721, -0.525592, -0.298694, 0.190994, -0.015658, 0.608145,
+        -0.037676, 0.153410, -0.447511, -0.163566, -0.616316],
+    8: [0.017505, 0.369685, -0.637966, -0.498654, -0.295752, 0.192411, -0.023648, 0.582469,
+        -0.039345, 0.129082, -0.344731, -0.159964, -0.616460],
+}
+INIT = [-0.00529, 0.37932, -0.58198, -0.52039, -0.27235, 0.18962, -0.01401, 0.56066, -0.06275,
+        0.15277, -0.17448, -0.11349, -0.55157]
+
+
+def test_reference_init_matches_golden():
+    from nnmpi_amd.models.mlp import reference_init
+    m = reference_init()
+    flat = torch.cat([p.detach().reshape(-1) for p in m.parameters()])
+    assert torch.allclose(flat, torch.tensor(INIT), atol=1e-5)
+    assert list(m.state_dict().keys()) == ["layers.0.weight", "layers.0.bias",
+                                           "layers.2.weight", "layers.2.bias"]
+
+
+def test_golden_p1_single_process():
+    res = nnmpi_amd.engine.trainer.run_worker(TrainConfig())
+    assert res.losses == pytest.approx(GOLDEN_LOSSES[1][0], rel=1e-5)
+    assert torch.allclose(res.final_params, torch.tensor(GOLDEN_PARAMS[1]), atol=2e-6)
+
+
+@pytest.mark.parametrize("world", [2, 4, 8])
+def test_golden_multirank(world):
+    out = run_ranks(TrainConfig(print_rank="none"), world)
+    for r in range(world):
+        assert out[r]["losses"] == pytest.approx(GOLDEN_LOSSES[world][r], rel=1e-5), r
+    for r in range(world):
+        assert torch.allclose(out[r]["final"], torch.tensor(GOLDEN_PARAMS[world]), atol=5e-6), r
+        # replicas stay bitwise identical
+        assert torch.equal(out[r]["final"], out[0]["final"])

@@ -1,0 +1,163 @@
+"""HIP kernel numerics vs plain-PyTorch fp32 references (run on an MI355X via gpurun).
+
+Asymmetric operands (cdna_hip_programming.md §3: a symmetric/identity operand hides a
+transposed fragment map) and shapes that are not tile multiples."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+DEV = "cuda"
+
+
+def _lib():
+    from nnmpi_amd import native
+    return native.lib()
+
+
+def _s():
+    return torch.cuda.current_stream().cuda_stream
+
+
+def _rand(*shape, dtype=torch.float32, scale=1.0, seed=0):
+    g = torch.Generator(device="cpu").manual_seed(seed)
+    return (torch.randn(*shape, generator=g) * scale).to(DEV, dtype)
+
+
+def test_library_is_gfx950():
+    assert _lib().arch().startswith("gfx950")
+
+
+@pytest.mark.parametrize("la,lb", [(0, 0), (0, 1), (1, 0), (1, 1)])
+@pytest.mark.parametrize("M,N,K", [(64, 64, 64), (264, 136, 200), (128, 512, 512), (40, 24, 8)])
+def test_gemm_layouts(la, lb, M, N, K):
+    lib = _lib()
+    A = _rand(M, K, seed=1).to(torch.bfloat16)
+    B = _rand(K, N, seed=2).to(torch.bfloat16)
+    # storage: KMAJ A = [M][K]; XMAJ A = [K][M]; KMAJ B = [N][K]; XMAJ B = [K][N]
+    As = A.contiguous() if la == 0 else A.t().contiguous()
+    Bs = B.t().contiguous() if lb == 0 else B.contiguous()
+    C = torch.zeros(M, N, device=DEV)
+    lib.gemm_bf16(As.data_ptr(), As.stride(0), la, Bs.data_ptr(), Bs.stride(0), lb, M, N, K,
+                  C.data_ptr(), N, _s())
+    ref = A.float() @ B.float()
+    torch.testing.assert_close(C, ref, rtol=1e-4, atol=1e-3)
+
+
+def test_gemm_identity_asymmetric():
+    lib = _lib()
+    M = N = K = 64
+    A = torch.eye(64, device=DEV, dtype=torch.bfloat16)
+    B = torch.arange(64 * 64, device=DEV, dtype=torch.float32).reshape(64, 64).remainder(97).to(torch.bfloat16)
+    Bs = B.t().contiguous()
+    C = torch.zeros(M, N, device=DEV)
+    lib.gemm_bf16(A.data_ptr(), 64, 0, Bs.data_ptr(), 64, 0, M, N, K, C.data_ptr(), N, _s())
+    torch.testing.assert_close(C, B.float())
+
+
+@pytest.mark.parametrize("act", ["relu", "tanh", "none"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("M,N,K", [(8192, 512, 512), (1000, 264, 136), (4097, 1024, 784)])
+def test_linear_fwd(act, dtype, M, N, K):
+    from nnmpi_amd.ops.hip_ops import HipOps
+    from nnmpi_amd.ops.torch_ops import TorchOps
+    x = _rand(M, K, seed=3).to(dtype)
+    W = _rand(N, K, seed=4, scale=0.05).to(dtype)
+    b = _rand(N, seed=5)
+    out = torch.empty(M, N, device=DEV, dtype=dtype)
+    ref = torch.empty(M, N, device=DEV, dtype=dtype)
+    HipOps().linear_act(x, W, b, act, out)
+    TorchOps(DEV).linear_act(x, W, b, act, ref)
+    tol = dict(rtol=2e-2, atol=2e-2) if dtype == torch.bfloat16 else dict(rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(out.float(), ref.float(), **tol)
+
+
+@pytest.mark.parametrize("act", ["relu", "tanh"])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("M,N,K", [(8192, 512, 512), (1000, 264, 136)])
+def test_linear_dgrad(act, dtype, M, N, K):
+    from nnmpi_amd.ops.hip_ops import HipOps
+    from nnmpi_amd.ops.torch_ops import TorchOps
+    dz = _rand(M, K, seed=6).to(dtype)
+    W = _rand(K, N, seed=7, scale=0.05).to(dtype)     # layer weight [out=K][in=N]
+    a_prev = torch.relu(_rand(M, N, seed=8)).to(dtype) if act == "relu" else torch.tanh(_rand(M, N, seed=8)).to(dtype)
+    out = torch.empty(M, N, device=DEV, dtype=dtype)
+    ref = torch.empty(M, N, device=DEV, dtype=dtype)
+    HipOps().linear_dgrad(dz, W, a_prev, act, out)
+    TorchOps(DEV).linear_dgrad(dz, W, a_prev, act, ref)
+    tol = dict(rtol=2e-2, atol=2e-2) if dtype == torch.bfloat16 else dict(rtol=1e-5, atol=1e-5)
+    torch.testing.assert_close(out.float(), ref.float(), **tol)
+
+
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("rows,out_f,in_f", [(8192, 512, 512), (8193, 512, 512), (100, 264, 136),
+                                             (4096, 1024, 784)])
+def test_linear_wgrad(dtype, rows, out_f, in_f):
+    from nnmpi_amd.ops.hip_ops import HipOps
+    ops = HipOps()
+    dz = _rand(rows, out_f, seed=9).to(dtype)
+    x = _rand(rows, in_f, seed=10).to(dtype)
+    gW = torch.full((out_f, in_f), 7.0, device=DEV)
+    gb = torch.full((out_f,), 7.0, device=DEV)
+    ws = torch.zeros(ops.wgrad_workspace_bytes(rows, out_f, in_f, dtype) // 4 + 16, device=DEV)
+    ops.linear_wgrad(dz, x, gW, gb, ws=ws)
+    refW = dz.double().t() @ x.double()
+    refb = dz.double().sum(0)
+    scale = (rows ** 0.5)
+    torch.testing.assert_close(gW.double(), refW, rtol=1e-3, atol=1e-3 * scale)
+    torch.testing.assert_close(gb.double(), refb, rtol=1e-3, atol=1e-3 * scale)
+
+
+@pytest.mark.parametrize("loss,out_f", [("mse", 1), ("mse", 3), ("xent", 10)])
+@pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
+@pytest.mark.parametrize("rows,in_f", [(8192, 512), (777, 1024), (64, 8192)])
+def test_head(loss, out_f, dtype, rows, in_f):
+    from nnmpi_amd.ops.hip_ops import HipOps
+    from nnmpi_amd.ops.torch_ops import TorchOps
+    if out_f * in_f * 4 > 65536:
+        pytest.skip("head weight larger than LDS budget")
+    ops = HipOps()
+    a = torch.relu(_rand(rows, in_f, seed=11)).to(dtype)
+    W = _rand(out_f, in_f, seed=12, scale=0.05)
+    b = _rand(out_f, seed=13)
+    y = _rand(rows, out_f, seed=14) if loss == "mse" else None
+    lab = (torch.arange(rows, device=DEV) * 7 % out_f) if loss == "xent" else None
+    res = {}
+    for name, o in (("hip", ops), ("ref", TorchOps(DEV))):
+        gW = torch.zeros(out_f, in_f, device=DEV)
+        gb = torch.zeros(out_f, device=DEV)
+        dz = torch.zeros(rows, in_f, device=DEV, dtype=dtype)
+        dl = torch.zeros(rows, out_f, device=DEV)
+        lo = torch.zeros(4, device=DEV)
+        ws = torch.zeros(ops.head_workspace_bytes(rows, in_f, out_f) // 4 + 16, device=DEV)
+        o.head(a, W, b, y, lab, loss, 1.0 / rows, "relu", dz, gW, gb, dl, lo, 1.0 / rows, ws=ws)
+        res[name] = (gW, gb, dz, lo[0])
+    tol = dict(rtol=2e-3, atol=2e-3)
+    torch.testing.assert_close(res["hip"][0], res["ref"][0], **tol)
+    torch.testing.assert_close(res["hip"][1], res["ref"][1], **tol)
+    dtol = dict(rtol=2e-2, atol=2e-3) if dtype == torch.bfloat16 else dict(rtol=1e-4, atol=1e-5)
+    torch.testing.assert_close(res["hip"][2].float(), res["ref"][2].float(), **dtol)
+    torch.testing.assert_close(res["hip"][3], res["ref"][3], rtol=1e-4, atol=1e-4)
+
+
+@pytest.mark.parametrize("first,nesterov,wd,damp", [(True, False, 0.0, 0.0), (False, False, 0.0, 0.0),
+                                                    (False, True, 1e-2, 0.0), (False, False, 1e-2, 0.3)])
+def test_sgd_matches_torch_optim(first, nesterov, wd, damp):
+    from nnmpi_amd.engine.arena import Arena
+    from nnmpi_amd.ops.hip_ops import HipOps
+    ar = Arena([(64, 200), (1, 64)], DEV, shadow_dtype=torch.bfloat16)
+    ar.master.copy_(_rand(ar.numel, seed=20))
+    ar.grad.copy_(_rand(ar.numel, seed=21))
+    ar.momentum.copy_(_rand(ar.numel, seed=22))
+    p = torch.nn.Parameter(ar.master.clone())
+    opt = torch.optim.SGD([p], lr=0.01, momentum=0.9, dampening=damp, weight_decay=wd, nesterov=nesterov)
+    if not first:
+        opt.state[p]["momentum_buffer"] = ar.momentum.clone()
+    p.grad = ar.grad.clone() * 0.5
+    opt.step()
+    hp = torch.tensor([0.01, 0.9, damp, wd, 0.5, 0, 0, 0], device=DEV)
+    HipOps().sgd(ar, hp, nesterov, first)
+    torch.testing.assert_close(ar.master, p.detach(), rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(ar.momentum, opt.state[p]["momentum_buffer"], rtol=1e-6, atol=1e-6)
+    assert torch.equal(ar.shadow, ar.master.to(torch.bfloat16))
+    assert torch.count_nonzero(ar.grad) == 0
