@@ -56,6 +56,8 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
     check(linear_dgrad_bf16(P<const bf16>(dZ), lddz, P<const bf16>(W), ldw, P<const bf16>(Ap), ldap,
                             P<bf16>(dX), lddx, M, N, K, act, S(s)), "linear_dgrad_bf16");
   });
+  m.def("set_gemm_impl", &set_gemm_impl);
+  m.def("get_gemm_impl", &get_gemm_impl);
   m.def("wgrad_workspace_bytes", &wgrad_workspace_bytes);
   m.def("wgrad_splits", &wgrad_splits);
   m.def("linear_wgrad_bf16", [](uptr dZ, int lddz, uptr X, int ldx, uptr dW, uptr db, int M, int N,

@@ -26,6 +26,7 @@
 #include "kernels.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace nnmpi {
 
@@ -48,6 +49,7 @@ struct GemmParams {
   int ldaux;
   float* bias_grad;
   long long bg_split_stride;
+  unsigned a_bytes, b_bytes;  // extents of A / B storage (buffer-resource range, DMA path)
 };
 
 // XOR swizzle of the 16-byte chunk index for XMAJ images (rows of BX bf16).
@@ -134,6 +136,86 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int xb, int kk, int
   }
 }
 
+// Epilogue shared by both main loops: lane holds C[m][n..n+3] for each (i, j) fragment.
+// All epilogue operands (bias, activation aux) are loaded up front, then every fragment is
+// finished and stored: no load waits behind the stores (stores count in vmcnt on gfx950).
+template <int BM, int BN, int EPI, int ACT, bool BIASGRAD>
+__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[BM / 32][BN / 32],
+                                              f32x4 (&accb)[BM / 32], bool do_bg, int m0, int n0,
+                                              int wm, int wn, int lane, int split) {
+  constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NJ = WN / 16;
+  int mrow[MI];
+  int ncol[NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) mrow[i] = m0 + wm * WM + i * 16 + (lane & 15);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) ncol[j] = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
+  if constexpr (EPI == EPI_BIAS_ACT) {
+    f32x4 bias[NJ];
+    // unconditional (clamped) loads: no per-element branch -> no vmcnt(0) per element
+    if (p.bias) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bias[j] = *reinterpret_cast<const f32x4*>(p.bias + min(ncol[j], p.N - 4));
+    } else {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bias[j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      if (mrow[i] >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if (ncol[j] >= p.N) continue;
+        const f32x4 v = acc[i][j] + bias[j];
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (bf16)act_fwd_t<ACT>(v[r]);
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(p.C) + (long long)mrow[i] * p.ldc + ncol[j]) = o;
+      }
+    }
+  } else if constexpr (EPI == EPI_DACT) {
+    bf16x4 aux[MI][NJ];
+#pragma unroll
+    for (int i = 0; i < MI; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        aux[i][j] = *reinterpret_cast<const bf16x4*>(p.aux + (long long)min(mrow[i], p.M - 1) * p.ldaux +
+                                                     min(ncol[j], p.N - 4));
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      if (mrow[i] >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if (ncol[j] >= p.N) continue;
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc[i][j][r] * act_bwd_t<ACT>((float)aux[i][j][r]));
+        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(p.C) + (long long)mrow[i] * p.ldc + ncol[j]) = o;
+      }
+    }
+  } else {
+    float* cbase = reinterpret_cast<float*>(p.C) + split * p.c_split_stride;
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      if (mrow[i] >= p.M) continue;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if (ncol[j] >= p.N) continue;
+        *reinterpret_cast<f32x4*>(cbase + (long long)mrow[i] * p.ldc + ncol[j]) = acc[i][j];
+      }
+    }
+  }
+  if constexpr (BIASGRAD) {
+    if (do_bg && (lane >> 4) == 0) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int m = m0 + wm * WM + i * 16 + lane;
+        if (m < p.M) p.bias_grad[split * p.bg_split_stride + m] = accb[i][0];
+      }
+    }
+  }
+}
+
 template <int BM, int BN, int LA, int LB, int EPI, int ACT, bool BIASGRAD>
 __global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
@@ -208,46 +290,166 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_kernel(GemmParams p) {
     __syncthreads();
   }
 
-  // ---- epilogue: lane holds C[m][n..n+3] for each (i, j) ----
+  gemm_epilogue<BM, BN, EPI, ACT, BIASGRAD>(p, acc, accb, do_bg, m0, n0, wm, wn, lane, split);
+}
+
+
+// ------------------------------------------------------------------------------------------
+// v2 main loop: LDS-DMA (buffer_load ... lds) into an NS-deep ring, counted vmcnt, raw barrier.
+//
+// The MLP GEMMs are short-K (K = 512..8192 per block) and, at one 256-thread block per CU, a
+// register-staged loop exposes one full memory round trip per 64-deep k-step.  Here every wave
+// DMAs its share of each stage straight into LDS (16 B per lane, no VGPR round trip) and keeps
+// NS-1 stages in flight; one counted `s_waitcnt vmcnt` + one `s_barrier` per k-step
+// (cdna_hip_programming.md §5 "Pipelining across barriers", rules 21/4(a)).  The LDS images are
+// the same XOR-swizzled images as v1; since a DMA writes lane-linearly, the swizzle is applied to
+// each lane's SOURCE address (rule 21).  Out-of-range chunks (M/N/K tails, split-K ends) get a
+// source offset past the buffer-resource range, so the hardware returns zeros.
+// ------------------------------------------------------------------------------------------
+constexpr unsigned DMA_OOB = 0x7FFFFFF0u;
+
+__device__ __forceinline__ constexpr int waitcnt_vm(int n) {
+  return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(waitcnt_vm(N)); }
+
+template <int BX, int LAYOUT>
+struct DmaPlan {
+  static constexpr int IMG = BX * GEMM_BK * 2;          // bytes per stage for this operand
+  static constexpr int NI = IMG / 1024 / 4;             // DMA instructions per wave per stage
+  static_assert(NI >= 1, "tile too small for 4 waves");
+  unsigned off[NI];   // byte offset of this lane's source chunk for k0 = 0
+  int kq[NI];         // k offset of the chunk within the tile
+  bool xv[NI];        // x in range
+  unsigned kstride;   // bytes per unit of k0
+
+  __device__ __forceinline__ void init(int w, int lane, int x0, int X, int ld) {
 #pragma unroll
-  for (int i = 0; i < MI; ++i) {
-    const int m = m0 + wm * WM + i * 16 + (lane & 15);
-    if (m >= p.M) continue;
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) {
-      const int n = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
-      if (n >= p.N) continue;
-      f32x4 v = acc[i][j];
-      if constexpr (EPI == EPI_BIAS_ACT) {
-        if (p.bias) {
-          const float4 b = *reinterpret_cast<const float4*>(p.bias + n);
-          v[0] += b.x; v[1] += b.y; v[2] += b.z; v[3] += b.w;
-        }
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16)act_fwd_t<ACT>(v[r]);
-        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(p.C) + (long long)m * p.ldc + n) = o;
-      } else if constexpr (EPI == EPI_DACT) {
-        const bf16x4 a = *reinterpret_cast<const bf16x4*>(p.aux + (long long)m * p.ldaux + n);
-        bf16x4 o;
-#pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16)(v[r] * act_bwd_t<ACT>((float)a[r]));
-        *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(p.C) + (long long)m * p.ldc + n) = o;
+    for (int q = 0; q < NI; ++q) {
+      const int o = (w * NI + q) * 1024 + lane * 16;
+      if constexpr (LAYOUT == KMAJ) {
+        const int r = o >> 7, cp = (o >> 4) & 7, c = cp ^ ((r >> 1) & 7);
+        off[q] = (unsigned)(((long long)(x0 + r) * ld + c * 8) * 2);
+        kq[q] = c * 8;
+        xv[q] = (x0 + r) < X;
       } else {
-        float* c = reinterpret_cast<float*>(p.C) + split * p.c_split_stride + (long long)m * p.ldc + n;
-        *reinterpret_cast<f32x4*>(c) = v;
+        constexpr int RB = BX * 2;
+        const int r = o / RB, cp = (o % RB) >> 4, c = cp ^ swz_x<BX>(r);
+        off[q] = (unsigned)(((long long)r * ld + x0 + c * 8) * 2);
+        kq[q] = r;
+        xv[q] = (x0 + c * 8) < X;
       }
     }
+    kstride = (LAYOUT == KMAJ) ? 2u : (unsigned)ld * 2u;
   }
-  if constexpr (BIASGRAD) {
-    if (do_bg && (lane >> 4) == 0) {
+
+  __device__ __forceinline__ void issue(__amdgpu_buffer_rsrc_t rs, char* lds_stage, int w, int k0,
+                                        int kend) const {
 #pragma unroll
-      for (int i = 0; i < MI; ++i) {
-        const int m = m0 + wm * WM + i * 16 + lane;
-        if (m < p.M) p.bias_grad[split * p.bg_split_stride + m] = accb[i][0];
-      }
+    for (int q = 0; q < NI; ++q) {
+      const unsigned v = (xv[q] && (k0 + kq[q]) < kend) ? off[q] + (unsigned)k0 * kstride : DMA_OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds(
+          rs, (__attribute__((address_space(3))) void*)(lds_stage + (w * NI + q) * 1024), 16, v, 0, 0, 0);
     }
   }
+};
+
+template <int BM, int BN, int LA, int LB, int EPI, int ACT, bool BIASGRAD, int NS>
+__global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_dma_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  constexpr int BK = GEMM_BK;
+  constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
+  constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NJ = WN / 16;
+  constexpr int PER_TILE = DmaPlan<BM, LA>::NI + DmaPlan<BN, LB>::NI;
+
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 1, wn = w & 1;
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int bid = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy);
+  const int tx = bid % gx, ty = bid / gx;
+  const int m0 = ty * BM, n0 = tx * BN;
+  const int split = blockIdx.z;
+  const int kbeg = split * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int nt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)p.b_bytes, 0x00020000);
+  DmaPlan<BM, LA> da;
+  DmaPlan<BN, LB> db;
+  da.init(w, lane, m0, p.M, p.lda);
+  db.init(w, lane, n0, p.N, p.ldb);
+
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accb[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bg = BIASGRAD && tx == 0 && wn == 0;
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.0f;
+
+  // prologue: NS-1 stages in flight
+#pragma unroll
+  for (int t = 0; t < NS - 1; ++t) {
+    if (t < nt) {
+      char* st = smem + t * STAGE;
+      da.issue(rsA, st, w, kbeg + t * BK, kend);
+      db.issue(rsB, st + A_BYTES, w, kbeg + t * BK, kend);
+    }
+  }
+  for (int t = 0; t < nt; ++t) {
+    // retire stage t: allow the (newer) stages t+1 .. min(t+NS-2, nt-1) to stay in flight
+    const int newer = min(NS - 2, nt - 1 - t);
+    if constexpr (NS >= 4) {
+      if (newer >= 2) wait_vm<2 * PER_TILE>();
+      else if (newer == 1) wait_vm<PER_TILE>();
+      else wait_vm<0>();
+    } else if constexpr (NS == 3) {
+      if (newer >= 1) wait_vm<PER_TILE>();
+      else wait_vm<0>();
+    } else {
+      wait_vm<0>();
+    }
+    __builtin_amdgcn_s_barrier();
+    // refill the stage consumed in iteration t-1 (all waves are past its reads)
+    if (t + NS - 1 < nt) {
+      char* st = smem + ((t + NS - 1) % NS) * STAGE;
+      da.issue(rsA, st, w, kbeg + (t + NS - 1) * BK, kend);
+      db.issue(rsB, st + A_BYTES, w, kbeg + (t + NS - 1) * BK, kend);
+    }
+    const char* cur = smem + (t % NS) * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 af[MI], bfr[NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) af[i] = read_frag<BM, LA>(cur, wm * WM + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bfr[j] = read_frag<BN, LB>(cur + A_BYTES, wn * WN + j * 16, kk, lane);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      if constexpr (BIASGRAD) {
+        if (do_bg) {
+#pragma unroll
+          for (int i = 0; i < MI; ++i)
+            accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[i], accb[i], 0, 0, 0);
+        }
+      }
+    }
+    // all of this wave's LDS reads of stage t are consumed before the next barrier
+    asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  gemm_epilogue<BM, BN, EPI, ACT, BIASGRAD>(p, acc, accb, do_bg, m0, n0, wm, wn, lane, split);
 }
 
 // Deterministic split-K combine: out[m][n] = sum_{s=0..S-1} ws[s][m][n] (fixed order), plus the
@@ -273,18 +475,63 @@ __global__ void __launch_bounds__(256) splitk_reduce_kernel(
       bout[m] = s;
     }
   }
-  if (loss_out != nullptr && blockIdx.x == 0 && threadIdx.x == 0) {
+  if (loss_out != nullptr && blockIdx.x == 0) {
+    // parallel, order-fixed reduction of the loss partials (strided per-thread sums, then a
+    // fixed LDS tree): deterministic for a given n_loss_part
+    __shared__ float red[256];
     float s = 0.f;
-    for (int i = 0; i < n_loss_part; ++i) s += loss_part[i];
-    *loss_out = s * loss_scale;
+    for (int i = threadIdx.x; i < n_loss_part; i += blockDim.x) s += loss_part[i];
+    red[threadIdx.x] = s;
+    __syncthreads();
+    for (int o = 128; o > 0; o >>= 1) {
+      if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+      __syncthreads();
+    }
+    if (threadIdx.x == 0) *loss_out = red[0] * loss_scale;
   }
 }
 
 // ------------------------------------------------------------------------------------------
 // host launchers
 // ------------------------------------------------------------------------------------------
+static int g_gemm_impl = -1;
+
+static int gemm_impl() {
+  if (g_gemm_impl < 0) {
+    const char* e = getenv("NNMPI_GEMM");
+    g_gemm_impl = (e && e[0] == '1') ? 1 : 2;   // 2 = LDS-DMA ring (default), 1 = register-staged
+  }
+  return g_gemm_impl;
+}
+
+void set_gemm_impl(int impl) { g_gemm_impl = impl; }
+int get_gemm_impl() { return gemm_impl(); }
+
+template <int LA, int LB>
+static void set_extents(GemmParams& p) {
+  // storage extents (bytes) of the operands, for the buffer-resource range checks
+  const long long a = (LA == KMAJ) ? ((long long)(p.M - 1) * p.lda + p.K) : ((long long)(p.K - 1) * p.lda + p.M);
+  const long long b = (LB == KMAJ) ? ((long long)(p.N - 1) * p.ldb + p.K) : ((long long)(p.K - 1) * p.ldb + p.N);
+  p.a_bytes = (unsigned)std::min<long long>(a * 2, DMA_OOB - 16);
+  p.b_bytes = (unsigned)std::min<long long>(b * 2, DMA_OOB - 16);
+}
+
 template <int BM, int BN, int LA, int LB, int EPI, int ACT, bool BG>
-static hipError_t launch_t(const GemmParams& p, int splits, hipStream_t s) {
+static hipError_t launch_t(GemmParams p, int splits, hipStream_t s) {
+  dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, splits);
+  if (gemm_impl() == 2) {
+    constexpr int NS = 4;
+    constexpr int smem = NS * (BM + BN) * GEMM_BK * 2;
+    set_extents<LA, LB>(p);
+    auto kfn = gemm_bf16_dma_kernel<BM, BN, LA, LB, EPI, ACT, BG, NS>;
+    static bool attr = false;
+    if (!attr) {
+      hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+      attr = true;
+    }
+    hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), smem, s, p);
+    return hipGetLastError();
+  }
   constexpr int smem = 2 * (BM + BN) * GEMM_BK * 2;
   auto kfn = gemm_bf16_kernel<BM, BN, LA, LB, EPI, ACT, BG>;
   static bool attr = false;
@@ -292,7 +539,6 @@ static hipError_t launch_t(const GemmParams& p, int splits, hipStream_t s) {
     hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
-  dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, splits);
   hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), smem, s, p);
   return hipGetLastError();
 }

@@ -19,6 +19,8 @@ hipError_t linear_dgrad_bf16(const bf16* dZ, int lddz, const bf16* W, int ldw, c
                              int lda_prev, bf16* dX, int lddx, int M, int N, int K, int act,
                              hipStream_t s);
 int wgrad_splits(int M, int N, int K);
+void set_gemm_impl(int impl);  // 1 = register-staged main loop, 2 = LDS-DMA ring
+int get_gemm_impl();
 size_t wgrad_workspace_bytes(int M, int N, int K);
 hipError_t linear_wgrad_bf16(const bf16* dZ, int lddz, const bf16* X, int ldx, float* dW,
                              float* db, int M, int N, int K, float* ws, hipStream_t s);

@@ -137,6 +137,7 @@ __global__ void __launch_bounds__(256) tiny_mlp_kernel(TinyMLPDesc d, const floa
   for (int i = tid; i < numel; i += 256) {
     dst[i] = ((wsum[i] + wsum[numel + i]) + wsum[2 * numel + i]) + wsum[3 * numel + i];
   }
+  wave_loss = wave_sum(wave_loss);  // lanes own different rows here
   if (lane == 0) red[w] = wave_loss;
   __syncthreads();
   if (tid == 0) loss_part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];

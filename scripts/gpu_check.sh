@@ -1,0 +1,52 @@
+#!/bin/bash
+# One GPU-box session: smoke -> GPU tests -> 1-GPU bench -> rocprofv3 kernel stats.
+# Each GPU step has its own time limit; a crash/timeout (rc not in {0,1}) ends the script.
+# Usage: scripts/gpu_check.sh [steps...]   (default: smoke tests bench prof)
+cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
+export TMPDIR=/tmp
+mkdir -p gpurun_out
+STEPS="${*:-smoke tests bench prof}"
+
+ok_or_stop() {  # $1 = rc, $2 = name
+  if [ "$1" -ne 0 ] && [ "$1" -ne 1 ]; then
+    echo "[gpu_check] $2 ended with rc=$1 -> stopping" | tee -a gpurun_out/summary.txt
+    exit "$1"
+  fi
+  echo "[gpu_check] $2 rc=$1" | tee -a gpurun_out/summary.txt
+}
+
+for s in $STEPS; do
+  case "$s" in
+    smoke)
+      timeout -k 10 400 python -c "import __graft_entry__ as g; g.build(); g.smoke()" > gpurun_out/smoke.log 2>&1
+      ok_or_stop $? smoke ;;
+    tests)
+      timeout -k 10 900 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1
+      ok_or_stop $? tests ;;
+    testsall)
+      timeout -k 10 900 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1
+      ok_or_stop $? testsall ;;
+    gemm)
+      timeout -k 10 300 python scripts/gemm_bench.py > gpurun_out/gemm_bench.json 2> gpurun_out/gemm_bench.err
+      ok_or_stop $? gemm
+      timeout -k 10 300 python scripts/gemm_bench.py --inf 8192 --outf 8192 --rows 4096 --rounds 3 --iters 5 >> gpurun_out/gemm_bench.json 2>> gpurun_out/gemm_bench.err
+      ok_or_stop $? gemm8k
+      cat gpurun_out/gemm_bench.json ;;
+    bench)
+      timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
+      ok_or_stop $? bench
+      cat gpurun_out/bench.json ;;
+    benchall)
+      for c in proxy512 mnist wide8192 ref; do
+        timeout -k 10 300 python bench.py --config $c --steps 50 --warmup 5 >> gpurun_out/bench_all.json 2>> gpurun_out/bench_all.err
+        ok_or_stop $? "bench $c"
+      done
+      cat gpurun_out/bench_all.json ;;
+    prof)
+      rm -rf gpurun_out/prof
+      timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 50 --warmup 5 > gpurun_out/prof.log 2>&1
+      ok_or_stop $? prof
+      find gpurun_out/prof -name "*kernel_stats.csv" -exec cp {} gpurun_out/kernel_stats.csv \; ;;
+  esac
+done
+echo "[gpu_check] done" | tee -a gpurun_out/summary.txt
