@@ -50,9 +50,11 @@ def parse():
     p.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     p.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     p.add_argument("--comm", choices=["native", "torch"], default="native")
-    p.add_argument("--bucket_mb", type=float, default=25.0)
+    p.add_argument("--bucket_mb", type=float, default=1.0)
     p.add_argument("--no_graph", action="store_true")
+    p.add_argument("--no_overlap", action="store_true")
     p.add_argument("--even", action="store_true", help="no uneven extra rows")
+    p.add_argument("--lr", type=float, default=1e-5)
     return p.parse_args()
 
 
@@ -124,7 +126,8 @@ def main():
         sync = NoSync(arena)
     ops = HipOps(dev)
     eng = MLPEngine(spec, arena, ops, sync, device=dev, dtype=dtype, rows_capacity=rows,
-                    lr=1e-3, momentum=0.9, use_graph=not a.no_graph)
+                    lr=a.lr, momentum=0.9, use_graph=not a.no_graph,
+                    overlap=not a.no_overlap)
     eng.load_batch(X.to(dtype), Y, labels)
     del X
     cfg = TrainConfig(widths=list(widths), loss=c["loss"], n_features=widths[0])
@@ -138,6 +141,7 @@ def main():
 
     for _ in range(a.warmup):
         eng.step()
+    loss0 = eng.loss()
     barrier()
     t0 = time.perf_counter()
     for _ in range(a.steps):
@@ -174,8 +178,10 @@ def main():
             "config": {"model": c["model"], "global_batch": samples, "seq_len": None,
                        "parallelism": f"dp{world}", "rows_per_gpu": rows_pg,
                        "uneven_split": (not a.even and world > 1), "comm": a.comm if world > 1 else "none",
-                       "graph": not a.no_graph},
+                       "graph": not a.no_graph, "overlap": not a.no_overlap,
+                       "bucket_mb": a.bucket_mb},
             "model_tflops_per_s": round(tflops, 2),
+            "loss_after_warmup": loss0,
             "final_loss": loss,
         }
         print(json.dumps(out), flush=True)

@@ -8,6 +8,7 @@
 #include <string>
 
 #include "comm/rccl_comm.h"
+#include "kernels/common.h"
 #include "kernels/kernels.h"
 
 namespace py = pybind11;
@@ -22,6 +23,21 @@ static void check(hipError_t e, const char* what) {
 template <typename T>
 static T* P(uptr p) { return reinterpret_cast<T*>(p); }
 static hipStream_t S(uptr s) { return reinterpret_cast<hipStream_t>(s); }
+
+// (g_base, p_base, m_base, s_base, hp, nesterov, first) -> SgdFuse, or none
+static bool to_sgd(const py::object& o, SgdFuse& f) {
+  if (o.is_none()) return false;
+  auto t = o.cast<py::tuple>();
+  if (t.size() != 7) throw std::runtime_error("sgd fusion tuple needs 7 entries");
+  f.g_base = P<const float>(t[0].cast<uptr>());
+  f.p_base = P<float>(t[1].cast<uptr>());
+  f.m_base = P<float>(t[2].cast<uptr>());
+  f.s_base = P<bf16>(t[3].cast<uptr>());
+  f.hp = P<const float>(t[4].cast<uptr>());
+  f.nesterov = t[5].cast<int>();
+  f.first = t[6].cast<int>();
+  return true;
+}
 
 PYBIND11_MODULE(_nnmpi_hip, m) {
   m.doc() = "MI355X-native kernels and RCCL runtime for nnmpi_amd";
@@ -58,13 +74,18 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
   });
   m.def("set_gemm_impl", &set_gemm_impl);
   m.def("get_gemm_impl", &get_gemm_impl);
+  m.def("set_gemm_tile", &set_gemm_tile);
+  m.def("set_gemm_variant", &set_gemm_variant);
   m.def("wgrad_workspace_bytes", &wgrad_workspace_bytes);
   m.def("wgrad_splits", &wgrad_splits);
   m.def("linear_wgrad_bf16", [](uptr dZ, int lddz, uptr X, int ldx, uptr dW, uptr db, int M, int N,
-                                int K, uptr ws, uptr s) {
+                                int K, uptr ws, uptr s, py::object sgd) {
+    SgdFuse f{};
+    const bool fu = to_sgd(sgd, f);
     check(linear_wgrad_bf16(P<const bf16>(dZ), lddz, P<const bf16>(X), ldx, P<float>(dW), P<float>(db),
-                            M, N, K, P<float>(ws), S(s)), "linear_wgrad_bf16");
-  });
+                            M, N, K, P<float>(ws), S(s), fu ? &f : nullptr), "linear_wgrad_bf16");
+  }, py::arg("dZ"), py::arg("lddz"), py::arg("X"), py::arg("ldx"), py::arg("dW"), py::arg("db"),
+     py::arg("M"), py::arg("N"), py::arg("K"), py::arg("ws"), py::arg("s"), py::arg("sgd") = py::none());
   m.def("gemm_bf16", [](uptr A, int lda, int la, uptr B, int ldb, int lb, int M, int N, int K, uptr C,
                         int ldc, uptr s) {
     check(gemm_bf16_generic(P<const bf16>(A), lda, la, P<const bf16>(B), ldb, lb, M, N, K, P<float>(C),
@@ -103,6 +124,22 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
                    P<const float>(y), P<const int64_t>(labels), loss, inv_count, act_prev, P<void>(dz),
                    P<float>(dl), P<float>(lp), S(s)), "head_fwd");
   });
+  m.def("head_can_fuse", &head_can_fuse);
+  m.def("head_fused_workspace_bytes", &head_fused_workspace_bytes);
+  m.def("head_fused", [](uptr a, int a_bf16, int rows, int in, uptr W, uptr b, uptr y, float inv_count,
+                         int act_prev, uptr dz, uptr gW, uptr gb, uptr ws, uptr lp, float lscale,
+                         uptr lout, uptr s, py::object sgd) {
+    SgdFuse f{};
+    const bool fu = to_sgd(sgd, f);
+    check(head_fused(P<const void>(a), a_bf16, rows, in, P<const float>(W), P<const float>(b),
+                     P<const float>(y), inv_count, act_prev, P<void>(dz), P<float>(gW), P<float>(gb),
+                     P<float>(ws), P<float>(lp), lscale, P<float>(lout), S(s), fu ? &f : nullptr),
+          "head_fused");
+  }, py::arg("a"), py::arg("a_bf16"), py::arg("rows"), py::arg("in"), py::arg("W"), py::arg("b"),
+     py::arg("y"), py::arg("inv_count"), py::arg("act_prev"), py::arg("dz"), py::arg("gW"),
+     py::arg("gb"), py::arg("ws"), py::arg("lp"), py::arg("lscale"), py::arg("lout"), py::arg("s"),
+     py::arg("sgd") = py::none());
+  m.def("wgrad_will_split", [](int M, int N, int K) { return wgrad_splits(M, N, K) > 1; });
   m.def("head_wgrad_workspace_bytes", &head_wgrad_workspace_bytes);
   m.def("head_wgrad", [](uptr a, int a_bf16, int rows, int in, uptr dl, int out, uptr gW, uptr gb,
                          uptr ws, uptr lp, int nlp, float lscale, uptr lout, uptr s) {

@@ -64,4 +64,64 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
+// Optional optimizer fusion for kernels that produce final (already reduced) gradients: the
+// parameter / momentum / bf16-shadow arrays share the gradient arena's layout, so an element's
+// position is found from its offset to g_base.  g_base == nullptr disables the fusion.
+struct SgdFuse {
+  const float* g_base;
+  float* p_base;
+  float* m_base;
+  bf16* s_base;
+  const float* hp;   // {lr, momentum, dampening, weight_decay, grad_scale}
+  int nesterov;
+  int first;
+};
+
+// torch.optim.SGD update of one element (sgd.py semantics; dampening/nesterov/weight decay).
+// Contraction is pinned (explicit fmaf, no compiler contraction) so every kernel that applies
+// the update -- the standalone optimizer pass or a fused reducer epilogue -- rounds identically.
+__device__ __forceinline__ float sgd_elem(float p, float g, float& buf, float lr, float mom,
+                                          float damp, float wd, float gs, bool nesterov,
+                                          bool first) {
+#pragma clang fp contract(off)
+  float d = g * gs;
+  if (wd != 0.f) d = fmaf(wd, p, d);
+  if (mom != 0.f) {
+    buf = first ? d : fmaf(mom, buf, (1.f - damp) * d);
+    d = nesterov ? fmaf(mom, buf, d) : buf;
+  }
+  return fmaf(-lr, d, p);
+}
+
+__device__ __forceinline__ void sgd_fused_store(const SgdFuse& f, const float* gaddr, float g) {
+  const long long off = gaddr - f.g_base;
+  float buf = f.m_base[off];
+  const float pn = sgd_elem(f.p_base[off], g, buf, f.hp[0], f.hp[1], f.hp[2], f.hp[3], f.hp[4],
+                            f.nesterov != 0, f.first != 0);
+  f.p_base[off] = pn;
+  if (f.hp[1] != 0.f) f.m_base[off] = buf;
+  if (f.s_base) f.s_base[off] = (bf16)pn;
+}
+
+__device__ __forceinline__ void sgd_fused_store4(const SgdFuse& f, const float* gaddr, f32x4 g) {
+  const long long off = gaddr - f.g_base;
+  f32x4 p = *reinterpret_cast<const f32x4*>(f.p_base + off);
+  f32x4 b = *reinterpret_cast<const f32x4*>(f.m_base + off);
+  const float lr = f.hp[0], mom = f.hp[1], damp = f.hp[2], wd = f.hp[3], gs = f.hp[4];
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float bb = b[r];
+    p[r] = sgd_elem(p[r], g[r], bb, lr, mom, damp, wd, gs, f.nesterov != 0, f.first != 0);
+    b[r] = bb;
+  }
+  *reinterpret_cast<f32x4*>(f.p_base + off) = p;
+  if (mom != 0.f) *reinterpret_cast<f32x4*>(f.m_base + off) = b;
+  if (f.s_base) {
+    bf16x4 sv;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sv[r] = (bf16)p[r];
+    *reinterpret_cast<bf16x4*>(f.s_base + off) = sv;
+  }
+}
+
 }  // namespace nnmpi

@@ -139,11 +139,12 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int xb, int kk, int
 // Epilogue shared by both main loops: lane holds C[m][n..n+3] for each (i, j) fragment.
 // All epilogue operands (bias, activation aux) are loaded up front, then every fragment is
 // finished and stored: no load waits behind the stores (stores count in vmcnt on gfx950).
-template <int BM, int BN, int EPI, int ACT, bool BIASGRAD>
-__device__ __forceinline__ void gemm_epilogue(const GemmParams& p, f32x4 (&acc)[BM / 32][BN / 32],
-                                              f32x4 (&accb)[BM / 32], bool do_bg, int m0, int n0,
+template <int BM, int BN, int WGM, int WGN, int EPI, int ACT, bool BIASGRAD>
+__device__ __forceinline__ void gemm_epilogue(const GemmParams& p,
+                                              f32x4 (&acc)[BM / WGM / 16][BN / WGN / 16],
+                                              f32x4 (&accb)[BM / WGM / 16], bool do_bg, int m0, int n0,
                                               int wm, int wn, int lane, int split) {
-  constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NJ = WN / 16;
+  constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 16, NJ = WN / 16;
   int mrow[MI];
   int ncol[NJ];
 #pragma unroll
@@ -290,7 +291,7 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_kernel(GemmParams p) {
     __syncthreads();
   }
 
-  gemm_epilogue<BM, BN, EPI, ACT, BIASGRAD>(p, acc, accb, do_bg, m0, n0, wm, wn, lane, split);
+  gemm_epilogue<BM, BN, 2, 2, EPI, ACT, BIASGRAD>(p, acc, accb, do_bg, m0, n0, wm, wn, lane, split);
 }
 
 
@@ -315,11 +316,11 @@ __device__ __forceinline__ constexpr int waitcnt_vm(int n) {
 template <int N>
 __device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(waitcnt_vm(N)); }
 
-template <int BX, int LAYOUT>
+template <int BX, int LAYOUT, int NW>
 struct DmaPlan {
   static constexpr int IMG = BX * GEMM_BK * 2;          // bytes per stage for this operand
-  static constexpr int NI = IMG / 1024 / 4;             // DMA instructions per wave per stage
-  static_assert(NI >= 1, "tile too small for 4 waves");
+  static constexpr int NI = IMG / 1024 / NW;            // DMA instructions per wave per stage
+  static_assert(NI >= 1 && NI * NW * 1024 == IMG, "operand stage must split evenly over the waves");
   unsigned off[NI];   // byte offset of this lane's source chunk for k0 = 0
   int kq[NI];         // k offset of the chunk within the tile
   bool xv[NI];        // x in range
@@ -356,17 +357,18 @@ struct DmaPlan {
   }
 };
 
-template <int BM, int BN, int LA, int LB, int EPI, int ACT, bool BIASGRAD, int NS>
-__global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_dma_kernel(GemmParams p) {
+template <int BM, int BN, int WGM, int WGN, int LA, int LB, int EPI, int ACT, bool BIASGRAD, int NS>
+__global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_dma_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
+  constexpr int NW = WGM * WGN;
   constexpr int BK = GEMM_BK;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
-  constexpr int WM = BM / 2, WN = BN / 2, MI = WM / 16, NJ = WN / 16;
-  constexpr int PER_TILE = DmaPlan<BM, LA>::NI + DmaPlan<BN, LB>::NI;
+  constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 16, NJ = WN / 16;
+  constexpr int PER_TILE = DmaPlan<BM, LA, NW>::NI + DmaPlan<BN, LB, NW>::NI;
 
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int wm = w >> 1, wn = w & 1;
+  const int wm = w / WGN, wn = w % WGN;
   const int gx = gridDim.x, gy = gridDim.y;
   const int bid = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy);
   const int tx = bid % gx, ty = bid / gx;
@@ -378,8 +380,8 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_dma_kernel(GemmParams 
 
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)p.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)p.b_bytes, 0x00020000);
-  DmaPlan<BM, LA> da;
-  DmaPlan<BN, LB> db;
+  DmaPlan<BM, LA, NW> da;
+  DmaPlan<BN, LB, NW> db;
   da.init(w, lane, m0, p.M, p.lda);
   db.init(w, lane, n0, p.N, p.ldb);
 
@@ -449,45 +451,76 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_dma_kernel(GemmParams 
     // all of this wave's LDS reads of stage t are consumed before the next barrier
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
-  gemm_epilogue<BM, BN, EPI, ACT, BIASGRAD>(p, acc, accb, do_bg, m0, n0, wm, wn, lane, split);
+  gemm_epilogue<BM, BN, WGM, WGN, EPI, ACT, BIASGRAD>(p, acc, accb, do_bg, m0, n0, wm, wn, lane, split);
 }
 
-// Deterministic split-K combine: out[m][n] = sum_{s=0..S-1} ws[s][m][n] (fixed order), plus the
-// matching bias-grad rows and an optional loss reduction (sum of partials / count).
-__global__ void __launch_bounds__(256) splitk_reduce_kernel(
+// Deterministic split-K / partial-slab combine, one launch for the three jobs a backward needs:
+//   blocks [0, nb_main)         out[m][n] = sum_z ws[z][m][n]     (64 float4 columns per block)
+//   blocks [nb_main, +nb_bias)  bout[m]   = sum_z bws[z][m]       (64 scalars per block)
+//   one more block (optional)   *loss_out = loss_scale * sum_i loss_part[i]
+// WS waves per block split the S partials (wave w sums z = w, w+WS, ... in order) and the wave
+// partials are combined in wave order through LDS: bitwise reproducible for a given (S, WS).
+template <int WS>
+__global__ void __launch_bounds__(64 * WS) slab_reduce_kernel(
     const float* __restrict__ ws, int S, long long stride, int M, int N, float* __restrict__ out,
-    int ldo, const float* __restrict__ bws, long long bstride, float* __restrict__ bout,
-    const float* __restrict__ loss_part, int n_loss_part, float loss_scale, float* __restrict__ loss_out) {
-  const long long nvec = (long long)M * (N / 4);
-  const long long gtid = (long long)blockIdx.x * blockDim.x + threadIdx.x;
-  const long long gsz = (long long)gridDim.x * blockDim.x;
-  for (long long v = gtid; v < nvec; v += gsz) {
-    const int m = (int)(v / (N / 4));
-    const int n = (int)(v % (N / 4)) * 4;
-    f32x4 s = {0.f, 0.f, 0.f, 0.f};
-    for (int z = 0; z < S; ++z) s += *reinterpret_cast<const f32x4*>(ws + z * stride + (long long)m * N + n);
-    *reinterpret_cast<f32x4*>(out + (long long)m * ldo + n) = s;
-  }
-  if (bws != nullptr) {
-    for (long long m = gtid; m < M; m += gsz) {
-      float s = 0.f;
-      for (int z = 0; z < S; ++z) s += bws[z * bstride + m];
-      bout[m] = s;
+    int ldo, int nb_main, const float* __restrict__ bws, long long bstride, float* __restrict__ bout,
+    int nb_bias, const float* __restrict__ loss_part, int n_loss_part, float loss_scale,
+    float* __restrict__ loss_out, SgdFuse sg) {
+  __shared__ f32x4 part[WS][64];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  const int b = blockIdx.x;
+  if (b < nb_main) {
+    const int nv = N >> 2;
+    const long long nvec = (long long)M * nv;
+    const long long v = (long long)b * 64 + lane;
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    long long m = 0, n = 0;
+    if (v < nvec) {
+      m = v / nv;
+      n = (v % nv) * 4;
+      const float* p = ws + m * N + n;
+#pragma unroll 4
+      for (int z = w; z < S; z += WS) acc += *reinterpret_cast<const f32x4*>(p + z * stride);
     }
-  }
-  if (loss_out != nullptr && blockIdx.x == 0) {
-    // parallel, order-fixed reduction of the loss partials (strided per-thread sums, then a
-    // fixed LDS tree): deterministic for a given n_loss_part
-    __shared__ float red[256];
-    float s = 0.f;
-    for (int i = threadIdx.x; i < n_loss_part; i += blockDim.x) s += loss_part[i];
-    red[threadIdx.x] = s;
+    part[w][lane] = acc;
     __syncthreads();
-    for (int o = 128; o > 0; o >>= 1) {
-      if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
-      __syncthreads();
+    if (w == 0 && v < nvec) {
+      f32x4 t = part[0][lane];
+#pragma unroll
+      for (int k = 1; k < WS; ++k) t += part[k][lane];
+      if (sg.g_base) sgd_fused_store4(sg, out + m * ldo + n, t);
+      else *reinterpret_cast<f32x4*>(out + m * ldo + n) = t;
     }
-    if (threadIdx.x == 0) *loss_out = red[0] * loss_scale;
+    return;
+  }
+  if (b < nb_main + nb_bias) {
+    const long long m = (long long)(b - nb_main) * 64 + lane;
+    float acc = 0.f;
+    if (m < M) {
+#pragma unroll 4
+      for (int z = w; z < S; z += WS) acc += bws[z * bstride + m];
+    }
+    part[w][lane][0] = acc;
+    __syncthreads();
+    if (w == 0 && m < M) {
+      float t = part[0][lane][0];
+#pragma unroll
+      for (int k = 1; k < WS; ++k) t += part[k][lane][0];
+      if (sg.g_base) sgd_fused_store(sg, bout + m, t);
+      else bout[m] = t;
+    }
+    return;
+  }
+  // loss partials: strided per-thread sums, then a fixed-order combine
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < n_loss_part; i += 64 * WS) acc += loss_part[i];
+  acc = wave_sum(acc);
+  if (lane == 0) part[w][0][0] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int k = 0; k < WS; ++k) t += part[k][0][0];
+    *loss_out = t * loss_scale;
   }
 }
 
@@ -516,27 +549,50 @@ static void set_extents(GemmParams& p) {
   p.b_bytes = (unsigned)std::min<long long>(b * 2, DMA_OOB - 16);
 }
 
+template <int BM, int BN, int WGM, int WGN, int NS, int LA, int LB, int EPI, int ACT, bool BG>
+static hipError_t launch_dma(GemmParams p, int splits, hipStream_t s) {
+  dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, splits);
+  constexpr int smem = NS * (BM + BN) * GEMM_BK * 2;
+  set_extents<LA, LB>(p);
+  auto kfn = gemm_bf16_dma_kernel<BM, BN, WGM, WGN, LA, LB, EPI, ACT, BG, NS>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr = true;
+  }
+  hipLaunchKernelGGL(kfn, grid, dim3(64 * WGM * WGN), smem, s, p);
+  return hipGetLastError();
+}
+
+// DMA-path variants (experiments select one with set_gemm_variant; 0 = default).
+static int g_variant = 0;
+void set_gemm_variant(int v) { g_variant = v; }
+
 template <int BM, int BN, int LA, int LB, int EPI, int ACT, bool BG>
 static hipError_t launch_t(GemmParams p, int splits, hipStream_t s) {
-  dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, splits);
   if (gemm_impl() == 2) {
-    constexpr int NS = 4;
-    constexpr int smem = NS * (BM + BN) * GEMM_BK * 2;
-    set_extents<LA, LB>(p);
-    auto kfn = gemm_bf16_dma_kernel<BM, BN, LA, LB, EPI, ACT, BG, NS>;
-    static bool attr = false;
-    if (!attr) {
-      hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-      attr = true;
+    if constexpr (BM == 128 && BN == 128) {
+      switch (g_variant) {
+        case 1: return launch_dma<128, 128, 2, 2, 3, LA, LB, EPI, ACT, BG>(p, splits, s);
+        case 2: return launch_dma<128, 128, 2, 4, 4, LA, LB, EPI, ACT, BG>(p, splits, s);
+        case 3: return launch_dma<128, 128, 4, 2, 4, LA, LB, EPI, ACT, BG>(p, splits, s);
+        case 4: return launch_dma<128, 128, 2, 4, 2, LA, LB, EPI, ACT, BG>(p, splits, s);
+        case 5: return launch_dma<64, 128, 2, 2, 3, LA, LB, EPI, ACT, BG>(p, splits, s);  // 2 blocks/CU
+        case 6: return launch_dma<128, 64, 2, 2, 3, LA, LB, EPI, ACT, BG>(p, splits, s);
+        case 7: return launch_dma<64, 128, 2, 4, 3, LA, LB, EPI, ACT, BG>(p, splits, s);
+        case 8: return launch_dma<128, 128, 2, 2, 4, LA, LB, EPI, ACT, BG>(p, splits, s);
+        default: return launch_dma<128, 128, 2, 4, 2, LA, LB, EPI, ACT, BG>(p, splits, s);  // = variant 4
+      }
+    } else {
+      return launch_dma<BM, BN, 2, 2, 4, LA, LB, EPI, ACT, BG>(p, splits, s);
     }
-    hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), smem, s, p);
-    return hipGetLastError();
   }
+  dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, splits);
   constexpr int smem = 2 * (BM + BN) * GEMM_BK * 2;
   auto kfn = gemm_bf16_kernel<BM, BN, LA, LB, EPI, ACT, BG>;
   static bool attr = false;
   if (!attr) {
-    hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr = true;
   }
   hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), smem, s, p);
@@ -552,7 +608,11 @@ static hipError_t launch_act(const GemmParams& p, int act, int splits, hipStream
   }
 }
 
+static int g_force_tile = 0;  // 0 = heuristic; 64 / 128 force a tile edge (experiments)
+void set_gemm_tile(int t) { g_force_tile = t; }
+
 static int pick_tile(int M, int N) {
+  if (g_force_tile) return g_force_tile;
   // 128x128 when that already yields ~a full wave of blocks, else 64x64.
   const long long t128 = (long long)((M + 127) / 128) * ((N + 127) / 128);
   return t128 >= 192 ? 128 : 64;
@@ -579,11 +639,18 @@ hipError_t linear_dgrad_bf16(const bf16* dZ, int lddz, const bf16* W, int ldw, c
   return launch_act<64, 64, KMAJ, XMAJ, EPI_DACT, false>(p, act, 1, s);
 }
 
+static int wgrad_tile(int M, int N) {
+  if (g_force_tile) return g_force_tile;
+  return (M >= 128 && N >= 128) ? 128 : 64;
+}
+
 int wgrad_splits(int M, int N, int K) {
-  const int tiles = ((M + 63) / 64) * ((N + 63) / 64);
-  int s = 1;
+  // split the (long) batch reduction until ~one block per CU; keep >= 4 k-steps per split
+  const int t = wgrad_tile(M, N);
+  const int tiles = ((M + t - 1) / t) * ((N + t - 1) / t);
   const int ksteps = (K + GEMM_BK - 1) / GEMM_BK;
-  while (tiles * s < 256 && s * 2 <= ksteps && s < 64) s *= 2;
+  int s = 1;
+  while (tiles * s < 256 && ksteps / (s * 2) >= 4 && s < 64) s *= 2;
   return s;
 }
 
@@ -594,33 +661,33 @@ size_t wgrad_workspace_bytes(int M, int N, int K) {
 }
 
 hipError_t linear_wgrad_bf16(const bf16* dZ, int lddz, const bf16* X, int ldx, float* dW,
-                             float* db, int M, int N, int K, float* ws, hipStream_t s) {
+                             float* db, int M, int N, int K, float* ws, hipStream_t s,
+                             const SgdFuse* sgd) {
   // dW[M=out][N=in] = sum_k dZ[k][m] X[k][n]; db[m] = sum_k dZ[k][m].
   const int splits = wgrad_splits(M, N, K);
   const int ksteps = (K + GEMM_BK - 1) / GEMM_BK;
+  const bool big = wgrad_tile(M, N) == 128;
   GemmParams p{};
   p.A = dZ; p.lda = lddz; p.B = X; p.ldb = ldx; p.M = M; p.N = N; p.K = K;
   p.k_per_split = ((ksteps + splits - 1) / splits) * GEMM_BK;
+  float* bws = nullptr;
   if (splits == 1) {
     p.C = dW; p.ldc = N; p.c_split_stride = 0;
     p.bias_grad = db; p.bg_split_stride = 0;
-    if (db) return launch_t<64, 64, XMAJ, XMAJ, EPI_F32, ACT_NONE, true>(p, 1, s);
-    return launch_t<64, 64, XMAJ, XMAJ, EPI_F32, ACT_NONE, false>(p, 1, s);
+  } else {
+    if (ws == nullptr) return hipErrorInvalidValue;
+    p.C = ws; p.ldc = N; p.c_split_stride = (long long)M * N;
+    bws = ws + (size_t)splits * M * N;
+    p.bias_grad = bws; p.bg_split_stride = M;
   }
-  if (ws == nullptr) return hipErrorInvalidValue;
-  p.C = ws; p.ldc = N; p.c_split_stride = (long long)M * N;
-  float* bws = ws + (size_t)splits * M * N;
-  p.bias_grad = bws; p.bg_split_stride = M;
-  hipError_t e = db ? launch_t<64, 64, XMAJ, XMAJ, EPI_F32, ACT_NONE, true>(p, splits, s)
-                    : launch_t<64, 64, XMAJ, XMAJ, EPI_F32, ACT_NONE, false>(p, splits, s);
-  if (e != hipSuccess) return e;
-  const long long nvec = (long long)M * (N / 4);
-  int blocks = (int)std::min<long long>((nvec + 255) / 256, 1024);
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, splits,
-                     (long long)M * N, M, N, dW, N, db ? bws : nullptr, (long long)M, db,
-                     nullptr, 0, 0.f, nullptr);
-  return hipGetLastError();
+  hipError_t e;
+  if (big) e = db ? launch_t<128, 128, XMAJ, XMAJ, EPI_F32, ACT_NONE, true>(p, splits, s)
+                  : launch_t<128, 128, XMAJ, XMAJ, EPI_F32, ACT_NONE, false>(p, splits, s);
+  else e = db ? launch_t<64, 64, XMAJ, XMAJ, EPI_F32, ACT_NONE, true>(p, splits, s)
+              : launch_t<64, 64, XMAJ, XMAJ, EPI_F32, ACT_NONE, false>(p, splits, s);
+  if (e != hipSuccess || splits == 1) return e;
+  return splitk_reduce(ws, splits, (long long)M * N, M, N, dW, N, db ? bws : nullptr, (long long)M, db,
+                       nullptr, 0, 0.f, nullptr, s, sgd);
 }
 
 hipError_t gemm_bf16_generic(const bf16* A, int lda, int la, const bf16* B, int ldb, int lb,
@@ -638,12 +705,23 @@ hipError_t gemm_bf16_generic(const bf16* A, int lda, int la, const bf16* B, int 
 
 hipError_t splitk_reduce(const float* ws, int S, long long stride, int M, int N, float* out, int ldo,
                          const float* bws, long long bstride, float* bout, const float* loss_part,
-                         int n_loss_part, float loss_scale, float* loss_out, hipStream_t s) {
-  const long long nvec = (long long)M * (N / 4);
-  int blocks = (int)std::min<long long>((std::max<long long>(nvec, M) + 255) / 256, 1024);
-  if (blocks < 1) blocks = 1;
-  hipLaunchKernelGGL(splitk_reduce_kernel, dim3(blocks), dim3(256), 0, s, ws, S, stride, M, N, out, ldo,
-                     bws, bstride, bout, loss_part, n_loss_part, loss_scale, loss_out);
+                         int n_loss_part, float loss_scale, float* loss_out, hipStream_t s,
+                         const SgdFuse* sgd) {
+  SgdFuse sg{};
+  if (sgd) sg = *sgd;
+  const long long nvec = (ws && out && S > 0) ? (long long)M * (N / 4) : 0;
+  const int nb_main = (int)((nvec + 63) / 64);
+  const int nb_bias = (bws && bout && S > 0) ? (M + 63) / 64 : 0;
+  const int nb = nb_main + nb_bias + (loss_out ? 1 : 0);
+  if (nb == 0) return hipSuccess;
+#define SLAB_LAUNCH(WSV)                                                                          \
+  hipLaunchKernelGGL(slab_reduce_kernel<WSV>, dim3(nb), dim3(64 * WSV), 0, s, ws, S, stride, M, N, \
+                     out, ldo, nb_main, bws, bstride, bout, nb_bias, loss_part, n_loss_part,       \
+                     loss_scale, loss_out, sg)
+  if (S >= 64 || n_loss_part >= 4096) SLAB_LAUNCH(16);
+  else if (S >= 8) SLAB_LAUNCH(8);
+  else SLAB_LAUNCH(4);
+#undef SLAB_LAUNCH
   return hipGetLastError();
 }
 

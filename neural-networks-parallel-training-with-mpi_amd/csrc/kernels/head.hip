@@ -16,6 +16,9 @@ namespace nnmpi {
 
 constexpr int HEAD_OMAX = 16;
 
+template <typename TA>
+__device__ __forceinline__ void load8(const TA* p, float (&v)[8]);
+
 struct HeadArgs {
   const void* a;
   int rows, in;
@@ -58,150 +61,298 @@ __device__ __forceinline__ void store8(TA* p, const float (&v)[8]) {
   }
 }
 
-template <typename TA, int CMAX, int LOSS, int ACT>
-__global__ void __launch_bounds__(256) head_fwd_kernel(HeadArgs p) {
-  extern __shared__ __attribute__((aligned(16))) float wl[];  // [out][in]
+// One wave per row, RPW rows per wave-iteration (their loads, targets and the RPW x OUTM
+// butterfly reductions are all issued together, so no shuffle or load latency is exposed per
+// row).  With FUSE (out == 1 heads) the head weights live in registers and each lane also
+// accumulates the head's weight/bias gradient for its own 8*CMAX columns across all rows it
+// visits; the 4 waves are combined through LDS in wave order and every block writes one partial
+// slab (gW [in], gb, loss) for the deterministic reducer.  All per-element conditions are
+// expressed as predicates/clamps (no branches around loads or shuffles).
+template <typename TA, int CMAX, int LOSS, int ACT, bool FUSE, int RPW, int OUTM>
+__global__ void __launch_bounds__(256) head_fwd_kernel(HeadArgs p, float* __restrict__ wslab,
+                                                       float* __restrict__ bslab) {
+  extern __shared__ __attribute__((aligned(16))) float wl[];  // [out][in] (+ [in] if FUSE)
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nW = p.out * p.in;
   for (int i = tid * 4; i < nW; i += 256 * 4)
     *reinterpret_cast<float4*>(wl + i) = *reinterpret_cast<const float4*>(p.W + i);
-  __shared__ float red[4];
+  __shared__ float red[4][2];
   __syncthreads();
 
   const int nch = p.in >> 3;
   const TA* A = reinterpret_cast<const TA*>(p.a);
   TA* DZ = reinterpret_cast<TA*>(p.dz_prev);
+  const int nout = FUSE ? 1 : p.out;
   float wave_loss = 0.f;
-  for (int r = blockIdx.x * 4 + w; r < p.rows; r += gridDim.x * 4) {
-    float av[CMAX][8];
+  float gacc[CMAX][8];
+  float gbacc = 0.f;
+  // per-lane column validity as multiplicative masks; the chunk index is clamped for loads
+  float cmask[CMAX];
+  int chc[CMAX];
 #pragma unroll
-    for (int c = 0; c < CMAX; ++c) {
-      const int ch = c * 64 + lane;
-      if (ch < nch) load8<TA>(A + (long long)r * p.in + ch * 8, av[c]);
-      else {
+  for (int c = 0; c < CMAX; ++c) {
+    const int ch = c * 64 + lane;
+    cmask[c] = ch < nch ? 1.f : 0.f;
+    chc[c] = min(ch, nch - 1);
 #pragma unroll
-        for (int e = 0; e < 8; ++e) av[c][e] = 0.f;
+    for (int e = 0; e < 8; ++e) gacc[c][e] = 0.f;
+  }
+  // FUSE: the single output row of W in registers (masked)
+  float wreg[FUSE ? CMAX : 1][8];
+  if constexpr (FUSE) {
+#pragma unroll
+    for (int c = 0; c < CMAX; ++c)
+#pragma unroll
+      for (int e = 0; e < 8; ++e) wreg[c][e] = wl[chc[c] * 8 + e] * cmask[c];
+  }
+  float bias[OUTM];
+#pragma unroll
+  for (int o = 0; o < OUTM; ++o) bias[o] = p.b[min(o, nout - 1)];
+
+  const int gw = blockIdx.x * 4 + w, nwaves = gridDim.x * 4;
+  for (int r0 = gw * RPW; r0 < p.rows; r0 += nwaves * RPW) {
+    float av[RPW][CMAX][8];
+    float yv[RPW][OUTM];
+    int labv[RPW];
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const int r = min(r0 + q, p.rows - 1);   // clamped: loads stay unconditional
+#pragma unroll
+      for (int c = 0; c < CMAX; ++c) load8<TA>(A + (long long)r * p.in + chc[c] * 8, av[q][c]);
+      if constexpr (LOSS == LOSS_MSE) {
+#pragma unroll
+        for (int o = 0; o < OUTM; ++o) yv[q][o] = p.y[(long long)r * nout + min(o, nout - 1)];
+      } else {
+        labv[q] = (int)p.labels[r];
       }
     }
-    float lg[HEAD_OMAX];
+    // partial dot products for every (row, output), then one batched butterfly
+    float part[RPW][OUTM];
 #pragma unroll
-    for (int o = 0; o < HEAD_OMAX; ++o) {
-      float s = 0.f;
-      if (o < p.out) {
+    for (int q = 0; q < RPW; ++q)
+#pragma unroll
+      for (int o = 0; o < OUTM; ++o) {
+        float sacc = 0.f;
 #pragma unroll
         for (int c = 0; c < CMAX; ++c) {
-          const int ch = c * 64 + lane;
-          if (ch < nch) {
-            const float* wr = wl + o * p.in + ch * 8;
+          if constexpr (FUSE) {
 #pragma unroll
-            for (int e = 0; e < 8; ++e) s += av[c][e] * wr[e];
+            for (int e = 0; e < 8; ++e) sacc += av[q][c][e] * wreg[c][e];
+          } else {
+            const float* wr = wl + min(o, nout - 1) * p.in + chc[c] * 8;
+            float t = 0.f;
+#pragma unroll
+            for (int e = 0; e < 8; ++e) t += av[q][c][e] * wr[e];
+            sacc += t * cmask[c];
           }
         }
-        s = wave_sum(s) + p.b[o];
+        part[q][o] = sacc;
       }
-      lg[o] = s;
-    }
-    float dl[HEAD_OMAX];
-    float row_loss = 0.f;
-    if constexpr (LOSS == LOSS_MSE) {
 #pragma unroll
-      for (int o = 0; o < HEAD_OMAX; ++o) {
-        float d = 0.f;
-        if (o < p.out) d = lg[o] - p.y[(long long)r * p.out + o];
-        row_loss += d * d;
-        dl[o] = 2.f * d * p.inv_count;
+    for (int sh = 32; sh >= 1; sh >>= 1)
+#pragma unroll
+      for (int q = 0; q < RPW; ++q)
+#pragma unroll
+        for (int o = 0; o < OUTM; ++o) part[q][o] += __shfl_xor(part[q][o], sh, 64);
+
+#pragma unroll
+    for (int q = 0; q < RPW; ++q) {
+      const bool valid = (r0 + q) < p.rows;
+      const int r = valid ? r0 + q : p.rows - 1;
+      float lg[OUTM];
+#pragma unroll
+      for (int o = 0; o < OUTM; ++o) lg[o] = part[q][o] + bias[o];
+      float dl[OUTM];
+      float row_loss = 0.f;
+      if constexpr (LOSS == LOSS_MSE) {
+#pragma unroll
+        for (int o = 0; o < OUTM; ++o) {
+          const float d = (o < nout) ? lg[o] - yv[q][o] : 0.f;
+          row_loss += d * d;
+          dl[o] = 2.f * d * p.inv_count;
+        }
+      } else {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int o = 0; o < OUTM; ++o) if (o < nout) mx = fmaxf(mx, lg[o]);
+        float se = 0.f;
+#pragma unroll
+        for (int o = 0; o < OUTM; ++o) if (o < nout) se += __expf(lg[o] - mx);
+        const float lse = mx + __logf(se);
+        const int lab = labv[q];
+        float lgl = 0.f;
+#pragma unroll
+        for (int o = 0; o < OUTM; ++o) {
+          if (o == lab) lgl = lg[o];
+          dl[o] = (o < nout) ? (__expf(lg[o] - lse) - (o == lab ? 1.f : 0.f)) * p.inv_count : 0.f;
+        }
+        row_loss = lse - lgl;
       }
-    } else {
-      float mx = -INFINITY;
+      if (!valid) {
+        row_loss = 0.f;
 #pragma unroll
-      for (int o = 0; o < HEAD_OMAX; ++o) if (o < p.out) mx = fmaxf(mx, lg[o]);
-      float se = 0.f;
-#pragma unroll
-      for (int o = 0; o < HEAD_OMAX; ++o) if (o < p.out) se += __expf(lg[o] - mx);
-      const float lse = mx + __logf(se);
-      const int lab = (int)p.labels[r];
-      float lgl = 0.f;
-#pragma unroll
-      for (int o = 0; o < HEAD_OMAX; ++o) {
-        if (o == lab) lgl = lg[o];
-        dl[o] = (o < p.out) ? (__expf(lg[o] - lse) - (o == lab ? 1.f : 0.f)) * p.inv_count : 0.f;
+        for (int o = 0; o < OUTM; ++o) dl[o] = 0.f;
       }
-      row_loss = lse - lgl;
-    }
-    wave_loss += row_loss;
-    float myd = 0.f;
+      wave_loss += row_loss;
+      if constexpr (FUSE) {
+        gbacc += dl[0];
 #pragma unroll
-    for (int o = 0; o < HEAD_OMAX; ++o) if (lane == o) myd = dl[o];
-    if (lane < p.out) p.dlogits[(long long)r * p.out + lane] = myd;
-    if (DZ != nullptr) {
+        for (int c = 0; c < CMAX; ++c)
 #pragma unroll
-      for (int c = 0; c < CMAX; ++c) {
-        const int ch = c * 64 + lane;
-        if (ch < nch) {
+          for (int e = 0; e < 8; ++e) gacc[c][e] += dl[0] * av[q][c][e];
+      } else {
+        float myd = 0.f;
+#pragma unroll
+        for (int o = 0; o < OUTM; ++o) if (lane == o) myd = dl[o];
+        if (valid && lane < nout) p.dlogits[(long long)r * nout + lane] = myd;
+      }
+      if (DZ != nullptr) {
+#pragma unroll
+        for (int c = 0; c < CMAX; ++c) {
           float g[8];
 #pragma unroll
           for (int e = 0; e < 8; ++e) g[e] = 0.f;
 #pragma unroll
-          for (int o = 0; o < HEAD_OMAX; ++o) {
-            if (o < p.out) {
-              const float* wr = wl + o * p.in + ch * 8;
+          for (int o = 0; o < OUTM; ++o) {
+            if constexpr (FUSE) {
+#pragma unroll
+              for (int e = 0; e < 8; ++e) g[e] += dl[o] * wreg[c][e];
+            } else {
+              const float* wr = wl + min(o, nout - 1) * p.in + chc[c] * 8;
 #pragma unroll
               for (int e = 0; e < 8; ++e) g[e] += dl[o] * wr[e];
             }
           }
 #pragma unroll
-          for (int e = 0; e < 8; ++e) g[e] *= act_bwd_t<ACT>(av[c][e]);
-          store8<TA>(DZ + (long long)r * p.in + ch * 8, g);
+          for (int e = 0; e < 8; ++e) g[e] *= act_bwd_t<ACT>(av[q][c][e]);
+          if (valid && cmask[c] != 0.f) store8<TA>(DZ + (long long)r * p.in + chc[c] * 8, g);
         }
       }
     }
   }
-  if (lane == 0) red[w] = wave_loss;
+  if (lane == 0) {
+    red[w][0] = wave_loss;
+    red[w][1] = gbacc;
+  }
+  if constexpr (FUSE) {
+    // combine the 4 waves' column partials in wave order through LDS (after the W image)
+    float* gl = wl + nW;
+    for (int ww = 0; ww < 4; ++ww) {
+      __syncthreads();
+      if (w == ww) {
+#pragma unroll
+        for (int c = 0; c < CMAX; ++c) {
+          if (cmask[c] != 0.f) {
+#pragma unroll
+            for (int e = 0; e < 8; ++e) {
+              float* d = gl + chc[c] * 8 + e;
+              *d = (ww == 0) ? gacc[c][e] : *d + gacc[c][e];
+            }
+          }
+        }
+      }
+    }
+    __syncthreads();
+    float* dst = wslab + (long long)blockIdx.x * p.in;
+    for (int i = tid * 4; i < p.in; i += 256 * 4)
+      *reinterpret_cast<float4*>(dst + i) = *reinterpret_cast<const float4*>(gl + i);
+  }
   __syncthreads();
-  if (tid == 0) p.loss_part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (tid == 0) {
+    p.loss_part[blockIdx.x] = ((red[0][0] + red[1][0]) + red[2][0]) + red[3][0];
+    if constexpr (FUSE) bslab[blockIdx.x] = ((red[0][1] + red[1][1]) + red[2][1]) + red[3][1];
+  }
 }
 
-int head_fwd_parts(int rows) { return std::max(1, std::min((rows + 3) / 4, 1024)); }
+static int head_rpw(int in) {
+  const int nch = in / 8;
+  return nch <= 64 ? 16 : nch <= 128 ? 8 : nch <= 256 ? 4 : 1;
+}
 
-template <typename TA, int CMAX, int LOSS>
-static hipError_t head_launch_act(const HeadArgs& a, int act, int blocks, size_t smem, hipStream_t s) {
+// one wave-iteration per wave where possible: blocks = rows / (4 waves * RPW), capped at 256
+int head_fwd_parts(int rows, int in) {
+  const int per_block = 4 * head_rpw(in);
+  return std::max(1, std::min((rows + per_block - 1) / per_block, 256));
+}
+
+template <typename TA, int CMAX, int LOSS, bool FUSE, int RPW, int OUTM>
+static hipError_t head_launch_act(const HeadArgs& a, int act, int blocks, size_t smem, float* wslab,
+                                  float* bslab, hipStream_t s) {
   switch (act) {
     case ACT_RELU:
-      hipLaunchKernelGGL((head_fwd_kernel<TA, CMAX, LOSS, ACT_RELU>), dim3(blocks), dim3(256), smem, s, a);
+      hipLaunchKernelGGL((head_fwd_kernel<TA, CMAX, LOSS, ACT_RELU, FUSE, RPW, OUTM>), dim3(blocks), dim3(256), smem, s, a, wslab, bslab);
       break;
     case ACT_TANH:
-      hipLaunchKernelGGL((head_fwd_kernel<TA, CMAX, LOSS, ACT_TANH>), dim3(blocks), dim3(256), smem, s, a);
+      hipLaunchKernelGGL((head_fwd_kernel<TA, CMAX, LOSS, ACT_TANH, FUSE, RPW, OUTM>), dim3(blocks), dim3(256), smem, s, a, wslab, bslab);
       break;
     default:
-      hipLaunchKernelGGL((head_fwd_kernel<TA, CMAX, LOSS, ACT_NONE>), dim3(blocks), dim3(256), smem, s, a);
+      hipLaunchKernelGGL((head_fwd_kernel<TA, CMAX, LOSS, ACT_NONE, FUSE, RPW, OUTM>), dim3(blocks), dim3(256), smem, s, a, wslab, bslab);
   }
   return hipGetLastError();
 }
 
-template <typename TA, int LOSS>
-static hipError_t head_launch_c(const HeadArgs& a, int act, int blocks, size_t smem, hipStream_t s) {
+template <typename TA, int LOSS, bool FUSE, int OM>
+static hipError_t head_launch_c(const HeadArgs& a, int act, int blocks, size_t smem, float* wslab,
+                                float* bslab, hipStream_t s) {
   const int nch = a.in / 8;
-  if (nch <= 64) return head_launch_act<TA, 1, LOSS>(a, act, blocks, smem, s);
-  if (nch <= 128) return head_launch_act<TA, 2, LOSS>(a, act, blocks, smem, s);
-  if (nch <= 256) return head_launch_act<TA, 4, LOSS>(a, act, blocks, smem, s);
-  if (nch <= 1024) return head_launch_act<TA, 16, LOSS>(a, act, blocks, smem, s);
+  // fused (out == 1) heads keep many rows in flight; wide heads one row (register budget)
+  constexpr int D = (FUSE || OM == 1) ? 1 : 16;
+  if (nch <= 64) return head_launch_act<TA, 1, LOSS, FUSE, (16 / D > 0 ? 16 / D : 1), OM>(a, act, blocks, smem, wslab, bslab, s);
+  if (nch <= 128) return head_launch_act<TA, 2, LOSS, FUSE, (8 / D > 0 ? 8 / D : 1), OM>(a, act, blocks, smem, wslab, bslab, s);
+  if (nch <= 256) return head_launch_act<TA, 4, LOSS, FUSE, (4 / D > 0 ? 4 / D : 1), OM>(a, act, blocks, smem, wslab, bslab, s);
+  if (nch <= 1024) return head_launch_act<TA, 16, LOSS, FUSE, 1, OM>(a, act, blocks, smem, wslab, bslab, s);
   return hipErrorInvalidValue;
+}
+
+static hipError_t head_fwd_impl(const void* a, int a_bf16, int rows, int in, const float* W,
+                                const float* b, int out, const float* y, const int64_t* labels,
+                                int loss, float inv_count, int act_prev, void* dz_prev,
+                                float* dlogits, float* loss_part, bool fuse, float* wslab,
+                                float* bslab, hipStream_t s) {
+  if (out < 1 || out > HEAD_OMAX || in % 8 != 0 || in > 8192) return hipErrorInvalidValue;
+  const size_t smem = (size_t)(out * in + (fuse ? in : 0)) * sizeof(float);
+  if (smem > 65536 + 32768) return hipErrorInvalidValue;
+  HeadArgs h{a, rows, in, W, b, out, y, labels, inv_count, act_prev, dz_prev, dlogits, loss_part};
+  const int blocks = head_fwd_parts(rows, in);
+#define HL(TA, LS, FU, OM) head_launch_c<TA, LS, FU, OM>(h, act_prev, blocks, smem, wslab, bslab, s)
+  if (fuse) {
+    if (loss == LOSS_XENT || out != 1) return hipErrorInvalidValue;
+    return a_bf16 ? HL(bf16, LOSS_MSE, true, 1) : HL(float, LOSS_MSE, true, 1);
+  }
+  if (loss == LOSS_XENT) return a_bf16 ? HL(bf16, LOSS_XENT, false, HEAD_OMAX) : HL(float, LOSS_XENT, false, HEAD_OMAX);
+  if (out == 1) return a_bf16 ? HL(bf16, LOSS_MSE, false, 1) : HL(float, LOSS_MSE, false, 1);
+  return a_bf16 ? HL(bf16, LOSS_MSE, false, HEAD_OMAX) : HL(float, LOSS_MSE, false, HEAD_OMAX);
+#undef HL
 }
 
 hipError_t head_fwd(const void* a, int a_bf16, int rows, int in, const float* W, const float* b,
                     int out, const float* y, const int64_t* labels, int loss, float inv_count,
                     int act_prev, void* dz_prev, float* dlogits, float* loss_part, hipStream_t s) {
-  if (out < 1 || out > HEAD_OMAX || in % 8 != 0 || in > 8192) return hipErrorInvalidValue;
-  const size_t smem = (size_t)out * in * sizeof(float);
-  if (smem > 65536) return hipErrorInvalidValue;
-  HeadArgs h{a, rows, in, W, b, out, y, labels, inv_count, act_prev, dz_prev, dlogits, loss_part};
-  const int blocks = head_fwd_parts(rows);
-  if (a_bf16) {
-    return loss == LOSS_XENT ? head_launch_c<bf16, LOSS_XENT>(h, act_prev, blocks, smem, s)
-                             : head_launch_c<bf16, LOSS_MSE>(h, act_prev, blocks, smem, s);
-  }
-  return loss == LOSS_XENT ? head_launch_c<float, LOSS_XENT>(h, act_prev, blocks, smem, s)
-                           : head_launch_c<float, LOSS_MSE>(h, act_prev, blocks, smem, s);
+  return head_fwd_impl(a, a_bf16, rows, in, W, b, out, y, labels, loss, inv_count, act_prev, dz_prev,
+                       dlogits, loss_part, false, nullptr, nullptr, s);
+}
+
+bool head_can_fuse(int out, int in, int loss) { return out == 1 && loss == LOSS_MSE && in <= 2048; }
+
+size_t head_fused_workspace_bytes(int rows, int in) {
+  const int G = head_fwd_parts(rows, in);
+  return ((size_t)G * in + (size_t)((G + 3) & ~3) + 4) * sizeof(float);
+}
+
+// Whole regression head (out == 1, MSE) in two launches: fused fwd/loss/dZ/wgrad partials, then
+// the deterministic slab reducer (gW, gb, loss).
+hipError_t head_fused(const void* a, int a_bf16, int rows, int in, const float* W, const float* b,
+                      const float* y, float inv_count, int act_prev, void* dz_prev, float* gW,
+                      float* gb, float* ws, float* loss_part, float loss_scale, float* loss_out,
+                      hipStream_t s, const SgdFuse* sgd) {
+  const int G = head_fwd_parts(rows, in);
+  float* wslab = ws;
+  float* bslab = ws + (size_t)G * in;
+  hipError_t e = head_fwd_impl(a, a_bf16, rows, in, W, b, 1, y, nullptr, LOSS_MSE, inv_count, act_prev,
+                               dz_prev, nullptr, loss_part, true, wslab, bslab, s);
+  if (e != hipSuccess) return e;
+  return splitk_reduce(wslab, G, in, 1, in, gW, in, bslab, 1, gb, loss_part, G, loss_scale, loss_out, s,
+                       sgd);
 }
 
 // ---- head weight gradient: gW[o][i] = sum_r dl[r][o] a[r][i], gb[o] = sum_r dl[r][o] ----
@@ -257,8 +408,8 @@ __global__ void __launch_bounds__(64) head_wgrad_kernel(const TA* __restrict__ a
 
 static int head_splits(int rows, int in) {
   const int gx = (in + 511) / 512;
-  int s = std::max(1, 512 / gx);
-  s = std::min(s, std::max(1, rows / 16));
+  int s = std::max(1, 256 / gx);
+  s = std::min(s, std::max(1, rows / 64));
   return s;
 }
 

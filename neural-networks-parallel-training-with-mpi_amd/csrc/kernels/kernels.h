@@ -9,6 +9,8 @@ namespace nnmpi {
 
 typedef __bf16 bf16;
 
+struct SgdFuse;   // common.h: fused optimizer update for kernels that emit final gradients
+
 enum Epi : int { EPI_BIAS_ACT = 0, EPI_DACT = 1, EPI_F32 = 2 };
 enum Loss : int { LOSS_MSE = 0, LOSS_XENT = 1 };
 
@@ -21,15 +23,20 @@ hipError_t linear_dgrad_bf16(const bf16* dZ, int lddz, const bf16* W, int ldw, c
 int wgrad_splits(int M, int N, int K);
 void set_gemm_impl(int impl);  // 1 = register-staged main loop, 2 = LDS-DMA ring
 int get_gemm_impl();
+void set_gemm_tile(int t);     // 0 = heuristic, 64 / 128 = force (experiments)
+void set_gemm_variant(int v);  // DMA-path main-loop variant (experiments), 0 = default
 size_t wgrad_workspace_bytes(int M, int N, int K);
 hipError_t linear_wgrad_bf16(const bf16* dZ, int lddz, const bf16* X, int ldx, float* dW,
-                             float* db, int M, int N, int K, float* ws, hipStream_t s);
+                             float* db, int M, int N, int K, float* ws, hipStream_t s,
+                             const SgdFuse* sgd = nullptr);
 hipError_t gemm_bf16_generic(const bf16* A, int lda, int la, const bf16* B, int ldb, int lb,
                              int M, int N, int K, float* C, int ldc, hipStream_t s);
+// sgd != nullptr: instead of storing the reduced gradients, apply the optimizer update to the
+// parameters at the same arena positions (single-rank fast path: gradient final once reduced).
 hipError_t splitk_reduce(const float* ws, int S, long long stride, int M, int N, float* out,
                          int ldo, const float* bws, long long bstride, float* bout,
                          const float* loss_part, int n_loss_part, float loss_scale,
-                         float* loss_out, hipStream_t s);
+                         float* loss_out, hipStream_t s, const SgdFuse* sgd = nullptr);
 
 // ---- fp32 GEMM (gemm_f32.hip) ----
 hipError_t linear_fwd_f32(const float* X, int ldx, const float* W, int ldw, const float* bias,
@@ -45,10 +52,16 @@ hipError_t linear_wgrad_f32(const float* dZ, int lddz, const float* X, int ldx, 
 // a: [rows][in] activations (bf16 if a_bf16 else fp32); W: [out][in] fp32; y: [rows][out] fp32
 // (MSE) or labels int64 (XENT).  Writes dlogits [rows][out] fp32, dz_prev [rows][in] (same dtype
 // as a; may be null), loss partials [n_part].
-int head_fwd_parts(int rows);
+int head_fwd_parts(int rows, int in);
 hipError_t head_fwd(const void* a, int a_bf16, int rows, int in, const float* W, const float* b,
                     int out, const float* y, const int64_t* labels, int loss, float inv_count,
                     int act_prev, void* dz_prev, float* dlogits, float* loss_part, hipStream_t s);
+bool head_can_fuse(int out, int in, int loss);
+size_t head_fused_workspace_bytes(int rows, int in);
+hipError_t head_fused(const void* a, int a_bf16, int rows, int in, const float* W, const float* b,
+                      const float* y, float inv_count, int act_prev, void* dz_prev, float* gW,
+                      float* gb, float* ws, float* loss_part, float loss_scale, float* loss_out,
+                      hipStream_t s, const SgdFuse* sgd = nullptr);
 size_t head_wgrad_workspace_bytes(int rows, int in, int out);
 hipError_t head_wgrad(const void* a, int a_bf16, int rows, int in, const float* dlogits, int out,
                       float* gW, float* gb, float* ws, const float* loss_part, int n_loss_part,

@@ -22,16 +22,14 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* 
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
     f32x4 gv = reinterpret_cast<f32x4*>(g)[i];
-    f32x4 d = gv * gs;
-    if (wd != 0.f) d += wd * pv;
-    if (mom != 0.f) {
-      f32x4 b;
-      if (first) b = d;
-      else b = mom * reinterpret_cast<f32x4*>(buf)[i] + (1.f - damp) * d;
-      reinterpret_cast<f32x4*>(buf)[i] = b;
-      d = nesterov ? d + mom * b : b;
+    f32x4 bv = (mom != 0.f && !first) ? reinterpret_cast<f32x4*>(buf)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float bb = bv[r];
+      pv[r] = sgd_elem(pv[r], gv[r], bb, lr, mom, damp, wd, gs, nesterov != 0, first != 0);
+      bv[r] = bb;
     }
-    pv -= lr * d;
+    if (mom != 0.f) reinterpret_cast<f32x4*>(buf)[i] = bv;
     reinterpret_cast<f32x4*>(p)[i] = pv;
     if (shadow) {
       bf16x4 s;

@@ -37,7 +37,7 @@ class MLPEngine:
     def __init__(self, spec: MLPSpec, arena: Arena, ops, sync, *, device, dtype: torch.dtype,
                  rows_capacity: int, lr: float, momentum: float, dampening: float = 0.0,
                  weight_decay: float = 0.0, nesterov: bool = False, use_graph: bool = True,
-                 use_tiny: Optional[bool] = None):
+                 use_tiny: Optional[bool] = None, overlap: bool = True, fuse_sgd: bool = True):
         self.spec = spec
         self.arena = arena
         self.ops = ops
@@ -69,14 +69,19 @@ class MLPEngine:
             self.Y = None
             self.labels = torch.zeros(R, dtype=torch.int64, device=dev)
         self.acts = [torch.zeros(R, w[i + 1], dtype=dtype, device=dev) for i in range(L - 1)]
-        maxw = max(w[1:-1]) if L > 1 else 1
-        self.dzbuf = [torch.zeros(R * maxw, dtype=dtype, device=dev) for _ in range(2)]
+        self.dzl = [torch.zeros(R, w[i + 1], dtype=dtype, device=dev) for i in range(L - 1)]
         self.dlogits = torch.zeros(R, w[-1], dtype=torch.float32, device=dev)
         self.loss_out = torch.zeros(4, dtype=torch.float32, device=dev)
         self.hp = torch.tensor([lr, momentum, dampening, weight_decay, 1.0, 0, 0, 0],
                                dtype=torch.float32, device=dev)
+        self.overlap = bool(overlap) and self.is_cuda and not self.use_tiny
+        from ..parallel.sync import NoSync
+        self.fuse_sgd = (bool(fuse_sgd) and self.overlap and isinstance(sync, NoSync)
+                         and dtype == torch.bfloat16 and hasattr(ops, "sgd_fusion"))
         self.ws = torch.zeros(max(1, self._workspace_bytes() // 4 + 64), dtype=torch.float32,
                               device=dev)
+        if self.is_cuda:
+            self.ev_wfree = [torch.cuda.Event(enable_timing=False) for _ in range(L)]
         self.rows = 0
         self.steps_done = 0
         self._graphs: Dict[tuple, object] = {}
@@ -142,6 +147,12 @@ class MLPEngine:
     def _dz(self, k: int, rows: int, width: int) -> torch.Tensor:
         return self.dzbuf[k][: rows * width].view(rows, width)
 
+    def _dzl(self, layer: int, rows: int) -> torch.Tensor:
+        """Gradient w.r.t. the pre-activation of hidden layer ``layer`` (own buffer per layer,
+        so a concurrent wgrad(layer) never races with the next dgrad's output)."""
+        return self.dzl[layer][:rows]
+
+    # ---------------- sequential schedule (CPU path, and the no-overlap debug mode) ----------
     def forward_backward(self):
         rows, ops, ar, L = self.rows, self.ops, self.arena, self.L
         if rows == 0:  # empty shard: contributes a zero gradient, still joins every collective
@@ -157,36 +168,131 @@ class MLPEngine:
                 self.sync.ready(i)
             return
         x = self.X[:rows]
-        h = x
-        for i in range(L - 1):
-            out = self.acts[i][:rows]
-            ops.linear_act(h, ar.compute_weight(i), ar.bias(i), self.act, out)
-            h = out
+        h = self._forward(x)
         last = L - 1
-        dz = self._dz(0, rows, self.spec.widths[last]) if L > 1 else None
-        ops.head(h, ar.weight(last), ar.bias(last),
-                 self.Y[:rows] if self.Y is not None else None,
-                 self.labels[:rows] if self.labels is not None else None,
-                 self.loss_kind, self.inv_count, self.act if L > 1 else "none", dz,
-                 ar.grad_weight(last), ar.grad_bias(last), self.dlogits[:rows], self.loss_out,
-                 self.loss_scale, ws=self.ws)
+        dz = self._dzl(last - 1, rows) if L > 1 else None
+        self._head(h, dz)
         self.sync.ready(last)
-        k = 0
         for i in range(L - 2, -1, -1):
             x_in = self.acts[i - 1][:rows] if i > 0 else x
             ops.linear_wgrad(dz, x_in, ar.grad_weight(i), ar.grad_bias(i), ws=self.ws)
             self.sync.ready(i)
             if i > 0:
-                k ^= 1
-                dz_next = self._dz(k, rows, self.spec.widths[i])
+                dz_next = self._dzl(i - 1, rows)
                 ops.linear_dgrad(dz, ar.compute_weight(i), self.acts[i - 1][:rows], self.act, dz_next)
                 dz = dz_next
 
+    def _forward(self, x):
+        h = x
+        for i in range(self.L - 1):
+            out = self.acts[i][:self.rows]
+            self.ops.linear_act(h, self.arena.compute_weight(i), self.arena.bias(i), self.act, out)
+            h = out
+        return h
+
+    def _head(self, h, dz, sgd=None):
+        rows, ar, last = self.rows, self.arena, self.L - 1
+        kw = {"sgd": sgd} if sgd is not None else {}
+        self.ops.head(h, ar.weight(last), ar.bias(last),
+                      self.Y[:rows] if self.Y is not None else None,
+                      self.labels[:rows] if self.labels is not None else None,
+                      self.loss_kind, self.inv_count, self.act if self.L > 1 else "none", dz,
+                      ar.grad_weight(last), ar.grad_bias(last), self.dlogits[:rows], self.loss_out,
+                      self.loss_scale, ws=self.ws, **kw)
+
     def _step_body(self, first: bool):
+        if self.overlap:
+            return self._step_body_overlap(first)
         self.sync.begin()
         self.forward_backward()
         self.sync.finish()
         self.ops.sgd(self.arena, self.hp, self.nesterov, first)
+
+    # ---------------- comm-overlapped schedule (GPU) -----------------------------------------
+    # Compute stays on ONE stream (measured: splitting wgrad onto a side stream only adds
+    # cross-stream waits — every GEMM already fills all 256 CUs, so nothing overlaps).  What runs
+    # concurrently is communication: as soon as a bucket's last wgrad is done its all-reduce
+    # starts on the comm stream, followed there by that bucket's SGD update (gated on the last
+    # reader of its weights, ev_wfree), so only the final bucket's all-reduce + update remain
+    # on the critical path.  With one rank the update of the whole arena runs once at the end.
+    def _step_body_overlap(self, first: bool):
+        rows, ops, ar, L = self.rows, self.ops, self.arena, self.L
+        if self.fuse_sgd:
+            return self._step_body_fused(first)
+        main = self.stream
+        self.sync.begin()
+        self._sgd_done = set()
+        self._first = first
+        x = self.X[:rows]
+        h = self._forward(x)
+        last = L - 1
+        dz = self._dzl(last - 1, rows) if L > 1 else None
+        self._head(h, dz)
+        main.record_event(self.ev_wfree[last])
+        self._layer_done(last, main)
+        for i in range(L - 2, -1, -1):
+            x_in = self.acts[i - 1][:rows] if i > 0 else x
+            ops.linear_wgrad(dz, x_in, ar.grad_weight(i), ar.grad_bias(i), ws=self.ws)
+            if i > 0:
+                dz_next = self._dzl(i - 1, rows)
+                ops.linear_dgrad(dz, ar.compute_weight(i), self.acts[i - 1][:rows], self.act, dz_next)
+                dz = dz_next
+            main.record_event(self.ev_wfree[i])
+            self._layer_done(i, main)
+        self.sync.finish()   # joins the comm stream into main
+        rest = [b for b in ar.buckets if b.index not in self._sgd_done]
+        if len(rest) == len(ar.buckets):
+            ops.sgd(ar, self.hp, self.nesterov, first)      # one pass over the whole arena
+        else:
+            for b in rest:
+                ops.sgd(ar, self.hp, self.nesterov, first, offset=b.offset, numel=b.numel)
+
+    # Single rank: a layer's gradient is final as soon as its split-K partials are combined, so
+    # the reducer applies the SGD update itself (no gradient round trip through HBM, no separate
+    # optimizer pass).  dgrad_i runs BEFORE wgrad_i here: it is the last reader of W_i.
+    def _step_body_fused(self, first: bool):
+        rows, ops, ar, L = self.rows, self.ops, self.arena, self.L
+        fz = ops.sgd_fusion(ar, self.hp, self.nesterov, first)
+        x = self.X[:rows]
+        h = self._forward(x)
+        last = L - 1
+        dz = self._dzl(last - 1, rows) if L > 1 else None
+        unfused = []
+        if ops.head_can_fuse_sgd(self.spec.widths[-1], self.spec.widths[-2], self.loss_kind):
+            self._head(h, dz, sgd=fz)
+        else:
+            self._head(h, dz)
+            unfused.append(last)
+        for i in range(L - 2, -1, -1):
+            x_in = self.acts[i - 1][:rows] if i > 0 else x
+            dz_i = dz
+            if i > 0:
+                dz_next = self._dzl(i - 1, rows)
+                ops.linear_dgrad(dz_i, ar.compute_weight(i), self.acts[i - 1][:rows], self.act, dz_next)
+                dz = dz_next
+            out_f, in_f = self.spec.layer_shape(i)
+            if ops.wgrad_can_fuse_sgd(rows, out_f, in_f, self.dtype):
+                ops.linear_wgrad(dz_i, x_in, ar.grad_weight(i), ar.grad_bias(i), ws=self.ws, sgd=fz)
+            else:
+                ops.linear_wgrad(dz_i, x_in, ar.grad_weight(i), ar.grad_bias(i), ws=self.ws)
+                unfused.append(i)
+        for i in unfused:
+            s, e = ar.layer_range[i]
+            ops.sgd(ar, self.hp, self.nesterov, first, offset=s, numel=e - s)
+
+    def _layer_done(self, layer: int, stream):
+        b = self.arena.bucket_of_layer(layer)
+        if layer != min(b.layers):
+            return
+        rs = self.sync.launch_bucket(b, stream)
+        if rs is None or rs is stream:
+            return   # reduced on this stream already (single rank): update once at the end
+        with torch.cuda.stream(rs):
+            for l in b.layers:
+                rs.wait_event(self.ev_wfree[l])
+            self.ops.sgd(self.arena, self.hp, self.nesterov, self._first, offset=b.offset,
+                         numel=b.numel)
+        self._sgd_done.add(b.index)
 
     def step(self):
         """One optimizer step on the loaded batch.  Asynchronous on the GPU."""

@@ -272,7 +272,7 @@ def _run(j: Job) -> TrainResult:
     eng = MLPEngine(spec, arena, ops, sync, device=j.device, dtype=dtype,
                     rows_capacity=max(cap, 1), lr=cfg.lr, momentum=cfg.momentum,
                     dampening=cfg.dampening, weight_decay=cfg.weight_decay,
-                    nesterov=cfg.nesterov, use_graph=cfg.graph)
+                    nesterov=cfg.nesterov, use_graph=cfg.graph, overlap=cfg.overlap)
     eng.steps_done = steps_done
     Xc = X.to(dtype)
     metrics = MetricsWriter(cfg.metrics_json if rank == 0 else None)

@@ -64,38 +64,59 @@ class HipOps:
             return int(self.lib.wgrad_workspace_bytes(out_f, in_f, rows))
         return int(self.lib.wgrad_f32_workspace_bytes(out_f, in_f, rows))
 
-    def linear_wgrad(self, dz, x, gW, gb, ws=None):
+    def wgrad_can_fuse_sgd(self, rows, out_f, in_f, dtype) -> bool:
+        """True when the wgrad's split-K reducer can apply the optimizer update itself."""
+        return dtype == torch.bfloat16 and bool(self.lib.wgrad_will_split(out_f, in_f, rows))
+
+    @staticmethod
+    def sgd_fusion(arena, hp, nesterov: bool, first: bool):
+        sh = _p(arena.shadow) if arena.shadow is not None else 0
+        return (_p(arena.grad), _p(arena.master), _p(arena.momentum), sh, _p(hp), int(nesterov),
+                int(first))
+
+    def linear_wgrad(self, dz, x, gW, gb, ws=None, sgd=None):
         rows, M = dz.shape
         N = x.shape[1]
         if dz.dtype == torch.bfloat16:
             _check(M % 8 == 0 and N % 8 == 0, f"bf16 wgrad needs out%8==0, in%8==0 ({M}, {N})")
             self.lib.linear_wgrad_bf16(_p(dz), dz.stride(0), _p(x), x.stride(0), _p(gW), _p(gb),
-                                       M, N, rows, _p(ws), self.stream)
+                                       M, N, rows, _p(ws), self.stream, sgd)
         else:
             self.lib.linear_wgrad_f32(_p(dz), dz.stride(0), _p(x), x.stride(0), _p(gW), _p(gb),
                                       M, N, rows, _p(ws), self.stream)
 
     # ---------------- head ----------------
-    def head_parts(self, rows: int) -> int:
-        return int(self.lib.head_fwd_parts(rows))
+    def head_parts(self, rows: int, in_f: int) -> int:
+        return int(self.lib.head_fwd_parts(rows, in_f))
 
-    def _head_split(self, rows):
-        parts = self.head_parts(rows)
+    def _head_split(self, rows, in_f):
+        parts = self.head_parts(rows, in_f)
         return parts, (parts + 3) // 4 * 4 + 4   # keep the slab region 16-byte aligned
 
-    def head_workspace_bytes(self, rows, in_f, out_f) -> int:
-        _, off = self._head_split(rows)
-        return int(self.lib.head_wgrad_workspace_bytes(rows, in_f, out_f)) + 4 * off
+    def head_workspace_bytes(self, rows, in_f, out_f, loss="mse") -> int:
+        _, off = self._head_split(rows, in_f)
+        return max(int(self.lib.head_wgrad_workspace_bytes(rows, in_f, out_f)),
+                   int(self.lib.head_fused_workspace_bytes(rows, in_f))) + 4 * off
+
+    def head_can_fuse_sgd(self, out_f, in_f, loss) -> bool:
+        return bool(self.lib.head_can_fuse(out_f, in_f, LOSS_CODES[loss]))
 
     def head(self, a, W, b, y, labels, loss: str, inv_count: float, act_prev: str, dz_out,
-             gW, gb, dlogits, loss_out, loss_scale: float, ws=None):
+             gW, gb, dlogits, loss_out, loss_scale: float, ws=None, sgd=None):
         rows, in_f = a.shape
         out_f = W.shape[0]
         _check(in_f % 8 == 0, f"head needs in%8==0 (in={in_f})")
-        parts, off = self._head_split(rows)
+        parts, off = self._head_split(rows, in_f)
         lp = ws[:parts]
         wws = ws[off:]
         a_bf16 = 1 if a.dtype == torch.bfloat16 else 0
+        if self.lib.head_can_fuse(out_f, in_f, LOSS_CODES[loss]):
+            # regression head: fwd + loss + dZ + wgrad partials in one kernel, then one reduce
+            self.lib.head_fused(_p(a), a_bf16, rows, in_f, _p(W), _p(b), _p(y), float(inv_count),
+                                ACT_CODES[act_prev], _p(dz_out), _p(gW), _p(gb), _p(wws), _p(lp),
+                                float(loss_scale), _p(loss_out), self.stream, sgd)
+            return
+        assert sgd is None, "optimizer fusion needs the fused regression head"
         self.lib.head_fwd(_p(a), a_bf16, rows, in_f, _p(W), _p(b), out_f, _p(y), _p(labels),
                           LOSS_CODES[loss], float(inv_count), ACT_CODES[act_prev], _p(dz_out),
                           _p(dlogits), _p(lp), self.stream)
@@ -116,7 +137,11 @@ class HipOps:
                                _p(ws), _p(loss_out), self.stream)
 
     # ---------------- optimizer ----------------
-    def sgd(self, arena, hp, nesterov: bool, first: bool, zero_grad: bool = True):
-        self.lib.sgd_momentum(_p(arena.master), _p(arena.grad), _p(arena.momentum),
-                              _p(arena.shadow), arena.numel, _p(hp), int(nesterov), int(first),
-                              int(zero_grad), self.stream)
+    def sgd(self, arena, hp, nesterov: bool, first: bool, zero_grad: bool = True, offset: int = 0,
+            numel: int = None):
+        n = arena.numel - offset if numel is None else numel
+        e = 4  # bytes per fp32 element
+        sh = _p(arena.shadow) + 2 * offset if arena.shadow is not None else 0
+        self.lib.sgd_momentum(_p(arena.master) + e * offset, _p(arena.grad) + e * offset,
+                              _p(arena.momentum) + e * offset, sh, n, _p(hp), int(nesterov),
+                              int(first), int(zero_grad), self.stream)

@@ -77,9 +77,12 @@ class TorchOps:
         if dz_out is not None:
             dz_out.copy_(dl.mm(W.float()) * act_bwd_from_out(af, act_prev))
 
-    def sgd(self, arena, hp, nesterov: bool, first: bool, zero_grad: bool = True):
+    def sgd(self, arena, hp, nesterov: bool, first: bool, zero_grad: bool = True, offset: int = 0,
+            numel: int = None):
         lr, mom, damp, wd, gs = [float(v) for v in hp.tolist()[:5]]
-        p, g, buf = arena.master, arena.grad, arena.momentum
+        n = arena.numel - offset if numel is None else numel
+        sl = slice(offset, offset + n)
+        p, g, buf = arena.master[sl], arena.grad[sl], arena.momentum[sl]
         with torch.no_grad():
             d = g * gs
             if wd != 0:
@@ -92,6 +95,6 @@ class TorchOps:
                 d = d + mom * buf if nesterov else buf
             p.sub_(lr * d)
             if arena.shadow is not None:
-                arena.shadow.copy_(p)
+                arena.shadow[sl].copy_(p)
             if zero_grad:
                 g.zero_()

@@ -49,12 +49,22 @@ class GradSync:
     def _launch(self, bucket):
         pass
 
+    def launch_bucket(self, bucket, stream):
+        """Launch the reduction of a complete bucket whose gradients were produced on ``stream``.
+        Returns the stream on which the reduced bucket is ready (the engine runs that bucket's
+        optimizer update there), or None when the update must wait for :meth:`finish`."""
+        self._launch(bucket)
+        return None
+
     def finish(self):
         pass
 
 
 class NoSync(GradSync):
     world = 1
+
+    def launch_bucket(self, bucket, stream):
+        return stream   # single rank: the local gradient is final
 
 
 class TorchDistSync(GradSync):
@@ -94,12 +104,19 @@ class NativeRcclSync(GradSync):
         self.gs = native.lib().GradSync(native_comm, len(arena.buckets), priority)
         self._launched = False
 
-    def _launch(self, bucket):
+        import torch
+        self._comm_stream = torch.cuda.ExternalStream(self.gs.comm_stream)
+
+    def _launch(self, bucket, stream=None):
         view = self.arena.grad[bucket.offset:bucket.offset + bucket.numel]
         self.seq += 1
-        self.gs.bucket_ready(bucket.index, view.data_ptr(), bucket.numel, 0,
-                             self.native.stream_handle())
+        h = int(stream.cuda_stream) if stream is not None else self.native.stream_handle()
+        self.gs.bucket_ready(bucket.index, view.data_ptr(), bucket.numel, 0, h)
         self._launched = True
+
+    def launch_bucket(self, bucket, stream):
+        self._launch(bucket, stream)
+        return self._comm_stream
 
     def finish(self):
         if self._launched:

@@ -24,6 +24,9 @@ def main():
     ap.add_argument("--rounds", type=int, default=10)
     ap.add_argument("--iters", type=int, default=20)
     ap.add_argument("--impls", default="1,2")
+    ap.add_argument("--tiles", default="0,64,128")
+    ap.add_argument("--only", default="fwd,dgrad,wgrad")
+    ap.add_argument("--variants", default="0")
     a = ap.parse_args()
     lib = native.lib()
     ops = HipOps()
@@ -43,12 +46,26 @@ def main():
         "dgrad": lambda: ops.linear_dgrad(dz, W, x, "relu", dx),
         "wgrad": lambda: ops.linear_wgrad(dz, x, gW, gb, ws=ws),
     }
-    impls = [int(i) for i in a.impls.split(",")]
+    tjobs = {
+        "fwd": lambda: torch.mm(x, W.t(), out=y),
+        "dgrad": lambda: torch.mm(dz, W, out=dx),
+        "wgrad": lambda: torch.mm(dz.t(), x, out=gWb),
+    }
+    gWb = torch.empty(N, K, device=dev, dtype=torch.bfloat16)
+    jobs = {k: v for k, v in jobs.items() if k in a.only.split(",")}
+    impls = [(int(i), int(t), int(v)) for i in a.impls.split(",") for t in a.tiles.split(",")
+             for v in (a.variants.split(",") if i == "2" else ["0"])]
     res = {(j, i): [] for j in jobs for i in impls}
     for r in range(a.rounds):
-        for name, fn in jobs.items():
+        for name in jobs:
             for impl in impls:
-                lib.set_gemm_impl(impl)
+                if impl[0] == 0:   # vendor reference point: torch.mm (hipBLASLt), bf16 out
+                    fn = tjobs[name]
+                else:
+                    fn = jobs[name]
+                lib.set_gemm_impl(max(impl[0], 1))
+                lib.set_gemm_tile(impl[1])
+                lib.set_gemm_variant(impl[2])
                 fn()
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
@@ -60,10 +77,12 @@ def main():
     flops = 2.0 * R * K * N
     for (name, impl), v in res.items():
         med = statistics.median(v)
-        print(json.dumps({"kernel": name, "impl": impl, "rows": R, "in": K, "out": N,
+        print(json.dumps({"kernel": name, "impl": impl[0], "tile": impl[1], "variant": impl[2], "rows": R, "in": K, "out": N,
                           "median_us": round(med, 2), "min_us": round(min(v), 2),
                           "tflops": round(flops / (med * 1e-6) / 1e12, 1)}))
     lib.set_gemm_impl(2)
+    lib.set_gemm_tile(0)
+    lib.set_gemm_variant(0)
 
 
 if __name__ == "__main__":

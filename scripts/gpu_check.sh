@@ -29,7 +29,7 @@ for s in $STEPS; do
     gemm)
       timeout -k 10 300 python scripts/gemm_bench.py > gpurun_out/gemm_bench.json 2> gpurun_out/gemm_bench.err
       ok_or_stop $? gemm
-      timeout -k 10 300 python scripts/gemm_bench.py --inf 8192 --outf 8192 --rows 4096 --rounds 3 --iters 5 >> gpurun_out/gemm_bench.json 2>> gpurun_out/gemm_bench.err
+      timeout -k 10 300 python scripts/gemm_bench.py --inf 8192 --outf 8192 --rows 4096 --rounds 3 --iters 5 --tiles 0 >> gpurun_out/gemm_bench.json 2>> gpurun_out/gemm_bench.err
       ok_or_stop $? gemm8k
       cat gpurun_out/gemm_bench.json ;;
     bench)
