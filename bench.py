@@ -26,6 +26,8 @@ sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
 
 # Reference numbers (reference algorithm on the 512-wide proxy, CPU, samples/s)
 BASELINE_SAMPLES_PER_S = {1: 32190.0, 2: 61546.0, 4: 88657.0, 8: 105377.0}
+# below this gradient volume the all-reduce is latency-bound: issue it inline (see parallel/sync.py)
+INLINE_MAX_GRAD_BYTES = 64 << 20
 
 CONFIGS = {
     "proxy512": dict(widths=[512, 512, 512, 512, 1], loss="mse", rows=8192,
@@ -55,6 +57,11 @@ def parse():
     p.add_argument("--no_overlap", action="store_true")
     p.add_argument("--even", action="store_true", help="no uneven extra rows")
     p.add_argument("--lr", type=float, default=1e-5)
+    p.add_argument("--comm_mode", choices=["auto", "overlap", "inline"], default="auto",
+                   help="overlap: comm stream + per-bucket SGD; inline: all-reduce on the compute "
+                        "stream (auto: inline when the gradient volume is small)")
+    p.add_argument("--force_comm", action="store_true",
+                   help="use the RCCL gradient path even with one rank (smoke-tests comm overlap)")
     return p.parse_args()
 
 
@@ -109,15 +116,17 @@ def main():
     arena.bind_model(model)
     del model
     native_comm = None
-    if world > 1 and a.comm == "native":
+    if (world > 1 or a.force_comm) and a.comm == "native":
         lib = native.lib()
         uid = pg.broadcast_object(lib.rccl_unique_id() if rank == 0 else None, 0)
-        native_comm = lib.RcclComm(uid, world, rank, dev.index)
+        native_comm = native.make_comm(uid, world, rank, dev.index)
         s = torch.cuda.current_stream()
         native_comm.broadcast(arena.master.data_ptr(), arena.numel, 0, 0, int(s.cuda_stream))
         s.synchronize()
         arena.sync_shadow()
-        sync = NativeRcclSync(arena, native_comm, world)
+        inline = (a.comm_mode == "inline" or
+                  (a.comm_mode == "auto" and arena.numel * 4 <= INLINE_MAX_GRAD_BYTES))
+        sync = NativeRcclSync(arena, native_comm, world, inline=inline)
     elif world > 1:
         dist.broadcast(arena.master, src=0, group=pg.nccl)
         arena.sync_shadow()
@@ -177,8 +186,11 @@ def main():
             "data": "synthetic (device-generated make_regression-style rows), random init",
             "config": {"model": c["model"], "global_batch": samples, "seq_len": None,
                        "parallelism": f"dp{world}", "rows_per_gpu": rows_pg,
-                       "uneven_split": (not a.even and world > 1), "comm": a.comm if world > 1 else "none",
+                       "uneven_split": (not a.even and world > 1),
+                       "comm": a.comm if (world > 1 or a.force_comm) else "none",
                        "graph": not a.no_graph, "overlap": not a.no_overlap,
+                       "comm_mode": (("inline" if sync.inline else "overlap")
+                                     if hasattr(sync, "inline") else None),
                        "bucket_mb": a.bucket_mb},
             "model_tflops_per_s": round(tflops, 2),
             "loss_after_warmup": loss0,

@@ -188,8 +188,10 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
   // ---- RCCL runtime ----
   m.def("rccl_unique_id", []() { return py::bytes(RcclComm::get_unique_id()); });
   py::class_<RcclComm>(m, "RcclComm")
-      .def(py::init([](py::bytes uid, int nranks, int rank, int device) {
-             return new RcclComm(std::string(uid), nranks, rank, device);
+      // bytes -> std::string is converted by pybind11 while the GIL is held; no Python object
+      // lives inside the GIL-free body (ncclCommInitRank blocks until every rank has joined)
+      .def(py::init([](const std::string& uid, int nranks, int rank, int device) {
+             return new RcclComm(uid, nranks, rank, device);
            }), py::call_guard<py::gil_scoped_release>())
       .def_property_readonly("rank", &RcclComm::rank)
       .def_property_readonly("size", &RcclComm::size)

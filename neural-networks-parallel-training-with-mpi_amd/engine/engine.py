@@ -138,7 +138,7 @@ class MLPEngine:
         with ctx, torch.no_grad():
             self.X[:n].copy_(X, non_blocking=True)
             if self.Y is not None and Y is not None:
-                self.Y[:n].copy_(Y.reshape(n, -1), non_blocking=True)
+                self.Y[:n].copy_(Y.reshape(n, self.Y.shape[1]), non_blocking=True)
             if self.labels is not None and labels is not None:
                 self.labels[:n].copy_(labels, non_blocking=True)
         self.rows = n
@@ -308,7 +308,16 @@ class MLPEngine:
                     key = (self.rows, self.inv_count, self.loss_scale)
                     g = self._graphs.get(key)
                     if g is None:
-                        g = self._capture()
+                        try:
+                            g = self._capture()
+                        except RuntimeError as e:   # e.g. a collective that cannot be captured
+                            import sys
+                            print(f"[nnmpi] hipGraph capture failed ({e}); running eagerly",
+                                  file=sys.stderr, flush=True)
+                            self.use_graph = False
+                            self._step_body(False)
+                            self.steps_done += 1
+                            return
                         self._graphs[key] = g
                     g.launch(int(self.stream.cuda_stream))
         self.steps_done += 1

@@ -40,6 +40,9 @@ from .arena import Arena
 from .engine import MLPEngine
 
 SKLEARN_MAX_ELEMS = 4_000_000
+# Below this gradient volume the all-reduce is latency-bound and is issued inline on the compute
+# stream (no cross-HW-queue dependencies; see parallel/sync.py); above it buckets overlap backward.
+INLINE_MAX_GRAD_BYTES = 64 << 20
 HOST_INIT_MAX_PARAMS = 20_000_000
 
 
@@ -86,8 +89,8 @@ class Job:
         comm = cfg.comm
         if comm == "auto":
             comm = "native" if self.device.type == "cuda" else "torch"
-        if self.world == 1:
-            comm = "none"
+        if self.world == 1 and cfg.comm != "native":
+            comm = "none"   # (an explicit --comm native keeps a 1-rank RCCL communicator: testing)
         self.comm_kind = comm
         self.pg = pdist.ProcessGroupContext(self.job, cfg.timeout_s,
                                             want_nccl=(comm == "torch" and self.device.type == "cuda"))
@@ -97,7 +100,7 @@ class Job:
             lib = native.lib()
             uid = lib.rccl_unique_id() if self.rank == 0 else None
             uid = self.pg.broadcast_object(uid, 0)
-            self.native_comm = lib.RcclComm(uid, self.world, self.rank, self.device.index)
+            self.native_comm = native.make_comm(uid, self.world, self.rank, self.device.index)
 
     def close(self):
         self.native_comm = None
@@ -207,12 +210,14 @@ def broadcast_params(j: Job, arena: Arena):
 
 def make_sync(j: Job, arena: Arena):
     cfg = j.cfg
-    if j.world == 1 or j.comm_kind == "none":
+    if j.comm_kind == "none":
         return NoSync(arena)
     if j.comm_kind == "native":
         if cfg.sync == "root":
             raise ValueError("--sync root is only provided on the torch.distributed path")
-        return NativeRcclSync(arena, j.native_comm, j.world)
+        inline = (cfg.comm_mode == "inline" or
+                  (cfg.comm_mode == "auto" and arena.numel * 4 <= INLINE_MAX_GRAD_BYTES))
+        return NativeRcclSync(arena, j.native_comm, j.world, inline=inline)
     group = j.pg.nccl if (j.device.type == "cuda" and j.pg.nccl is not None) else j.pg.gloo
     return TorchDistSync(arena, group, j.world, mode=cfg.sync, overlap=cfg.overlap)
 

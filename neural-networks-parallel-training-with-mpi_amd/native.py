@@ -52,6 +52,31 @@ def available() -> bool:
         return False
 
 
+class stdout_to_stderr:
+    """Redirect fd 1 to fd 2 for the duration (RCCL prints its version banner on stdout at
+    communicator init, which would break one-JSON-line stdout contracts)."""
+
+    def __enter__(self):
+        import sys as _sys
+        _sys.stdout.flush()
+        self._saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        import sys as _sys
+        _sys.stdout.flush()
+        os.dup2(self._saved, 1)
+        os.close(self._saved)
+        return False
+
+
+def make_comm(uid: bytes, world: int, rank: int, device: int):
+    """Create the native RCCL communicator (banner routed to stderr)."""
+    with stdout_to_stderr():
+        return lib().RcclComm(uid, world, rank, device)
+
+
 def stream_handle(stream=None) -> int:
     s = torch.cuda.current_stream() if stream is None else stream
     return int(s.cuda_stream)

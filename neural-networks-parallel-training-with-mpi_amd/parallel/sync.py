@@ -95,8 +95,15 @@ class TorchDistSync(GradSync):
 
 
 class NativeRcclSync(GradSync):
-    def __init__(self, arena, native_comm, world: int, priority: int = -1):
+    """``inline=True``: the all-reduce is issued on the producing (compute) stream itself — no
+    comm stream, no cross-queue events.  Measured on MI355X: every cross-HW-queue dependency
+    costs ~8-10 us and a hipGraph with parallel branches spreads even a linear kernel chain over
+    several queues, so for small (latency-bound) gradient volumes the serial inline form is
+    faster than overlap; large volumes use the overlapped comm stream."""
+
+    def __init__(self, arena, native_comm, world: int, priority: int = -1, inline: bool = False):
         super().__init__(arena)
+        self.inline = bool(inline)
         from .. import native
         self.native = native
         self.comm = native_comm
@@ -111,12 +118,15 @@ class NativeRcclSync(GradSync):
         view = self.arena.grad[bucket.offset:bucket.offset + bucket.numel]
         self.seq += 1
         h = int(stream.cuda_stream) if stream is not None else self.native.stream_handle()
+        if self.inline:
+            self.comm.allreduce(view.data_ptr(), bucket.numel, 0, 0, h)
+            return
         self.gs.bucket_ready(bucket.index, view.data_ptr(), bucket.numel, 0, h)
         self._launched = True
 
     def launch_bucket(self, bucket, stream):
         self._launch(bucket, stream)
-        return self._comm_stream
+        return None if self.inline else self._comm_stream
 
     def finish(self):
         if self._launched:

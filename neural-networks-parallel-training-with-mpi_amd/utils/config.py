@@ -67,6 +67,7 @@ class TrainConfig:
     device: str = "cpu"               # cpu | cuda
     comm: str = "auto"                # auto | torch | native | none
     sync: str = "allreduce"           # allreduce | root (reference-style reduce+bcast)
+    comm_mode: str = "auto"           # auto | overlap (comm stream) | inline (compute stream)
     bucket_mb: float = 1.0
     overlap: bool = True
     graph: bool = True                # capture the steady-state step in a HIP graph
@@ -135,6 +136,7 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--device", choices=["cpu", "cuda"], default="cpu")
     p.add_argument("--comm", choices=["auto", "torch", "native", "none"], default="auto")
     p.add_argument("--sync", choices=["allreduce", "root"], default="allreduce")
+    p.add_argument("--comm_mode", choices=["auto", "overlap", "inline"], default="auto")
     p.add_argument("--bucket_mb", type=float, default=1.0)
     p.add_argument("--no_overlap", dest="overlap", action="store_false")
     p.add_argument("--no_graph", dest="graph", action="store_false")

@@ -107,3 +107,22 @@ def test_fused_optimizer_path_is_bitwise_equal():
         eng_mod.MLPEngine.__init__ = orig
     assert a.losses == b.losses
     assert torch.equal(a.final_params, b.final_params)
+
+
+def test_native_rccl_path_single_rank_matches_local():
+    """1-rank RCCL communicator: bucketed all-reduce on the comm stream + per-bucket SGD
+    (captured in the step graph) must reproduce the communication-free run bitwise."""
+    a = trainer.run_worker(_cfg(device="cuda", comm="native", nepochs=5))
+    b = trainer.run_worker(_cfg(device="cuda", comm="none", nepochs=5))
+    assert a.losses == b.losses
+    assert torch.equal(a.final_params, b.final_params)
+
+
+def test_native_rccl_path_mnist_xent():
+    cfg = dict(widths=[784, 1024, 1024, 10], n_features=784, loss="xent", n_samples=2048,
+               dtype="bf16", nepochs=4, lr=0.05, print_rank="none", data_gen="device",
+               data_dist="local")
+    a = trainer.run_worker(TrainConfig(device="cuda", comm="native", **cfg))
+    b = trainer.run_worker(TrainConfig(device="cuda", comm="none", **cfg))
+    assert a.losses == b.losses
+    assert torch.equal(a.final_params, b.final_params)

@@ -1,0 +1,142 @@
+"""Multi-rank behaviour on CPU (gloo): uneven splits, DP == single-process equivalence, sync
+modes, mini-batches, sequence checker, checkpoint/resume, launchers."""
+import os
+import shutil
+import subprocess
+import sys
+
+import pytest
+import torch
+
+from _mp import run_ranks
+
+import nnmpi_amd  # noqa: F401
+from nnmpi_amd.engine import trainer
+from nnmpi_amd.utils.config import TrainConfig
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+
+
+@pytest.mark.parametrize("world", [3, 5, 6, 7])
+def test_uneven_world_sizes_train(world):
+    """The reference crashes for P in {3,5,6,7} (int8 counts as MPI.INT, D2); here they train."""
+    out = run_ranks(TrainConfig(print_rank="none"), world)
+    rows = [o["rows"] for o in out]
+    assert sum(rows) == 16 and max(rows) - min(rows) <= 1
+    for o in out:
+        assert torch.equal(o["final"], out[0]["final"])           # replicas identical
+        assert all(l == l for l in o["losses"])                    # finite
+
+
+def test_more_ranks_than_rows_allows_empty_shards():
+    cfg = TrainConfig(print_rank="none", n_samples=3, averaging="weighted", scaling="global")
+    out = run_ranks(cfg, 4)
+    assert [o["rows"] for o in out] == [1, 1, 1, 0]
+    for o in out:
+        assert torch.equal(o["final"], out[0]["final"])
+
+
+@pytest.mark.parametrize("world", [2, 3, 4])
+def test_dp_equals_single_process_with_global_scaling(world):
+    """With global feature scaling and sample-weighted averaging, P-rank DP == 1 rank."""
+    cfg = TrainConfig(print_rank="none", scaling="global", averaging="weighted", nepochs=6,
+                      n_samples=48, lr=0.01)
+    single = trainer.run_worker(cfg)
+    out = run_ranks(cfg, world)
+    for o in out:
+        torch.testing.assert_close(o["final"], single.final_params, rtol=1e-5, atol=2e-6)
+
+
+def test_root_sync_mode_matches_allreduce():
+    a = run_ranks(TrainConfig(print_rank="none", sync="root"), 4)
+    b = run_ranks(TrainConfig(print_rank="none", sync="allreduce"), 4)
+    for x, y in zip(a, b):
+        torch.testing.assert_close(x["final"], y["final"], rtol=1e-5, atol=2e-6)
+
+
+def test_minibatches_uneven_ranks_do_not_deadlock():
+    cfg = TrainConfig(print_rank="none", batch_size=2, n_samples=17, nepochs=2)
+    out = run_ranks(cfg, 3)
+    for o in out:
+        assert o["steps"] == 2 * 3          # ceil(6 rows / 2) steps per epoch on every rank
+        assert torch.equal(o["final"], out[0]["final"])
+
+
+def test_sequence_checker_passes():
+    out = run_ranks(TrainConfig(print_rank="none", seqcheck=True), 2)
+    assert len(out) == 2
+
+
+def test_bf16_cpu_path_trains():
+    cfg = TrainConfig(print_rank="none", widths=[64, 64, 64, 1], n_features=64, n_samples=512,
+                      dtype="bf16", nepochs=4, lr=1e-4)
+    out = run_ranks(cfg, 2)
+    assert out[0]["losses"][-1] < out[0]["losses"][0]
+    assert torch.equal(out[0]["final"], out[1]["final"])
+
+
+def test_checkpoint_resume_is_exact(tmp_path):
+    ck = str(tmp_path / "model.pt")
+    full = trainer.run_worker(TrainConfig(print_rank="none", nepochs=5))
+    trainer.run_worker(TrainConfig(print_rank="none", nepochs=3, checkpoint=ck))
+    res = trainer.run_worker(TrainConfig(print_rank="none", nepochs=5, resume=ck))
+    assert torch.equal(res.final_params, full.final_params)
+    sd = torch.load(ck, weights_only=True)
+    assert list(sd) == ["layers.0.weight", "layers.0.bias", "layers.2.weight", "layers.2.bias"]
+    # the saved state_dict loads into the reference-shaped module
+    from nnmpi_amd.models.mlp import MLP
+    MLP().load_state_dict(sd)
+
+
+def test_metrics_json(tmp_path):
+    mj = str(tmp_path / "m.jsonl")
+    trainer.run_worker(TrainConfig(print_rank="none", metrics_json=mj))
+    import json
+    lines = [json.loads(l) for l in open(mj)]
+    assert len(lines) == 3 and all("samples_per_s" in l for l in lines)
+
+
+def test_cli_single_process_prints_reference_lines():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "dataParallelTraining_NN_MPI.py")],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert lines[0] == "[ = = = = = Epoch 0 = = = = = ]"
+    assert lines[1].startswith("loss in worker 0: 2530.83")
+    assert len(lines) == 6
+
+
+def test_cli_typed_flags():
+    """Reference D6: --lr/--momentum overrides must be floats (the reference crashes)."""
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "dataParallelTraining_NN_MPI.py"),
+                        "--lr", "0.002", "--momentum", "0.5", "--nepochs", "1"],
+                       capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr
+    assert "loss in worker 0:" in r.stdout
+
+
+@pytest.mark.skipif(not os.path.exists("/opt/conda/bin/mpiexec"), reason="no mpiexec")
+def test_mpiexec_launch_matches_golden():
+    """`mpiexec -n 2 python dataParallelTraining_NN_MPI.py` (README.md:12) via PMI env."""
+    env = dict(os.environ)
+    env.pop("MASTER_ADDR", None)
+    env.pop("MASTER_PORT", None)
+    r = subprocess.run(["/opt/conda/bin/mpiexec", "-n", "2", sys.executable,
+                        os.path.join(ROOT, "dataParallelTraining_NN_MPI.py")],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    got = {}
+    for l in r.stdout.splitlines():
+        if l.startswith("loss in worker"):
+            rk = int(l.split()[3].rstrip(":"))
+            got.setdefault(rk, []).append(float(l.split()[-1]))
+    assert got[0] == pytest.approx([2230.0779, 2227.2249, 2221.5249], rel=1e-5)
+    assert got[1] == pytest.approx([2835.1191, 2831.0088, 2822.7886], rel=1e-5)
+
+
+def test_self_spawn_cli():
+    r = subprocess.run([sys.executable, os.path.join(ROOT, "dataParallelTraining_NN_MPI.py"),
+                        "--nprocs", "2", "--nepochs", "1"], capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "loss in worker 1: 2835.11" in r.stdout

@@ -1,0 +1,189 @@
+"""Unit tests (CPU): partitioning, config/CLI typing, dataset, arena layout, bucket plan, ops oracle."""
+import numpy as np
+import pytest
+import torch
+
+import nnmpi_amd
+from nnmpi_amd.data.partition import partition_rows
+from nnmpi_amd.engine.arena import Arena
+from nnmpi_amd.utils.config import TrainConfig, build_parser, config_from_args
+
+
+@pytest.mark.parametrize("n,p", [(16, 1), (16, 2), (16, 3), (16, 5), (16, 7), (16, 12), (3, 4),
+                                 (10_000, 7), (43 * 8, 8)])
+def test_partition(n, p):
+    part = partition_rows(n, p)
+    assert sum(part.counts) == n
+    assert part.displs[0] == 0
+    for r in range(1, p):
+        assert part.displs[r] == part.displs[r - 1] + part.counts[r - 1]
+    res = n % p
+    for r in range(p):
+        assert part.counts[r] == n // p + (1 if r < res else 0)    # reference rule (ref.py:117)
+
+
+def test_partition_large_counts_no_overflow():
+    """Reference D1: int8 element counts overflow above 42 rows/rank."""
+    part = partition_rows(1000, 3)
+    assert part.element_counts(3) == [1002, 999, 999]
+
+
+def test_cli_defaults_and_typing():
+    a = build_parser().parse_args([])
+    cfg = config_from_args(a)
+    assert (cfg.lr, cfg.momentum, cfg.batch_size, cfg.nepochs) == (0.001, 0.9, None, 3)
+    a = build_parser().parse_args(["--lr", "0.5", "--momentum", "0.1", "--batch_size", "4"])
+    cfg = config_from_args(a)
+    assert isinstance(cfg.lr, float) and cfg.lr == 0.5 and cfg.batch_size == 4
+
+
+def test_config_accepts_reference_style_namespace():
+    class A:  # the reference's argparse namespace: lr/momentum as strings (D6)
+        lr, momentum, batch_size, nepochs = "0.001", "0.9", 4, 3
+    cfg = config_from_args(A())
+    assert cfg.lr == 0.001 and cfg.batch_size == 4
+
+
+def test_preset():
+    cfg = config_from_args(build_parser().parse_args(["--preset", "mnist"]))
+    assert cfg.widths == [784, 1024, 1024, 10] and cfg.loss == "xent"
+
+
+def test_regression_dataset_numpy_and_tensor():
+    X = np.random.RandomState(0).randn(10, 2)
+    y = np.arange(10.0)
+    ds = nnmpi_amd.RegressionDataset(X, y)
+    assert len(ds) == 10 and ds[3][1].item() == 3.0
+    assert abs(float(ds.X.mean())) < 1e-12                       # standardized
+    ds2 = nnmpi_amd.RegressionDataset(torch.from_numpy(X), torch.from_numpy(y))   # D11 fixed
+    assert len(ds2) == 10
+
+
+def test_arena_layout_and_buckets():
+    ar = Arena([(512, 512), (512, 512), (1, 512)], "cpu", bucket_bytes=1 << 20)
+    # reverse layer order, 64-element aligned
+    assert ar.by_name["layers.4.weight"].offset == 0
+    for s in ar.slots:
+        assert s.offset % 64 == 0
+    covered = sorted((b.offset, b.offset + b.numel) for b in ar.buckets)
+    assert covered[0][0] == 0 and covered[-1][1] == ar.numel
+    for (s0, e0), (s1, e1) in zip(covered, covered[1:]):
+        assert e0 == s1                                          # contiguous, backward order
+    assert ar.buckets[0].layers[0] == 2
+
+
+def test_arena_binds_model_state_dict():
+    from nnmpi_amd.models.mlp import reference_init
+    m = reference_init()
+    ar = Arena([m.spec.layer_shape(i) for i in range(2)], "cpu")
+    ar.bind_model(m)
+    ar.master.add_(1.0)
+    sd = m.state_dict()
+    assert torch.equal(sd["layers.0.weight"], ar.weight(0))
+
+
+def test_torch_ops_match_autograd():
+    from nnmpi_amd.ops.torch_ops import TorchOps
+    torch.manual_seed(0)
+    ops = TorchOps()
+    x = torch.randn(32, 8)
+    W1, b1 = torch.randn(6, 8, requires_grad=True), torch.randn(6, requires_grad=True)
+    W2, b2 = torch.randn(1, 6, requires_grad=True), torch.randn(1, requires_grad=True)
+    y = torch.randn(32, 1)
+    h = torch.relu(x @ W1.t() + b1)
+    out = h @ W2.t() + b2
+    loss = torch.nn.functional.mse_loss(out, y)
+    loss.backward()
+    a = torch.empty(32, 6)
+    ops.linear_act(x, W1.detach(), b1.detach(), "relu", a)
+    gW2, gb2, dz = torch.empty(1, 6), torch.empty(1), torch.empty(32, 6)
+    lo = torch.zeros(4)
+    ops.head(a, W2.detach(), b2.detach(), y, None, "mse", 1 / 32, "relu", dz, gW2, gb2,
+             torch.empty(32, 1), lo, 1 / 32)
+    gW1, gb1 = torch.empty(6, 8), torch.empty(6)
+    ops.linear_wgrad(dz, x, gW1, gb1)
+    torch.testing.assert_close(lo[0], loss.detach())
+    torch.testing.assert_close(gW2, W2.grad)
+    torch.testing.assert_close(gb2, b2.grad)
+    torch.testing.assert_close(gW1, W1.grad)
+    torch.testing.assert_close(gb1, b1.grad)
+
+
+def test_xent_head_matches_autograd():
+    from nnmpi_amd.ops.torch_ops import TorchOps
+    torch.manual_seed(1)
+    a = torch.relu(torch.randn(16, 12))
+    W, b = torch.randn(5, 12, requires_grad=True), torch.randn(5, requires_grad=True)
+    lab = torch.randint(0, 5, (16,))
+    loss = torch.nn.functional.cross_entropy(a @ W.t() + b, lab)
+    loss.backward()
+    gW, gb, lo = torch.empty(5, 12), torch.empty(5), torch.zeros(4)
+    TorchOps().head(a, W.detach(), b.detach(), None, lab, "xent", 1 / 16, "relu", None, gW, gb,
+                    torch.empty(16, 5), lo, 1 / 16)
+    torch.testing.assert_close(lo[0], loss.detach())
+    torch.testing.assert_close(gW, W.grad)
+    torch.testing.assert_close(gb, b.grad)
+
+
+def test_sgd_variants_match_torch():
+    from nnmpi_amd.ops.torch_ops import TorchOps
+    for first, nest, wd, damp in [(True, False, 0, 0), (False, True, 0.01, 0), (False, False, 0.01, 0.2)]:
+        ar = Arena([(4, 8)], "cpu")
+        ar.master.copy_(torch.randn(ar.numel))
+        ar.grad.copy_(torch.randn(ar.numel))
+        ar.momentum.copy_(torch.randn(ar.numel))
+        p = torch.nn.Parameter(ar.master.clone())
+        opt = torch.optim.SGD([p], lr=0.1, momentum=0.9, dampening=damp, weight_decay=wd, nesterov=nest)
+        if not first:
+            opt.state[p]["momentum_buffer"] = ar.momentum.clone()
+        p.grad = ar.grad.clone()
+        opt.step()
+        TorchOps().sgd(ar, torch.tensor([0.1, 0.9, damp, wd, 1.0]), nest, first)
+        torch.testing.assert_close(ar.master, p.detach())
+
+
+def test_chunked_generator_is_partition_independent():
+    from nnmpi_amd.data.synth import chunked_regression
+    X, y = chunked_regression(0, 3000, 16)
+    X2, y2 = chunked_regression(1000, 1500, 16)
+    assert torch.equal(X[1000:2500], X2) and torch.equal(y[1000:2500], y2)
+
+
+def test_engine_cpu_mse_mnist_shapes_run():
+    from nnmpi_amd.engine import trainer
+    cfg = TrainConfig(print_rank="none", widths=[20, 16, 4], n_features=20, loss="xent",
+                      n_samples=64, nepochs=3, lr=0.1)
+    res = trainer.run_worker(cfg)
+    assert res.losses[-1] < res.losses[0]
+
+
+def test_watchdog_fires_on_stall():
+    import time
+    from nnmpi_amd.utils.watchdog import Watchdog
+    hit = []
+    wd = Watchdog(0.3, None, poll_s=0.05, on_fail=lambda why: hit.append(why))
+    time.sleep(0.8)
+    wd.stop()
+    assert hit and "no training progress" in hit[0]
+
+
+def test_watchdog_quiet_when_kicked():
+    import time
+    from nnmpi_amd.utils.watchdog import Watchdog
+    hit = []
+    wd = Watchdog(0.5, None, poll_s=0.05, on_fail=lambda why: hit.append(why))
+    for _ in range(10):
+        time.sleep(0.05)
+        wd.kick()
+    wd.stop()
+    assert not hit
+
+
+def test_sequence_checker_detects_mismatch():
+    from nnmpi_amd.utils.seqcheck import CollectiveMismatch, SequenceChecker
+
+    class FakePG:
+        def allgather_object(self, obj):
+            return [obj, (obj[0], obj[1] + 1)]
+    with pytest.raises(CollectiveMismatch):
+        SequenceChecker(FakePG()).check(0, 3)
