@@ -104,6 +104,9 @@ class NativeRcclSync(GradSync):
     def __init__(self, arena, native_comm, world: int, priority: int = -1, inline: bool = False):
         super().__init__(arena)
         self.inline = bool(inline)
+        if self.inline and len(arena.buckets) > 1:
+            # serial all-reduce: one call over the whole arena amortises the collective latency
+            arena.buckets = arena._plan_buckets(float(1 << 62), 4)
         from .. import native
         self.native = native
         self.comm = native_comm
