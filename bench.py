@@ -55,6 +55,8 @@ def parse():
     p.add_argument("--bucket_mb", type=float, default=1.0)
     p.add_argument("--no_graph", action="store_true")
     p.add_argument("--no_overlap", action="store_true")
+    p.add_argument("--no_group", action="store_true",
+                   help="separate dgrad / wgrad / combine launches instead of the grouped one")
     p.add_argument("--even", action="store_true", help="no uneven extra rows")
     p.add_argument("--lr", type=float, default=1e-5)
     p.add_argument("--comm_mode", choices=["auto", "overlap", "inline"], default="auto",
@@ -136,7 +138,7 @@ def main():
     ops = HipOps(dev)
     eng = MLPEngine(spec, arena, ops, sync, device=dev, dtype=dtype, rows_capacity=rows,
                     lr=a.lr, momentum=0.9, use_graph=not a.no_graph,
-                    overlap=not a.no_overlap)
+                    overlap=not a.no_overlap, grouped=not a.no_group)
     eng.load_batch(X.to(dtype), Y, labels)
     del X
     cfg = TrainConfig(widths=list(widths), loss=c["loss"], n_features=widths[0])
@@ -188,7 +190,7 @@ def main():
                        "parallelism": f"dp{world}", "rows_per_gpu": rows_pg,
                        "uneven_split": (not a.even and world > 1),
                        "comm": a.comm if (world > 1 or a.force_comm) else "none",
-                       "graph": not a.no_graph, "overlap": not a.no_overlap,
+                       "graph": not a.no_graph, "overlap": not a.no_overlap, "grouped": not a.no_group,
                        "comm_mode": (("inline" if sync.inline else "overlap")
                                      if hasattr(sync, "inline") else None),
                        "bucket_mb": a.bucket_mb},

@@ -139,6 +139,54 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
      py::arg("y"), py::arg("inv_count"), py::arg("act_prev"), py::arg("dz"), py::arg("gW"),
      py::arg("gb"), py::arg("ws"), py::arg("lp"), py::arg("lscale"), py::arg("lout"), py::arg("s"),
      py::arg("sgd") = py::none());
+  // ---- deferred combines + grouped backward launch ----
+  py::class_<SlabReduce>(m, "SlabReduce")
+      .def(py::init<>())
+      .def_readonly("S", &SlabReduce::S)
+      .def("pending", [](const SlabReduce& r) { return r.S > 0 || r.loss_out != nullptr; });
+  m.def("slab_reduce", [](const SlabReduce& r, uptr s) { check(slab_reduce(r, S(s)), "slab_reduce"); });
+  m.def("set_bwd_group", &set_bwd_group);
+  m.def("head_fused_deferred", [](uptr a, int a_bf16, int rows, int in, uptr W, uptr b, uptr y,
+                                  float inv_count, int act_prev, uptr dz, uptr gW, uptr gb, uptr ws,
+                                  uptr lp, float lscale, uptr lout, uptr s, py::object sgd) {
+    SgdFuse f{};
+    const bool fu = to_sgd(sgd, f);
+    SlabReduce r{};
+    check(head_fused(P<const void>(a), a_bf16, rows, in, P<const float>(W), P<const float>(b),
+                     P<const float>(y), inv_count, act_prev, P<void>(dz), P<float>(gW), P<float>(gb),
+                     P<float>(ws), P<float>(lp), lscale, P<float>(lout), S(s), fu ? &f : nullptr, &r),
+          "head_fused_deferred");
+    return r;
+  });
+  // dgrad: (dZ, lddz, W, ldw, Aprev, lda_prev, dX, lddx, M, N, K, act) or None
+  // wgrad: (dZ, lddz, X, ldx, dW, db, M, N, K, ws) or None; sgd: fusion tuple or None
+  // red: SlabReduce or None.  Returns the wgrad's pending combine.
+  m.def("bwd_group", [](py::object dgo, py::object wgo, py::object sgd, py::object redo, uptr s) {
+    DgradArgs d{};
+    WgradArgs w{};
+    SlabReduce red{}, pend{};
+    const bool hd = !dgo.is_none(), hw = !wgo.is_none(), hr = !redo.is_none();
+    if (hd) {
+      auto t = dgo.cast<py::tuple>();
+      if (t.size() != 12) throw std::runtime_error("dgrad tuple needs 12 entries");
+      d = DgradArgs{P<const bf16>(t[0].cast<uptr>()), t[1].cast<int>(), P<const bf16>(t[2].cast<uptr>()),
+                    t[3].cast<int>(), P<const bf16>(t[4].cast<uptr>()), t[5].cast<int>(),
+                    P<bf16>(t[6].cast<uptr>()), t[7].cast<int>(), t[8].cast<int>(), t[9].cast<int>(),
+                    t[10].cast<int>(), t[11].cast<int>()};
+    }
+    if (hw) {
+      auto t = wgo.cast<py::tuple>();
+      if (t.size() != 10) throw std::runtime_error("wgrad tuple needs 10 entries");
+      w = WgradArgs{P<const bf16>(t[0].cast<uptr>()), t[1].cast<int>(), P<const bf16>(t[2].cast<uptr>()),
+                    t[3].cast<int>(), P<float>(t[4].cast<uptr>()), P<float>(t[5].cast<uptr>()),
+                    t[6].cast<int>(), t[7].cast<int>(), t[8].cast<int>(), P<float>(t[9].cast<uptr>()),
+                    SgdFuse{}};
+      to_sgd(sgd, w.sg);
+    }
+    if (hr) red = redo.cast<SlabReduce>();
+    check(bwd_group(hd ? &d : nullptr, hw ? &w : nullptr, hr ? &red : nullptr, &pend, S(s)), "bwd_group");
+    return pend;
+  }, py::arg("dgrad"), py::arg("wgrad"), py::arg("sgd"), py::arg("red"), py::arg("s"));
   m.def("wgrad_will_split", [](int M, int N, int K) { return wgrad_splits(M, N, K) > 1; });
   m.def("head_wgrad_workspace_bytes", &head_wgrad_workspace_bytes);
   m.def("head_wgrad", [](uptr a, int a_bf16, int rows, int in, uptr dl, int out, uptr gW, uptr gb,

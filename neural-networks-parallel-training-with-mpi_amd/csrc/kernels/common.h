@@ -3,6 +3,8 @@
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 
+#include "kernels.h"
+
 namespace nnmpi {
 
 typedef __bf16 bf16;
@@ -63,19 +65,6 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   const int q = nwg / 8, r = nwg % 8, xcd = bid % 8;
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
-
-// Optional optimizer fusion for kernels that produce final (already reduced) gradients: the
-// parameter / momentum / bf16-shadow arrays share the gradient arena's layout, so an element's
-// position is found from its offset to g_base.  g_base == nullptr disables the fusion.
-struct SgdFuse {
-  const float* g_base;
-  float* p_base;
-  float* m_base;
-  bf16* s_base;
-  const float* hp;   // {lr, momentum, dampening, weight_decay, grad_scale}
-  int nesterov;
-  int first;
-};
 
 // torch.optim.SGD update of one element (sgd.py semantics; dampening/nesterov/weight decay).
 // Contraction is pinned (explicit fmaf, no compiler contraction) so every kernel that applies

@@ -357,9 +357,11 @@ struct DmaPlan {
   }
 };
 
+// One output tile (tx, ty) of K-split `split` — the body shared by the standalone GEMM launch
+// and the grouped backward launch (bwd_group_kernel).
 template <int BM, int BN, int WGM, int WGN, int LA, int LB, int EPI, int ACT, bool BIASGRAD, int NS>
-__global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_dma_kernel(GemmParams p) {
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
+__device__ __forceinline__ void dma_gemm_tile(const GemmParams& p, char* smem, int tx, int ty,
+                                              int split) {
   constexpr int NW = WGM * WGN;
   constexpr int BK = GEMM_BK;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -369,11 +371,7 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_dma_kernel(GemmParam
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w / WGN, wn = w % WGN;
-  const int gx = gridDim.x, gy = gridDim.y;
-  const int bid = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy);
-  const int tx = bid % gx, ty = bid / gx;
   const int m0 = ty * BM, n0 = tx * BN;
-  const int split = blockIdx.z;
   const int kbeg = split * p.k_per_split;
   const int kend = min(p.K, kbeg + p.k_per_split);
   const int nt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
@@ -454,73 +452,153 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_dma_kernel(GemmParam
   gemm_epilogue<BM, BN, WGM, WGN, EPI, ACT, BIASGRAD>(p, acc, accb, do_bg, m0, n0, wm, wn, lane, split);
 }
 
-// Deterministic split-K / partial-slab combine, one launch for the three jobs a backward needs:
+template <int BM, int BN, int WGM, int WGN, int LA, int LB, int EPI, int ACT, bool BIASGRAD, int NS>
+__global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_dma_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int bid = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy);
+  dma_gemm_tile<BM, BN, WGM, WGN, LA, LB, EPI, ACT, BIASGRAD, NS>(p, smem, bid % gx, bid / gx, blockIdx.z);
+}
+
+// Deterministic split-K / partial-slab combine (the three jobs a backward needs):
 //   blocks [0, nb_main)         out[m][n] = sum_z ws[z][m][n]     (64 float4 columns per block)
 //   blocks [nb_main, +nb_bias)  bout[m]   = sum_z bws[z][m]       (64 scalars per block)
 //   one more block (optional)   *loss_out = loss_scale * sum_i loss_part[i]
-// WS waves per block split the S partials (wave w sums z = w, w+WS, ... in order) and the wave
-// partials are combined in wave order through LDS: bitwise reproducible for a given (S, WS).
-template <int WS>
-__global__ void __launch_bounds__(64 * WS) slab_reduce_kernel(
-    const float* __restrict__ ws, int S, long long stride, int M, int N, float* __restrict__ out,
-    int ldo, int nb_main, const float* __restrict__ bws, long long bstride, float* __restrict__ bout,
-    int nb_bias, const float* __restrict__ loss_part, int n_loss_part, float loss_scale,
-    float* __restrict__ loss_out, SgdFuse sg) {
-  __shared__ f32x4 part[WS][64];
+// WS "virtual" waves split the S partials (virtual wave v sums z = v, v+WS, ... in order) and
+// the virtual-wave partials are combined in order through LDS: bitwise reproducible for a given
+// (S, WS).  NW physical waves run the WS virtual ones (NW == WS standalone; NW = 8 inside the
+// grouped backward launch, which therefore reproduces the standalone result bit for bit).
+template <int WS, int NW>
+__device__ __forceinline__ void slab_reduce_block(const SlabReduce& r, int b, int nb_main, int nb_bias,
+                                                  f32x4* part) {
+  constexpr int VPW = WS >= NW ? WS / NW : 1;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const int b = blockIdx.x;
+  const bool wact = w < WS;
   if (b < nb_main) {
-    const int nv = N >> 2;
-    const long long nvec = (long long)M * nv;
+    const int N = r.N, nv = N >> 2;
+    const long long nvec = (long long)r.M * nv;
     const long long v = (long long)b * 64 + lane;
-    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
     long long m = 0, n = 0;
     if (v < nvec) {
       m = v / nv;
       n = (v % nv) * 4;
-      const float* p = ws + m * N + n;
-#pragma unroll 4
-      for (int z = w; z < S; z += WS) acc += *reinterpret_cast<const f32x4*>(p + z * stride);
     }
-    part[w][lane] = acc;
+    if (wact) {
+      const float* p = r.ws + m * N + n;
+#pragma unroll
+      for (int j = 0; j < VPW; ++j) {
+        const int vw = w + j * NW;
+        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+        if (v < nvec) {
+#pragma unroll 4
+          for (int z = vw; z < r.S; z += WS) acc += *reinterpret_cast<const f32x4*>(p + z * r.stride);
+        }
+        part[vw * 64 + lane] = acc;
+      }
+    }
     __syncthreads();
     if (w == 0 && v < nvec) {
-      f32x4 t = part[0][lane];
+      f32x4 t = part[lane];
 #pragma unroll
-      for (int k = 1; k < WS; ++k) t += part[k][lane];
-      if (sg.g_base) sgd_fused_store4(sg, out + m * ldo + n, t);
-      else *reinterpret_cast<f32x4*>(out + m * ldo + n) = t;
+      for (int k = 1; k < WS; ++k) t += part[k * 64 + lane];
+      float* o = r.out + m * r.ldo + n;
+      if (r.sg.g_base) sgd_fused_store4(r.sg, o, t);
+      else *reinterpret_cast<f32x4*>(o) = t;
     }
     return;
   }
+  float* ps = reinterpret_cast<float*>(part);
   if (b < nb_main + nb_bias) {
     const long long m = (long long)(b - nb_main) * 64 + lane;
-    float acc = 0.f;
-    if (m < M) {
-#pragma unroll 4
-      for (int z = w; z < S; z += WS) acc += bws[z * bstride + m];
-    }
-    part[w][lane][0] = acc;
-    __syncthreads();
-    if (w == 0 && m < M) {
-      float t = part[0][lane][0];
+    if (wact) {
 #pragma unroll
-      for (int k = 1; k < WS; ++k) t += part[k][lane][0];
-      if (sg.g_base) sgd_fused_store(sg, bout + m, t);
-      else bout[m] = t;
+      for (int j = 0; j < VPW; ++j) {
+        const int vw = w + j * NW;
+        float acc = 0.f;
+        if (m < r.M) {
+#pragma unroll 4
+          for (int z = vw; z < r.S; z += WS) acc += r.bws[z * r.bstride + m];
+        }
+        ps[vw * 64 + lane] = acc;
+      }
+    }
+    __syncthreads();
+    if (w == 0 && m < r.M) {
+      float t = ps[lane];
+#pragma unroll
+      for (int k = 1; k < WS; ++k) t += ps[k * 64 + lane];
+      if (r.sg.g_base) sgd_fused_store(r.sg, r.bout + m, t);
+      else r.bout[m] = t;
     }
     return;
   }
   // loss partials: strided per-thread sums, then a fixed-order combine
-  float acc = 0.f;
-  for (int i = threadIdx.x; i < n_loss_part; i += 64 * WS) acc += loss_part[i];
-  acc = wave_sum(acc);
-  if (lane == 0) part[w][0][0] = acc;
+  if (wact) {
+#pragma unroll
+    for (int j = 0; j < VPW; ++j) {
+      const int vw = w + j * NW;
+      float acc = 0.f;
+      for (int i = vw * 64 + lane; i < r.n_loss_part; i += 64 * WS) acc += r.loss_part[i];
+      acc = wave_sum(acc);
+      if (lane == 0) ps[vw] = acc;
+    }
+  }
   __syncthreads();
   if (threadIdx.x == 0) {
     float t = 0.f;
-    for (int k = 0; k < WS; ++k) t += part[k][0][0];
-    *loss_out = t * loss_scale;
+    for (int k = 0; k < WS; ++k) t += ps[k];
+    *r.loss_out = t * r.loss_scale;
+  }
+}
+
+template <int WS>
+__global__ void __launch_bounds__(64 * WS) slab_reduce_kernel(SlabReduce r, int nb_main, int nb_bias) {
+  __shared__ f32x4 part[WS * 64];
+  slab_reduce_block<WS, WS>(r, blockIdx.x, nb_main, nb_bias, part);
+}
+
+// Grouped backward launch (see bwd_group): dgrad tiles, then wgrad (tile, split) blocks, then
+// the previous layer's combine blocks.  GEMM segments are padded to multiples of 8 blocks so the
+// XCD remap inside each segment sees the hardware's round-robin XCD assignment.
+struct BwdGroupParams {
+  GemmParams dg;
+  int dg_gx, dg_n, dg_blocks;
+  GemmParams wg;
+  int wg_gx, wg_tiles, wg_n, wg_blocks;
+  SlabReduce red;
+  int red_ws, nb_main, nb_bias;
+};
+
+constexpr int GRP_BM = 128, GRP_BN = 128, GRP_WGM = 2, GRP_WGN = 4, GRP_NS = 2;
+constexpr int GRP_THREADS = 64 * GRP_WGM * GRP_WGN;
+constexpr int GRP_SMEM = GRP_NS * (GRP_BM + GRP_BN) * GEMM_BK * 2;
+
+template <int ACT>
+__global__ void __launch_bounds__(GRP_THREADS) bwd_group_kernel(BwdGroupParams g) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  int bid = blockIdx.x;
+  if (bid < g.dg_blocks) {
+    const int l = xcd_remap(bid, g.dg_blocks);
+    if (l >= g.dg_n) return;
+    dma_gemm_tile<GRP_BM, GRP_BN, GRP_WGM, GRP_WGN, KMAJ, XMAJ, EPI_DACT, ACT, false, GRP_NS>(
+        g.dg, smem, l % g.dg_gx, l / g.dg_gx, 0);
+    return;
+  }
+  bid -= g.dg_blocks;
+  if (bid < g.wg_blocks) {
+    const int l = xcd_remap(bid, g.wg_blocks);
+    if (l >= g.wg_n) return;
+    const int split = l / g.wg_tiles, t = l % g.wg_tiles;
+    dma_gemm_tile<GRP_BM, GRP_BN, GRP_WGM, GRP_WGN, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, GRP_NS>(
+        g.wg, smem, t % g.wg_gx, t / g.wg_gx, split);
+    return;
+  }
+  bid -= g.wg_blocks;
+  f32x4* part = reinterpret_cast<f32x4*>(smem);
+  switch (g.red_ws) {
+    case 16: slab_reduce_block<16, 8>(g.red, bid, g.nb_main, g.nb_bias, part); break;
+    case 8: slab_reduce_block<8, 8>(g.red, bid, g.nb_main, g.nb_bias, part); break;
+    default: slab_reduce_block<4, 8>(g.red, bid, g.nb_main, g.nb_bias, part); break;
   }
 }
 
@@ -660,34 +738,58 @@ size_t wgrad_workspace_bytes(int M, int N, int K) {
   return (size_t)s * ((size_t)M * N + M) * sizeof(float);
 }
 
+// GEMM parameters of a weight gradient and the split-K combine it needs (pending.S == 0: the
+// GEMM writes dW / db directly).
+static int make_wgrad(const WgradArgs& a, GemmParams& p, SlabReduce& pending) {
+  // dW[M=out][N=in] = sum_k dZ[k][m] X[k][n]; db[m] = sum_k dZ[k][m].
+  const int M = a.M, N = a.N, K = a.K;
+  const int splits = wgrad_splits(M, N, K);
+  const int ksteps = (K + GEMM_BK - 1) / GEMM_BK;
+  p = GemmParams{};
+  p.A = a.dZ; p.lda = a.lddz; p.B = a.X; p.ldb = a.ldx; p.M = M; p.N = N; p.K = K;
+  p.k_per_split = ((ksteps + splits - 1) / splits) * GEMM_BK;
+  pending = SlabReduce{};
+  if (splits == 1) {
+    p.C = a.dW; p.ldc = N; p.c_split_stride = 0;
+    p.bias_grad = a.db; p.bg_split_stride = 0;
+    return splits;
+  }
+  p.C = a.ws; p.ldc = N; p.c_split_stride = (long long)M * N;
+  float* bws = a.ws + (size_t)splits * M * N;
+  p.bias_grad = a.db ? bws : nullptr; p.bg_split_stride = M;
+  pending.ws = a.ws; pending.S = splits; pending.stride = (long long)M * N; pending.M = M;
+  pending.N = N; pending.out = a.dW; pending.ldo = N;
+  if (a.db) { pending.bws = bws; pending.bstride = M; pending.bout = a.db; }
+  pending.sg = a.sg;
+  return splits;
+}
+
+hipError_t linear_wgrad_bf16_deferred(const bf16* dZ, int lddz, const bf16* X, int ldx, float* dW,
+                                      float* db, int M, int N, int K, float* ws, hipStream_t s,
+                                      const SgdFuse* sgd, SlabReduce* pending) {
+  WgradArgs a{dZ, lddz, X, ldx, dW, db, M, N, K, ws, SgdFuse{}};
+  if (sgd) a.sg = *sgd;
+  GemmParams p;
+  SlabReduce r;
+  const int splits = make_wgrad(a, p, r);
+  if (splits > 1 && ws == nullptr) return hipErrorInvalidValue;
+  hipError_t e;
+  if (wgrad_tile(M, N) == 128) e = db ? launch_t<128, 128, XMAJ, XMAJ, EPI_F32, ACT_NONE, true>(p, splits, s)
+                                     : launch_t<128, 128, XMAJ, XMAJ, EPI_F32, ACT_NONE, false>(p, splits, s);
+  else e = db ? launch_t<64, 64, XMAJ, XMAJ, EPI_F32, ACT_NONE, true>(p, splits, s)
+              : launch_t<64, 64, XMAJ, XMAJ, EPI_F32, ACT_NONE, false>(p, splits, s);
+  if (e != hipSuccess) return e;
+  if (pending) {
+    *pending = r;
+    return hipSuccess;
+  }
+  return r.S > 0 ? slab_reduce(r, s) : hipSuccess;
+}
+
 hipError_t linear_wgrad_bf16(const bf16* dZ, int lddz, const bf16* X, int ldx, float* dW,
                              float* db, int M, int N, int K, float* ws, hipStream_t s,
                              const SgdFuse* sgd) {
-  // dW[M=out][N=in] = sum_k dZ[k][m] X[k][n]; db[m] = sum_k dZ[k][m].
-  const int splits = wgrad_splits(M, N, K);
-  const int ksteps = (K + GEMM_BK - 1) / GEMM_BK;
-  const bool big = wgrad_tile(M, N) == 128;
-  GemmParams p{};
-  p.A = dZ; p.lda = lddz; p.B = X; p.ldb = ldx; p.M = M; p.N = N; p.K = K;
-  p.k_per_split = ((ksteps + splits - 1) / splits) * GEMM_BK;
-  float* bws = nullptr;
-  if (splits == 1) {
-    p.C = dW; p.ldc = N; p.c_split_stride = 0;
-    p.bias_grad = db; p.bg_split_stride = 0;
-  } else {
-    if (ws == nullptr) return hipErrorInvalidValue;
-    p.C = ws; p.ldc = N; p.c_split_stride = (long long)M * N;
-    bws = ws + (size_t)splits * M * N;
-    p.bias_grad = bws; p.bg_split_stride = M;
-  }
-  hipError_t e;
-  if (big) e = db ? launch_t<128, 128, XMAJ, XMAJ, EPI_F32, ACT_NONE, true>(p, splits, s)
-                  : launch_t<128, 128, XMAJ, XMAJ, EPI_F32, ACT_NONE, false>(p, splits, s);
-  else e = db ? launch_t<64, 64, XMAJ, XMAJ, EPI_F32, ACT_NONE, true>(p, splits, s)
-              : launch_t<64, 64, XMAJ, XMAJ, EPI_F32, ACT_NONE, false>(p, splits, s);
-  if (e != hipSuccess || splits == 1) return e;
-  return splitk_reduce(ws, splits, (long long)M * N, M, N, dW, N, db ? bws : nullptr, (long long)M, db,
-                       nullptr, 0, 0.f, nullptr, s, sgd);
+  return linear_wgrad_bf16_deferred(dZ, lddz, X, ldx, dW, db, M, N, K, ws, s, sgd, nullptr);
 }
 
 hipError_t gemm_bf16_generic(const bf16* A, int lda, int la, const bf16* B, int ldb, int lb,
@@ -703,25 +805,119 @@ hipError_t gemm_bf16_generic(const bf16* A, int lda, int la, const bf16* B, int 
   return launch_t<64, 64, XMAJ, XMAJ, EPI_F32, ACT_NONE, false>(p, 1, s);
 }
 
+static int slab_ws(const SlabReduce& r) {
+  if (r.S >= 64 || r.n_loss_part >= 4096) return 16;
+  return r.S >= 8 ? 8 : 4;
+}
+
+static void slab_blocks(const SlabReduce& r, int& nb_main, int& nb_bias, int& nb) {
+  const long long nvec = (r.ws && r.out && r.S > 0) ? (long long)r.M * (r.N / 4) : 0;
+  nb_main = (int)((nvec + 63) / 64);
+  nb_bias = (r.bws && r.bout && r.S > 0) ? (r.M + 63) / 64 : 0;
+  nb = nb_main + nb_bias + (r.loss_out ? 1 : 0);
+}
+
+hipError_t slab_reduce(const SlabReduce& r, hipStream_t s) {
+  int nb_main, nb_bias, nb;
+  slab_blocks(r, nb_main, nb_bias, nb);
+  if (nb == 0) return hipSuccess;
+  switch (slab_ws(r)) {
+    case 16: hipLaunchKernelGGL(slab_reduce_kernel<16>, dim3(nb), dim3(64 * 16), 0, s, r, nb_main, nb_bias); break;
+    case 8: hipLaunchKernelGGL(slab_reduce_kernel<8>, dim3(nb), dim3(64 * 8), 0, s, r, nb_main, nb_bias); break;
+    default: hipLaunchKernelGGL(slab_reduce_kernel<4>, dim3(nb), dim3(64 * 4), 0, s, r, nb_main, nb_bias); break;
+  }
+  return hipGetLastError();
+}
+
 hipError_t splitk_reduce(const float* ws, int S, long long stride, int M, int N, float* out, int ldo,
                          const float* bws, long long bstride, float* bout, const float* loss_part,
                          int n_loss_part, float loss_scale, float* loss_out, hipStream_t s,
                          const SgdFuse* sgd) {
-  SgdFuse sg{};
-  if (sgd) sg = *sgd;
-  const long long nvec = (ws && out && S > 0) ? (long long)M * (N / 4) : 0;
-  const int nb_main = (int)((nvec + 63) / 64);
-  const int nb_bias = (bws && bout && S > 0) ? (M + 63) / 64 : 0;
-  const int nb = nb_main + nb_bias + (loss_out ? 1 : 0);
+  SlabReduce r{ws, S, stride, M, N, out, ldo, bws, bstride, bout, loss_part, n_loss_part, loss_scale,
+               loss_out, SgdFuse{}};
+  if (sgd) r.sg = *sgd;
+  return slab_reduce(r, s);
+}
+
+static int g_group = -1;   // grouped backward launch: 1 on (default), 0 off (NNMPI_GROUP=0)
+void set_bwd_group(int on) { g_group = on; }
+static bool group_enabled() {
+  if (g_group < 0) {
+    const char* e = getenv("NNMPI_GROUP");
+    g_group = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_group == 1;
+}
+
+hipError_t bwd_group(const DgradArgs* dg, const WgradArgs* wg, const SlabReduce* red,
+                     SlabReduce* wg_pending, hipStream_t s) {
+  if (wg_pending) *wg_pending = SlabReduce{};
+  int nb_main = 0, nb_bias = 0, nbr = 0;
+  if (red) slab_blocks(*red, nb_main, nb_bias, nbr);
+  GemmParams pw{};
+  SlabReduce pend{};
+  int splits = 0;
+  if (wg) splits = make_wgrad(*wg, pw, pend);
+  // the grouped kernel covers the 128x128 tile shapes of the default DMA main loop
+  bool ok = group_enabled() && gemm_impl() == 2 && g_variant == 0;
+  if (dg) ok = ok && pick_tile(dg->M, dg->N) == 128;
+  if (wg) ok = ok && wgrad_tile(wg->M, wg->N) == 128 && wg->db != nullptr &&
+               (splits == 1 || wg->ws != nullptr);
+  if (!ok) {
+    hipError_t e = hipSuccess;
+    if (red && nbr) e = slab_reduce(*red, s);
+    if (e == hipSuccess && dg)
+      e = linear_dgrad_bf16(dg->dZ, dg->lddz, dg->W, dg->ldw, dg->Aprev, dg->lda_prev, dg->dX,
+                            dg->lddx, dg->M, dg->N, dg->K, dg->act, s);
+    if (e == hipSuccess && wg)
+      e = linear_wgrad_bf16_deferred(wg->dZ, wg->lddz, wg->X, wg->ldx, wg->dW, wg->db, wg->M, wg->N,
+                                     wg->K, wg->ws, s, &wg->sg, wg_pending);
+    return e;
+  }
+  BwdGroupParams g{};
+  if (dg) {
+    GemmParams& p = g.dg;
+    p.A = dg->dZ; p.lda = dg->lddz; p.B = dg->W; p.ldb = dg->ldw;
+    p.M = dg->M; p.N = dg->N; p.K = dg->K;
+    p.k_per_split = ((dg->K + GEMM_BK - 1) / GEMM_BK) * GEMM_BK;
+    p.C = dg->dX; p.ldc = dg->lddx; p.aux = dg->Aprev; p.ldaux = dg->lda_prev;
+    set_extents<KMAJ, XMAJ>(p);
+    g.dg_gx = (p.N + GRP_BN - 1) / GRP_BN;
+    g.dg_n = g.dg_gx * ((p.M + GRP_BM - 1) / GRP_BM);
+    g.dg_blocks = (g.dg_n + 7) & ~7;
+  }
+  if (wg) {
+    set_extents<XMAJ, XMAJ>(pw);
+    g.wg = pw;
+    g.wg_gx = (pw.N + GRP_BN - 1) / GRP_BN;
+    g.wg_tiles = g.wg_gx * ((pw.M + GRP_BM - 1) / GRP_BM);
+    g.wg_n = g.wg_tiles * splits;
+    g.wg_blocks = (g.wg_n + 7) & ~7;
+    if (wg_pending) *wg_pending = pend;
+  }
+  if (red) {
+    g.red = *red;
+    g.red_ws = slab_ws(*red);
+    g.nb_main = nb_main;
+    g.nb_bias = nb_bias;
+  }
+  const int nb = g.dg_blocks + g.wg_blocks + nbr;
   if (nb == 0) return hipSuccess;
-#define SLAB_LAUNCH(WSV)                                                                          \
-  hipLaunchKernelGGL(slab_reduce_kernel<WSV>, dim3(nb), dim3(64 * WSV), 0, s, ws, S, stride, M, N, \
-                     out, ldo, nb_main, bws, bstride, bout, nb_bias, loss_part, n_loss_part,       \
-                     loss_scale, loss_out, sg)
-  if (S >= 64 || n_loss_part >= 4096) SLAB_LAUNCH(16);
-  else if (S >= 8) SLAB_LAUNCH(8);
-  else SLAB_LAUNCH(4);
-#undef SLAB_LAUNCH
+  const int act = dg ? dg->act : ACT_NONE;
+  auto kfn = act == ACT_RELU ? bwd_group_kernel<ACT_RELU>
+           : act == ACT_TANH ? bwd_group_kernel<ACT_TANH> : bwd_group_kernel<ACT_NONE>;
+  static bool attr[3] = {false, false, false};
+  const int ai = act == ACT_RELU ? 0 : act == ACT_TANH ? 1 : 2;
+  if (!attr[ai]) {
+    (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, GRP_SMEM);
+    attr[ai] = true;
+  }
+  hipLaunchKernelGGL(kfn, dim3(nb), dim3(GRP_THREADS), GRP_SMEM, s, g);
+  if (!wg_pending && wg && pend.S > 0) {   // caller does not defer: combine right away
+    hipError_t e = hipGetLastError();
+    if (e != hipSuccess) return e;
+    return slab_reduce(pend, s);
+  }
   return hipGetLastError();
 }
 

@@ -344,15 +344,20 @@ size_t head_fused_workspace_bytes(int rows, int in) {
 hipError_t head_fused(const void* a, int a_bf16, int rows, int in, const float* W, const float* b,
                       const float* y, float inv_count, int act_prev, void* dz_prev, float* gW,
                       float* gb, float* ws, float* loss_part, float loss_scale, float* loss_out,
-                      hipStream_t s, const SgdFuse* sgd) {
+                      hipStream_t s, const SgdFuse* sgd, SlabReduce* pending) {
   const int G = head_fwd_parts(rows, in);
   float* wslab = ws;
   float* bslab = ws + (size_t)G * in;
   hipError_t e = head_fwd_impl(a, a_bf16, rows, in, W, b, 1, y, nullptr, LOSS_MSE, inv_count, act_prev,
                                dz_prev, nullptr, loss_part, true, wslab, bslab, s);
   if (e != hipSuccess) return e;
-  return splitk_reduce(wslab, G, in, 1, in, gW, in, bslab, 1, gb, loss_part, G, loss_scale, loss_out, s,
-                       sgd);
+  SlabReduce r{wslab, G, in, 1, in, gW, in, bslab, 1, gb, loss_part, G, loss_scale, loss_out, SgdFuse{}};
+  if (sgd) r.sg = *sgd;
+  if (pending) {
+    *pending = r;
+    return hipSuccess;
+  }
+  return slab_reduce(r, s);
 }
 
 // ---- head weight gradient: gW[o][i] = sum_r dl[r][o] a[r][i], gb[o] = sum_r dl[r][o] ----

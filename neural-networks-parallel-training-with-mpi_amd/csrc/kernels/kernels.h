@@ -9,7 +9,37 @@ namespace nnmpi {
 
 typedef __bf16 bf16;
 
-struct SgdFuse;   // common.h: fused optimizer update for kernels that emit final gradients
+// Optional optimizer fusion for kernels that produce final (already reduced) gradients: the
+// parameter / momentum / bf16-shadow arrays share the gradient arena's layout, so an element's
+// position is found from its offset to g_base.  g_base == nullptr disables the fusion.
+struct SgdFuse {
+  const float* g_base;
+  float* p_base;
+  float* m_base;
+  bf16* s_base;
+  const float* hp;   // {lr, momentum, dampening, weight_decay, grad_scale}
+  int nesterov;
+  int first;
+};
+
+// A split-K / partial-slab combine (see slab_reduce in gemm_bf16.hip), described so that its
+// launch can be deferred and merged into a later grouped launch (bwd_group).
+struct SlabReduce {
+  const float* ws;          // S slabs of M x N (stride elements apart); null = none
+  int S;
+  long long stride;
+  int M, N;
+  float* out;
+  int ldo;
+  const float* bws;         // S slabs of M bias partials (bstride apart); null = none
+  long long bstride;
+  float* bout;
+  const float* loss_part;   // loss partials (null = none)
+  int n_loss_part;
+  float loss_scale;
+  float* loss_out;
+  SgdFuse sg;               // sg.g_base != null: apply the optimizer update instead of storing
+};
 
 enum Epi : int { EPI_BIAS_ACT = 0, EPI_DACT = 1, EPI_F32 = 2 };
 enum Loss : int { LOSS_MSE = 0, LOSS_XENT = 1 };
@@ -37,6 +67,28 @@ hipError_t splitk_reduce(const float* ws, int S, long long stride, int M, int N,
                          int ldo, const float* bws, long long bstride, float* bout,
                          const float* loss_part, int n_loss_part, float loss_scale,
                          float* loss_out, hipStream_t s, const SgdFuse* sgd = nullptr);
+hipError_t slab_reduce(const SlabReduce& r, hipStream_t s);
+// Weight gradient whose split-K combine is NOT launched: *pending describes it (S == 0: the
+// GEMM wrote dW / db directly, nothing pending).
+hipError_t linear_wgrad_bf16_deferred(const bf16* dZ, int lddz, const bf16* X, int ldx, float* dW,
+                                      float* db, int M, int N, int K, float* ws, hipStream_t s,
+                                      const SgdFuse* sgd, SlabReduce* pending);
+// Grouped backward launch: dgrad of layer i, wgrad of layer i and the pending combine of layer
+// i+1 (three independent jobs) in ONE grid, so each job's tail is filled by the others and two
+// launch gaps disappear.  Any argument may be null.  The wgrad's own combine is returned in
+// *wg_pending (deferred to the next group).  Shapes the grouped kernel does not cover run as
+// separate launches with identical results.
+struct DgradArgs {
+  const bf16* dZ; int lddz; const bf16* W; int ldw; const bf16* Aprev; int lda_prev;
+  bf16* dX; int lddx; int M, N, K, act;
+};
+struct WgradArgs {
+  const bf16* dZ; int lddz; const bf16* X; int ldx; float* dW; float* db; int M, N, K;
+  float* ws; SgdFuse sg;
+};
+void set_bwd_group(int on);   // 1 = grouped kernel (default), 0 = separate launches (A/B)
+hipError_t bwd_group(const DgradArgs* dg, const WgradArgs* wg, const SlabReduce* red,
+                     SlabReduce* wg_pending, hipStream_t s);
 
 // ---- fp32 GEMM (gemm_f32.hip) ----
 hipError_t linear_fwd_f32(const float* X, int ldx, const float* W, int ldw, const float* bias,
@@ -61,7 +113,7 @@ size_t head_fused_workspace_bytes(int rows, int in);
 hipError_t head_fused(const void* a, int a_bf16, int rows, int in, const float* W, const float* b,
                       const float* y, float inv_count, int act_prev, void* dz_prev, float* gW,
                       float* gb, float* ws, float* loss_part, float loss_scale, float* loss_out,
-                      hipStream_t s, const SgdFuse* sgd = nullptr);
+                      hipStream_t s, const SgdFuse* sgd = nullptr, SlabReduce* pending = nullptr);
 size_t head_wgrad_workspace_bytes(int rows, int in, int out);
 hipError_t head_wgrad(const void* a, int a_bf16, int rows, int in, const float* dlogits, int out,
                       float* gW, float* gb, float* ws, const float* loss_part, int n_loss_part,

@@ -37,7 +37,8 @@ class MLPEngine:
     def __init__(self, spec: MLPSpec, arena: Arena, ops, sync, *, device, dtype: torch.dtype,
                  rows_capacity: int, lr: float, momentum: float, dampening: float = 0.0,
                  weight_decay: float = 0.0, nesterov: bool = False, use_graph: bool = True,
-                 use_tiny: Optional[bool] = None, overlap: bool = True, fuse_sgd: bool = True):
+                 use_tiny: Optional[bool] = None, overlap: bool = True, fuse_sgd: bool = True,
+                 grouped: bool = True):
         self.spec = spec
         self.arena = arena
         self.ops = ops
@@ -80,6 +81,13 @@ class MLPEngine:
                          and dtype == torch.bfloat16 and hasattr(ops, "sgd_fusion"))
         self.ws = torch.zeros(max(1, self._workspace_bytes() // 4 + 64), dtype=torch.float32,
                               device=dev)
+        # grouped backward (bf16 GPU): dgrad_i + wgrad_i + combine_{i+1} in one launch.  Layer
+        # i's slabs live in ws_pair[(L-1-i) % 2] so they never alias the pending combine's.
+        from ..parallel.sync import NativeRcclSync
+        inline_sync = isinstance(sync, NoSync) or (isinstance(sync, NativeRcclSync) and sync.inline)
+        self.grouped = (bool(grouped) and self.overlap and dtype == torch.bfloat16 and inline_sync
+                        and hasattr(ops, "bwd_group") and L > 1)
+        self.ws_pair = [self.ws, torch.zeros_like(self.ws)] if self.grouped else [self.ws, self.ws]
         if self.is_cuda:
             self.ev_wfree = [torch.cuda.Event(enable_timing=False) for _ in range(L)]
         self.rows = 0
@@ -217,6 +225,8 @@ class MLPEngine:
     # on the critical path.  With one rank the update of the whole arena runs once at the end.
     def _step_body_overlap(self, first: bool):
         rows, ops, ar, L = self.rows, self.ops, self.arena, self.L
+        if self.grouped:
+            return self._step_body_grouped(first)
         if self.fuse_sgd:
             return self._step_body_fused(first)
         main = self.stream
@@ -279,6 +289,54 @@ class MLPEngine:
         for i in unfused:
             s, e = ar.layer_range[i]
             ops.sgd(ar, self.hp, self.nesterov, first, offset=s, numel=e - s)
+
+    # Grouped schedule: the backward of layer i is ONE launch holding three independent jobs —
+    # dgrad_i, wgrad_i (split-K partial slabs) and the slab combine of layer i+1 (with the SGD
+    # update fused on a single rank) — so each job's tail is filled by the others' blocks and
+    # the step has L+1 fewer launch gaps.  Hazards: combine_{i+1} updates W_{i+1}, which no job
+    # of the group reads (dgrad_i reads W_i); the two slab workspaces alternate.
+    def _step_body_grouped(self, first: bool):
+        rows, ops, ar, L = self.rows, self.ops, self.arena, self.L
+        fz = ops.sgd_fusion(ar, self.hp, self.nesterov, first) if self.fuse_sgd else None
+        x = self.X[:rows]
+        h = self._forward(x)
+        last = L - 1
+        dz = self._dzl(last - 1, rows)
+        unfused = []
+        if ops.head_can_fuse_sgd(self.spec.widths[-1], self.spec.widths[-2], self.loss_kind):
+            pending = ops.head_deferred(h, ar.weight(last), ar.bias(last), self.Y[:rows],
+                                        self.inv_count, self.act, dz, ar.grad_weight(last),
+                                        ar.grad_bias(last), self.loss_out, self.loss_scale,
+                                        self.ws_pair[0], sgd=fz)
+        else:
+            self._head(h, dz)
+            pending = None
+            unfused.append(last)
+        for i in range(L - 2, -1, -1):
+            x_in = self.acts[i - 1][:rows] if i > 0 else x
+            dgrad = None
+            dz_i = dz
+            if i > 0:
+                dz = self._dzl(i - 1, rows)
+                dgrad = (dz_i, ar.compute_weight(i), self.acts[i - 1][:rows], self.act, dz)
+            out_f, in_f = self.spec.layer_shape(i)
+            fuse = fz is not None and ops.wgrad_can_fuse_sgd(rows, out_f, in_f, self.dtype)
+            if not fuse:
+                unfused.append(i)
+            pending = ops.bwd_group(dgrad, (dz_i, x_in, ar.grad_weight(i), ar.grad_bias(i),
+                                            self.ws_pair[(last - i) % 2]),
+                                    fz if fuse else None, pending)
+        ops.slab_reduce(pending)
+        if fz is not None:
+            for i in unfused:
+                s, e = ar.layer_range[i]
+                ops.sgd(ar, self.hp, self.nesterov, first, offset=s, numel=e - s)
+            return
+        self.sync.begin()
+        for b in ar.buckets:
+            self.sync.launch_bucket(b, self.stream)
+        self.sync.finish()
+        ops.sgd(ar, self.hp, self.nesterov, first)
 
     def _layer_done(self, layer: int, stream):
         b = self.arena.bucket_of_layer(layer)

@@ -123,6 +123,42 @@ class HipOps:
         self.lib.head_wgrad(_p(a), a_bf16, rows, in_f, _p(dlogits), out_f, _p(gW), _p(gb),
                             _p(wws), _p(lp), parts, float(loss_scale), _p(loss_out), self.stream)
 
+    # ---------------- grouped backward (bf16) ----------------
+    def head_deferred(self, a, W, b, y, inv_count: float, act_prev: str, dz_out, gW, gb, loss_out,
+                      loss_scale: float, ws, sgd=None):
+        """Fused regression head whose slab combine is deferred (returned, see bwd_group)."""
+        rows, in_f = a.shape
+        parts, off = self._head_split(rows, in_f)
+        a_bf16 = 1 if a.dtype == torch.bfloat16 else 0
+        return self.lib.head_fused_deferred(_p(a), a_bf16, rows, in_f, _p(W), _p(b), _p(y),
+                                            float(inv_count), ACT_CODES[act_prev], _p(dz_out),
+                                            _p(gW), _p(gb), _p(ws[off:]), _p(ws[:parts]),
+                                            float(loss_scale), _p(loss_out), self.stream, sgd)
+
+    def bwd_group(self, dgrad, wgrad, sgd, pending):
+        """One grouped launch: dgrad of layer i (``(dz, W, a_prev, act, out)`` or None), wgrad of
+        layer i (``(dz, x, gW, gb, ws)`` or None, optional optimizer fusion ``sgd``) and the
+        pending combine of layer i+1.  Returns layer i's pending combine."""
+        dg = wg = None
+        if dgrad is not None:
+            dz, W, a_prev, act, out = dgrad
+            rows, K = dz.shape
+            N = W.shape[1]
+            _check(dz.dtype == torch.bfloat16 and K % 8 == 0 and N % 8 == 0, "bf16 dgrad shapes")
+            dg = (_p(dz), dz.stride(0), _p(W), W.stride(0), _p(a_prev), a_prev.stride(0), _p(out),
+                  out.stride(0), rows, N, K, ACT_CODES[act])
+        if wgrad is not None:
+            dz, x, gW, gb, ws = wgrad
+            rows, M = dz.shape
+            N = x.shape[1]
+            _check(dz.dtype == torch.bfloat16 and M % 8 == 0 and N % 8 == 0, "bf16 wgrad shapes")
+            wg = (_p(dz), dz.stride(0), _p(x), x.stride(0), _p(gW), _p(gb), M, N, rows, _p(ws))
+        return self.lib.bwd_group(dg, wg, sgd, pending, self.stream)
+
+    def slab_reduce(self, pending):
+        if pending is not None:
+            self.lib.slab_reduce(pending, self.stream)
+
     # ---------------- tiny fused MLP ----------------
     def tiny_workspace_bytes(self, rows, numel) -> int:
         return int(self.lib.tiny_mlp_workspace_bytes(rows, numel))

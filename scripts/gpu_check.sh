@@ -36,6 +36,14 @@ for s in $STEPS; do
       timeout -k 10 300 python bench.py > gpurun_out/bench.json 2> gpurun_out/bench.err
       ok_or_stop $? bench
       cat gpurun_out/bench.json ;;
+    abgroup)
+      for r in 1 2; do
+        timeout -k 10 300 python bench.py >> gpurun_out/ab_group.json 2>> gpurun_out/ab_group.err
+        ok_or_stop $? "bench grouped"
+        timeout -k 10 300 python bench.py --no_group >> gpurun_out/ab_group.json 2>> gpurun_out/ab_group.err
+        ok_or_stop $? "bench ungrouped"
+      done
+      cat gpurun_out/ab_group.json ;;
     benchall)
       for c in proxy512 mnist wide8192 ref; do
         timeout -k 10 300 python bench.py --config $c --steps 50 --warmup 5 >> gpurun_out/bench_all.json 2>> gpurun_out/bench_all.err

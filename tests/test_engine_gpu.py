@@ -126,3 +126,37 @@ def test_native_rccl_path_mnist_xent():
     b = trainer.run_worker(TrainConfig(device="cuda", comm="none", **cfg))
     assert a.losses == b.losses
     assert torch.equal(a.final_params, b.final_params)
+
+
+def _run_ungrouped(cfg):
+    import nnmpi_amd.engine.engine as eng_mod
+    orig = eng_mod.MLPEngine.__init__
+
+    def no_group(self, *args, **kw):
+        kw["grouped"] = False
+        orig(self, *args, **kw)
+    eng_mod.MLPEngine.__init__ = no_group
+    try:
+        return trainer.run_worker(cfg)
+    finally:
+        eng_mod.MLPEngine.__init__ = orig
+
+
+@pytest.mark.parametrize("comm", ["none", "native"])
+def test_grouped_backward_is_bitwise_equal(comm):
+    """dgrad_i + wgrad_i + combine_{i+1} in one launch == separate launches, bit for bit
+    (fused-SGD single-rank path and the inline-RCCL path)."""
+    a = trainer.run_worker(_cfg(device="cuda", comm=comm, nepochs=5))
+    b = _run_ungrouped(_cfg(device="cuda", comm=comm, nepochs=5))
+    assert a.losses == b.losses
+    assert torch.equal(a.final_params, b.final_params)
+
+
+def test_grouped_backward_xent_head_bitwise_equal():
+    cfg = TrainConfig(device="cuda", widths=[784, 1024, 1024, 10], n_features=784, loss="xent",
+                      n_samples=2048, dtype="bf16", nepochs=4, lr=0.05, print_rank="none",
+                      data_gen="device", data_dist="local")
+    a = trainer.run_worker(cfg)
+    b = _run_ungrouped(cfg)
+    assert a.losses == b.losses
+    assert torch.equal(a.final_params, b.final_params)
