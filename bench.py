@@ -38,7 +38,8 @@ CONFIGS = {
                      model="mlp_8192x4_regression(8192x4-1)"),
     "mnist": dict(widths=[784, 1024, 1024, 10], loss="xent", rows=8192,
                   model="mlp_mnist_shape(784-1024-1024-10,xent)"),
-    "ref": dict(widths=[2, 3, 1], loss="mse", rows=16, model="mlp_reference(2-3-1)"),
+    # the reference config itself: fp32 like the reference (whole step in one tiny-MLP kernel)
+    "ref": dict(widths=[2, 3, 1], loss="mse", rows=16, model="mlp_reference(2-3-1)", dtype="fp32"),
 }
 
 
@@ -99,6 +100,8 @@ def main():
         n_global = rows_pg
     part = partition_rows(n_global, world)
     rows = part.rows(rank)
+    if "dtype" in c:
+        a.dtype = c["dtype"]
     dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
 
     # data (device-generated, partition-independent rows)

@@ -55,7 +55,8 @@ struct GemmParams {
 // XOR swizzle of the 16-byte chunk index for XMAJ images (rows of BX bf16).
 template <int BX>
 __device__ __forceinline__ int swz_x(int k) {
-  if constexpr (BX == 128) return ((k & 3) | ((k >> 1) & 4)) << 1;
+  // rows of 256 B (BX 128) or 512 B (BX 256) both start at bank 0: same chunk XOR
+  if constexpr (BX >= 128) return ((k & 3) | ((k >> 1) & 4)) << 1;
   else return (((k >> 1) & 1) | ((k >> 2) & 2)) << 1;  // BX == 64
 }
 
@@ -460,47 +461,59 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_dma_kernel(GemmParam
   dma_gemm_tile<BM, BN, WGM, WGN, LA, LB, EPI, ACT, BIASGRAD, NS>(p, smem, bid % gx, bid / gx, blockIdx.z);
 }
 
-// Deterministic split-K / partial-slab combine (the three jobs a backward needs):
-//   blocks [0, nb_main)         out[m][n] = sum_z ws[z][m][n]     (64 float4 columns per block)
-//   blocks [nb_main, +nb_bias)  bout[m]   = sum_z bws[z][m]       (64 scalars per block)
+// Deterministic split-K / partial-slab combine (the three jobs a backward needs), 512-thread
+// blocks (8 waves):
+//   main blocks   out[m][n] = sum_z ws[z][m][n]     (float4 columns)
+//   bias blocks   bout[m]   = sum_z bws[z][m]
 //   one more block (optional)   *loss_out = loss_scale * sum_i loss_part[i]
-// WS "virtual" waves split the S partials (virtual wave v sums z = v, v+WS, ... in order) and
-// the virtual-wave partials are combined in order through LDS: bitwise reproducible for a given
-// (S, WS).  NW physical waves run the WS virtual ones (NW == WS standalone; NW = 8 inside the
-// grouped backward launch, which therefore reproduces the standalone result bit for bit).
-template <int WS, int NW>
+// WS "virtual" waves split the S partials of a column group (virtual wave v sums z = v, v+WS,
+// ... in order; WS is picked so that each lane issues ~8 independent loads) and are combined in
+// order through LDS.  WS < 8: a block holds 8/WS column groups of 64; WS = 16: each physical
+// wave runs two virtual waves.  Bitwise reproducible for a given (S, WS); the standalone launch
+// and the grouped backward launch run this same body.
+constexpr int SLAB_NW = 8;
+constexpr int SLAB_THREADS = 64 * SLAB_NW;
+
+template <int WS>
+struct SlabShape {
+  static constexpr int VPW = WS > SLAB_NW ? WS / SLAB_NW : 1;   // virtual waves per wave
+  static constexpr int CG = WS >= SLAB_NW ? 1 : SLAB_NW / WS;   // column groups per block
+  static constexpr int COLS = 64 * CG;                         // columns (float4 / scalars) per block
+};
+
+template <int WS>
 __device__ __forceinline__ void slab_reduce_block(const SlabReduce& r, int b, int nb_main, int nb_bias,
                                                   f32x4* part) {
-  constexpr int VPW = WS >= NW ? WS / NW : 1;
+  using SS = SlabShape<WS>;
   const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
-  const bool wact = w < WS;
+  const int cg = WS >= SLAB_NW ? 0 : w / WS;
+  const int w0 = WS >= SLAB_NW ? w : w % WS;
+  const bool combiner = (w0 == 0);
   if (b < nb_main) {
     const int N = r.N, nv = N >> 2;
     const long long nvec = (long long)r.M * nv;
-    const long long v = (long long)b * 64 + lane;
+    const long long v = ((long long)b * SS::CG + cg) * 64 + lane;
     long long m = 0, n = 0;
     if (v < nvec) {
       m = v / nv;
       n = (v % nv) * 4;
     }
-    if (wact) {
-      const float* p = r.ws + m * N + n;
+    const float* p = r.ws + m * N + n;
 #pragma unroll
-      for (int j = 0; j < VPW; ++j) {
-        const int vw = w + j * NW;
-        f32x4 acc = {0.f, 0.f, 0.f, 0.f};
-        if (v < nvec) {
-#pragma unroll 4
-          for (int z = vw; z < r.S; z += WS) acc += *reinterpret_cast<const f32x4*>(p + z * r.stride);
-        }
-        part[vw * 64 + lane] = acc;
+    for (int j = 0; j < SS::VPW; ++j) {
+      const int vw = w0 + j * SLAB_NW;
+      f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+      if (v < nvec) {
+#pragma unroll 8
+        for (int z = vw; z < r.S; z += WS) acc += *reinterpret_cast<const f32x4*>(p + z * r.stride);
       }
+      part[(cg * WS + vw) * 64 + lane] = acc;
     }
     __syncthreads();
-    if (w == 0 && v < nvec) {
-      f32x4 t = part[lane];
+    if (combiner && v < nvec) {
+      f32x4 t = part[cg * WS * 64 + lane];
 #pragma unroll
-      for (int k = 1; k < WS; ++k) t += part[k * 64 + lane];
+      for (int k = 1; k < WS; ++k) t += part[(cg * WS + k) * 64 + lane];
       float* o = r.out + m * r.ldo + n;
       if (r.sg.g_base) sgd_fused_store4(r.sg, o, t);
       else *reinterpret_cast<f32x4*>(o) = t;
@@ -509,52 +522,57 @@ __device__ __forceinline__ void slab_reduce_block(const SlabReduce& r, int b, in
   }
   float* ps = reinterpret_cast<float*>(part);
   if (b < nb_main + nb_bias) {
-    const long long m = (long long)(b - nb_main) * 64 + lane;
-    if (wact) {
+    const long long m = ((long long)(b - nb_main) * SS::CG + cg) * 64 + lane;
 #pragma unroll
-      for (int j = 0; j < VPW; ++j) {
-        const int vw = w + j * NW;
-        float acc = 0.f;
-        if (m < r.M) {
-#pragma unroll 4
-          for (int z = vw; z < r.S; z += WS) acc += r.bws[z * r.bstride + m];
-        }
-        ps[vw * 64 + lane] = acc;
+    for (int j = 0; j < SS::VPW; ++j) {
+      const int vw = w0 + j * SLAB_NW;
+      float acc = 0.f;
+      if (m < r.M) {
+#pragma unroll 8
+        for (int z = vw; z < r.S; z += WS) acc += r.bws[z * r.bstride + m];
       }
+      ps[(cg * WS + vw) * 64 + lane] = acc;
     }
     __syncthreads();
-    if (w == 0 && m < r.M) {
-      float t = ps[lane];
+    if (combiner && m < r.M) {
+      float t = ps[cg * WS * 64 + lane];
 #pragma unroll
-      for (int k = 1; k < WS; ++k) t += ps[k * 64 + lane];
+      for (int k = 1; k < WS; ++k) t += ps[(cg * WS + k) * 64 + lane];
       if (r.sg.g_base) sgd_fused_store(r.sg, r.bout + m, t);
       else r.bout[m] = t;
     }
     return;
   }
-  // loss partials: strided per-thread sums, then a fixed-order combine
-  if (wact) {
-#pragma unroll
-    for (int j = 0; j < VPW; ++j) {
-      const int vw = w + j * NW;
-      float acc = 0.f;
-      for (int i = vw * 64 + lane; i < r.n_loss_part; i += 64 * WS) acc += r.loss_part[i];
-      acc = wave_sum(acc);
-      if (lane == 0) ps[vw] = acc;
-    }
-  }
+  // loss partials: strided per-thread sums, wave sums, then a fixed-order combine
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < r.n_loss_part; i += SLAB_THREADS) acc += r.loss_part[i];
+  acc = wave_sum(acc);
+  if (lane == 0) ps[w] = acc;
   __syncthreads();
   if (threadIdx.x == 0) {
     float t = 0.f;
-    for (int k = 0; k < WS; ++k) t += ps[k];
+    for (int k = 0; k < SLAB_NW; ++k) t += ps[k];
     *r.loss_out = t * r.loss_scale;
   }
 }
 
+constexpr int SLAB_PART_BYTES = 16 * 64 * 16;   // max(WS, NW) x 64 lanes x f32x4
+
 template <int WS>
-__global__ void __launch_bounds__(64 * WS) slab_reduce_kernel(SlabReduce r, int nb_main, int nb_bias) {
-  __shared__ f32x4 part[WS * 64];
-  slab_reduce_block<WS, WS>(r, blockIdx.x, nb_main, nb_bias, part);
+__global__ void __launch_bounds__(SLAB_THREADS) slab_reduce_kernel(SlabReduce r, int nb_main, int nb_bias) {
+  __shared__ f32x4 part[SLAB_PART_BYTES / 16];
+  slab_reduce_block<WS>(r, blockIdx.x, nb_main, nb_bias, part);
+}
+
+__device__ __forceinline__ void slab_reduce_any(int ws, const SlabReduce& r, int b, int nb_main,
+                                                int nb_bias, f32x4* part) {
+  switch (ws) {
+    case 1: slab_reduce_block<1>(r, b, nb_main, nb_bias, part); break;
+    case 2: slab_reduce_block<2>(r, b, nb_main, nb_bias, part); break;
+    case 4: slab_reduce_block<4>(r, b, nb_main, nb_bias, part); break;
+    case 8: slab_reduce_block<8>(r, b, nb_main, nb_bias, part); break;
+    default: slab_reduce_block<16>(r, b, nb_main, nb_bias, part); break;
+  }
 }
 
 // Grouped backward launch (see bwd_group): dgrad tiles, then wgrad (tile, split) blocks, then
@@ -594,12 +612,7 @@ __global__ void __launch_bounds__(GRP_THREADS) bwd_group_kernel(BwdGroupParams g
     return;
   }
   bid -= g.wg_blocks;
-  f32x4* part = reinterpret_cast<f32x4*>(smem);
-  switch (g.red_ws) {
-    case 16: slab_reduce_block<16, 8>(g.red, bid, g.nb_main, g.nb_bias, part); break;
-    case 8: slab_reduce_block<8, 8>(g.red, bid, g.nb_main, g.nb_bias, part); break;
-    default: slab_reduce_block<4, 8>(g.red, bid, g.nb_main, g.nb_bias, part); break;
-  }
+  slab_reduce_any(g.red_ws, g.red, bid, g.nb_main, g.nb_bias, reinterpret_cast<f32x4*>(smem));
 }
 
 // ------------------------------------------------------------------------------------------
@@ -648,6 +661,10 @@ void set_gemm_variant(int v) { g_variant = v; }
 
 template <int BM, int BN, int LA, int LB, int EPI, int ACT, bool BG>
 static hipError_t launch_t(GemmParams p, int splits, hipStream_t s) {
+  if constexpr (BM == 256 && BN == 256) {
+    // large shapes: 256x256 tile, 8 waves (each 128x64), 2-stage ring = 128 KiB LDS, 1 block/CU
+    return launch_dma<256, 256, 2, 4, 2, LA, LB, EPI, ACT, BG>(p, splits, s);
+  } else {
   if (gemm_impl() == 2) {
     if constexpr (BM == 128 && BN == 128) {
       switch (g_variant) {
@@ -675,6 +692,7 @@ static hipError_t launch_t(GemmParams p, int splits, hipStream_t s) {
   }
   hipLaunchKernelGGL(kfn, grid, dim3(GEMM_THREADS), smem, s, p);
   return hipGetLastError();
+  }
 }
 
 template <int BM, int BN, int LA, int LB, int EPI, bool BG>
@@ -691,7 +709,10 @@ void set_gemm_tile(int t) { g_force_tile = t; }
 
 static int pick_tile(int M, int N) {
   if (g_force_tile) return g_force_tile;
-  // 128x128 when that already yields ~a full wave of blocks, else 64x64.
+  // 256x256 once that alone fills the chip, 128x128 when that yields ~a full wave of blocks,
+  // else 64x64.
+  const long long t256 = (long long)((M + 255) / 256) * ((N + 255) / 256);
+  if (t256 >= 256 && gemm_impl() == 2) return 256;
   const long long t128 = (long long)((M + 127) / 128) * ((N + 127) / 128);
   return t128 >= 192 ? 128 : 64;
 }
@@ -702,7 +723,9 @@ hipError_t linear_fwd_bf16(const bf16* X, int ldx, const bf16* W, int ldw, const
   p.A = X; p.lda = ldx; p.B = W; p.ldb = ldw; p.M = M; p.N = N; p.K = K;
   p.k_per_split = ((K + GEMM_BK - 1) / GEMM_BK) * GEMM_BK;
   p.C = Y; p.ldc = ldy; p.bias = bias;
-  if (pick_tile(M, N) == 128) return launch_act<128, 128, KMAJ, KMAJ, EPI_BIAS_ACT, false>(p, act, 1, s);
+  const int t = pick_tile(M, N);
+  if (t == 256) return launch_act<256, 256, KMAJ, KMAJ, EPI_BIAS_ACT, false>(p, act, 1, s);
+  if (t == 128) return launch_act<128, 128, KMAJ, KMAJ, EPI_BIAS_ACT, false>(p, act, 1, s);
   return launch_act<64, 64, KMAJ, KMAJ, EPI_BIAS_ACT, false>(p, act, 1, s);
 }
 
@@ -713,12 +736,16 @@ hipError_t linear_dgrad_bf16(const bf16* dZ, int lddz, const bf16* W, int ldw, c
   p.A = dZ; p.lda = lddz; p.B = W; p.ldb = ldw; p.M = M; p.N = N; p.K = K;
   p.k_per_split = ((K + GEMM_BK - 1) / GEMM_BK) * GEMM_BK;
   p.C = dX; p.ldc = lddx; p.aux = Aprev; p.ldaux = lda_prev;
-  if (pick_tile(M, N) == 128) return launch_act<128, 128, KMAJ, XMAJ, EPI_DACT, false>(p, act, 1, s);
+  const int t = pick_tile(M, N);
+  if (t == 256) return launch_act<256, 256, KMAJ, XMAJ, EPI_DACT, false>(p, act, 1, s);
+  if (t == 128) return launch_act<128, 128, KMAJ, XMAJ, EPI_DACT, false>(p, act, 1, s);
   return launch_act<64, 64, KMAJ, XMAJ, EPI_DACT, false>(p, act, 1, s);
 }
 
 static int wgrad_tile(int M, int N) {
   if (g_force_tile) return g_force_tile;
+  const long long t256 = (long long)((M + 255) / 256) * ((N + 255) / 256);
+  if (t256 >= 256 && gemm_impl() == 2) return 256;
   return (M >= 128 && N >= 128) ? 128 : 64;
 }
 
@@ -774,8 +801,11 @@ hipError_t linear_wgrad_bf16_deferred(const bf16* dZ, int lddz, const bf16* X, i
   const int splits = make_wgrad(a, p, r);
   if (splits > 1 && ws == nullptr) return hipErrorInvalidValue;
   hipError_t e;
-  if (wgrad_tile(M, N) == 128) e = db ? launch_t<128, 128, XMAJ, XMAJ, EPI_F32, ACT_NONE, true>(p, splits, s)
-                                     : launch_t<128, 128, XMAJ, XMAJ, EPI_F32, ACT_NONE, false>(p, splits, s);
+  const int wt = wgrad_tile(M, N);
+  if (wt == 256) e = db ? launch_t<256, 256, XMAJ, XMAJ, EPI_F32, ACT_NONE, true>(p, splits, s)
+                        : launch_t<256, 256, XMAJ, XMAJ, EPI_F32, ACT_NONE, false>(p, splits, s);
+  else if (wt == 128) e = db ? launch_t<128, 128, XMAJ, XMAJ, EPI_F32, ACT_NONE, true>(p, splits, s)
+                             : launch_t<128, 128, XMAJ, XMAJ, EPI_F32, ACT_NONE, false>(p, splits, s);
   else e = db ? launch_t<64, 64, XMAJ, XMAJ, EPI_F32, ACT_NONE, true>(p, splits, s)
               : launch_t<64, 64, XMAJ, XMAJ, EPI_F32, ACT_NONE, false>(p, splits, s);
   if (e != hipSuccess) return e;
@@ -806,14 +836,19 @@ hipError_t gemm_bf16_generic(const bf16* A, int lda, int la, const bf16* B, int 
 }
 
 static int slab_ws(const SlabReduce& r) {
-  if (r.S >= 64 || r.n_loss_part >= 4096) return 16;
-  return r.S >= 8 ? 8 : 4;
+  // ~8 independent loads per lane: WS = S / 8 rounded up to a power of two, in [1, 16]
+  int ws = 1;
+  while (ws < 16 && ws * 8 < r.S) ws *= 2;
+  return ws;
 }
 
+static int slab_cols(int ws) { return ws >= SLAB_NW ? 64 : 64 * (SLAB_NW / ws); }
+
 static void slab_blocks(const SlabReduce& r, int& nb_main, int& nb_bias, int& nb) {
+  const int cols = slab_cols(slab_ws(r));
   const long long nvec = (r.ws && r.out && r.S > 0) ? (long long)r.M * (r.N / 4) : 0;
-  nb_main = (int)((nvec + 63) / 64);
-  nb_bias = (r.bws && r.bout && r.S > 0) ? (r.M + 63) / 64 : 0;
+  nb_main = (int)((nvec + cols - 1) / cols);
+  nb_bias = (r.bws && r.bout && r.S > 0) ? (r.M + cols - 1) / cols : 0;
   nb = nb_main + nb_bias + (r.loss_out ? 1 : 0);
 }
 
@@ -821,10 +856,13 @@ hipError_t slab_reduce(const SlabReduce& r, hipStream_t s) {
   int nb_main, nb_bias, nb;
   slab_blocks(r, nb_main, nb_bias, nb);
   if (nb == 0) return hipSuccess;
+  const dim3 g(nb), t(SLAB_THREADS);
   switch (slab_ws(r)) {
-    case 16: hipLaunchKernelGGL(slab_reduce_kernel<16>, dim3(nb), dim3(64 * 16), 0, s, r, nb_main, nb_bias); break;
-    case 8: hipLaunchKernelGGL(slab_reduce_kernel<8>, dim3(nb), dim3(64 * 8), 0, s, r, nb_main, nb_bias); break;
-    default: hipLaunchKernelGGL(slab_reduce_kernel<4>, dim3(nb), dim3(64 * 4), 0, s, r, nb_main, nb_bias); break;
+    case 1: hipLaunchKernelGGL(slab_reduce_kernel<1>, g, t, 0, s, r, nb_main, nb_bias); break;
+    case 2: hipLaunchKernelGGL(slab_reduce_kernel<2>, g, t, 0, s, r, nb_main, nb_bias); break;
+    case 4: hipLaunchKernelGGL(slab_reduce_kernel<4>, g, t, 0, s, r, nb_main, nb_bias); break;
+    case 8: hipLaunchKernelGGL(slab_reduce_kernel<8>, g, t, 0, s, r, nb_main, nb_bias); break;
+    default: hipLaunchKernelGGL(slab_reduce_kernel<16>, g, t, 0, s, r, nb_main, nb_bias); break;
   }
   return hipGetLastError();
 }

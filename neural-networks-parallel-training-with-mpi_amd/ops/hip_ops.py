@@ -59,6 +59,13 @@ class HipOps:
                                       a_prev.stride(0), _p(out), out.stride(0), M, N, K,
                                       ACT_CODES[act], self.stream)
 
+    @staticmethod
+    def _check_ws(ws, need: int, what: str):
+        """Host-side guard: a split-K workspace smaller than the launch needs would be written
+        out of bounds by the kernel (a GPU memory fault), so refuse the launch instead."""
+        have = 0 if ws is None else ws.numel() * ws.element_size()
+        _check(have >= int(need), f"{what} workspace too small: {have} < {int(need)} bytes")
+
     def wgrad_workspace_bytes(self, rows, out_f, in_f, dtype) -> int:
         if dtype == torch.bfloat16:
             return int(self.lib.wgrad_workspace_bytes(out_f, in_f, rows))
@@ -79,9 +86,11 @@ class HipOps:
         N = x.shape[1]
         if dz.dtype == torch.bfloat16:
             _check(M % 8 == 0 and N % 8 == 0, f"bf16 wgrad needs out%8==0, in%8==0 ({M}, {N})")
+            self._check_ws(ws, self.lib.wgrad_workspace_bytes(M, N, rows), "wgrad")
             self.lib.linear_wgrad_bf16(_p(dz), dz.stride(0), _p(x), x.stride(0), _p(gW), _p(gb),
                                        M, N, rows, _p(ws), self.stream, sgd)
         else:
+            self._check_ws(ws, self.lib.wgrad_f32_workspace_bytes(M, N, rows), "wgrad")
             self.lib.linear_wgrad_f32(_p(dz), dz.stride(0), _p(x), x.stride(0), _p(gW), _p(gb),
                                       M, N, rows, _p(ws), self.stream)
 
@@ -107,6 +116,7 @@ class HipOps:
         out_f = W.shape[0]
         _check(in_f % 8 == 0, f"head needs in%8==0 (in={in_f})")
         parts, off = self._head_split(rows, in_f)
+        self._check_ws(ws, self.head_workspace_bytes(rows, in_f, out_f), "head")
         lp = ws[:parts]
         wws = ws[off:]
         a_bf16 = 1 if a.dtype == torch.bfloat16 else 0
@@ -129,6 +139,7 @@ class HipOps:
         """Fused regression head whose slab combine is deferred (returned, see bwd_group)."""
         rows, in_f = a.shape
         parts, off = self._head_split(rows, in_f)
+        self._check_ws(ws, self.head_workspace_bytes(rows, in_f, 1), "head")
         a_bf16 = 1 if a.dtype == torch.bfloat16 else 0
         return self.lib.head_fused_deferred(_p(a), a_bf16, rows, in_f, _p(W), _p(b), _p(y),
                                             float(inv_count), ACT_CODES[act_prev], _p(dz_out),
@@ -152,6 +163,7 @@ class HipOps:
             rows, M = dz.shape
             N = x.shape[1]
             _check(dz.dtype == torch.bfloat16 and M % 8 == 0 and N % 8 == 0, "bf16 wgrad shapes")
+            self._check_ws(ws, self.lib.wgrad_workspace_bytes(M, N, rows), "wgrad")
             wg = (_p(dz), dz.stride(0), _p(x), x.stride(0), _p(gW), _p(gb), M, N, rows, _p(ws))
         return self.lib.bwd_group(dg, wg, sgd, pending, self.stream)
 

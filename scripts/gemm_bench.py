@@ -66,6 +66,10 @@ def main():
                 lib.set_gemm_impl(max(impl[0], 1))
                 lib.set_gemm_tile(impl[1])
                 lib.set_gemm_variant(impl[2])
+                # the split-K workspace depends on the (forced) tile: size it for THIS config
+                need = ops.wgrad_workspace_bytes(R, N, K, torch.bfloat16) // 4 + 64
+                if ws.numel() < need:
+                    ws = torch.empty(need, device=dev)
                 fn()
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()

@@ -44,6 +44,12 @@ for s in $STEPS; do
         ok_or_stop $? "bench ungrouped"
       done
       cat gpurun_out/ab_group.json ;;
+    gemmwide)
+      timeout -k 10 300 python scripts/gemm_bench.py --rows 4096 --inf 8192 --outf 8192 --rounds 3 --iters 5 --impls 0,2 --tiles 0,128,256 > gpurun_out/gemm_wide.json 2> gpurun_out/gemm_wide.err
+      ok_or_stop $? gemmwide
+      timeout -k 10 300 python scripts/gemm_bench.py --rows 8192 --inf 1024 --outf 1024 --rounds 5 --iters 10 --impls 0,2 --tiles 0,128,256 >> gpurun_out/gemm_wide.json 2>> gpurun_out/gemm_wide.err
+      ok_or_stop $? gemmmnist
+      cat gpurun_out/gemm_wide.json ;;
     benchall)
       for c in proxy512 mnist wide8192 ref; do
         timeout -k 10 300 python bench.py --config $c --steps 50 --warmup 5 >> gpurun_out/bench_all.json 2>> gpurun_out/bench_all.err

@@ -161,3 +161,40 @@ def test_sgd_matches_torch_optim(first, nesterov, wd, damp):
     torch.testing.assert_close(ar.momentum, opt.state[p]["momentum_buffer"], rtol=1e-6, atol=1e-6)
     assert torch.equal(ar.shadow, ar.master.to(torch.bfloat16))
     assert torch.count_nonzero(ar.grad) == 0
+
+
+@pytest.mark.parametrize("tile", [256, 128])
+@pytest.mark.parametrize("M,N,K", [(600, 520, 200), (4096, 1024, 512)])
+def test_forced_tile_fwd_dgrad_wgrad(tile, M, N, K):
+    """Every MLP GEMM orientation through a forced tile edge (256x256: the large-shape path),
+    ragged M/N/K tails included."""
+    from nnmpi_amd.ops.hip_ops import HipOps
+    from nnmpi_amd.ops.torch_ops import TorchOps
+    lib = _lib()
+    ops, tops = HipOps(), TorchOps(DEV)
+    x = _rand(M, K, seed=11).to(torch.bfloat16)
+    W = _rand(N, K, seed=12, scale=0.05).to(torch.bfloat16)
+    b = _rand(N, seed=13)
+    dz = _rand(M, N, seed=14).to(torch.bfloat16)
+    lib.set_gemm_tile(tile)
+    try:
+        out = torch.empty(M, N, device=DEV, dtype=torch.bfloat16)
+        ops.linear_act(x, W, b, "relu", out)
+        dx = torch.empty(M, K, device=DEV, dtype=torch.bfloat16)
+        ops.linear_dgrad(dz, W, x, "tanh", dx)
+        gW, gb = torch.empty(N, K, device=DEV), torch.empty(N, device=DEV)
+        ws = torch.empty(ops.wgrad_workspace_bytes(M, N, K, torch.bfloat16) // 4 + 64, device=DEV)
+        ops.linear_wgrad(dz, x, gW, gb, ws=ws)
+        torch.cuda.synchronize()
+    finally:
+        lib.set_gemm_tile(0)
+    ref = torch.empty_like(out)
+    tops.linear_act(x, W, b, "relu", ref)
+    torch.testing.assert_close(out.float(), ref.float(), rtol=2e-2, atol=2e-2)
+    rdx = torch.empty_like(dx)
+    tops.linear_dgrad(dz, W, x, "tanh", rdx)
+    torch.testing.assert_close(dx.float(), rdx.float(), rtol=2e-2, atol=2e-2)
+    rgW, rgb = torch.empty_like(gW), torch.empty_like(gb)
+    tops.linear_wgrad(dz, x, rgW, rgb)
+    torch.testing.assert_close(gW, rgW, rtol=1e-3, atol=2e-2)
+    torch.testing.assert_close(gb, rgb, rtol=1e-3, atol=2e-2)
