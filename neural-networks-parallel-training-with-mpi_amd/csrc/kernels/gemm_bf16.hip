@@ -52,6 +52,14 @@ struct GemmParams {
   unsigned a_bytes, b_bytes;  // extents of A / B storage (buffer-resource range, DMA path)
 };
 
+// s_waitcnt with only the vector-memory counter constrained (lgkm/exp counters left free).
+__device__ __forceinline__ constexpr int waitcnt_vm(int n) {
+  return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8);
+}
+
+template <int N>
+__device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(waitcnt_vm(N)); }
+
 // XOR swizzle of the 16-byte chunk index for XMAJ images (rows of BX bf16).
 template <int BX>
 __device__ __forceinline__ int swz_x(int k) {
@@ -137,21 +145,40 @@ __device__ __forceinline__ bf16x8 read_frag(const char* lds, int xb, int kk, int
   }
 }
 
+// read_frag for kernels that retire their LDS reads themselves (explicit lgkmcnt(0) +
+// sched_barrier before the consumers): the transposed reads are issued as inline asm, because
+// for the ds_read_b64_tr_b16 builtin the compiler cannot prove independence from in-flight
+// LDS-DMA writes and drains them with a vmcnt(0) in front of every such read, which would
+// serialise the DMA pipeline.
+template <int BX, int LAYOUT>
+__device__ __forceinline__ bf16x8 read_frag_async(const char* lds, int xb, int kk, int lane) {
+  if constexpr (LAYOUT == KMAJ) {
+    return read_frag<BX, LAYOUT>(lds, xb, kk, lane);
+  } else {
+    const int q = (lane & 15) >> 2, p = lane & 3;
+    const int k = kk * 32 + 8 * (lane >> 4) + q;
+    const int x = xb + 4 * p;
+    const unsigned a0 = (unsigned)(uintptr_t)(lds + xmaj_off<BX, LAYOUT>(k, x));
+    const unsigned a1 = (unsigned)(uintptr_t)(lds + xmaj_off<BX, LAYOUT>(k + 4, x));
+    typedef __attribute__((ext_vector_type(2))) unsigned u32x2;
+    u32x2 lo, hi;
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(lo) : "v"(a0));
+    asm volatile("ds_read_b64_tr_b16 %0, %1" : "=v"(hi) : "v"(a1));
+    typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+    u32x4 v = {lo[0], lo[1], hi[0], hi[1]};
+    return __builtin_bit_cast(bf16x8, v);
+  }
+}
+
 // Epilogue shared by both main loops: lane holds C[m][n..n+3] for each (i, j) fragment.
 // All epilogue operands (bias, activation aux) are loaded up front, then every fragment is
 // finished and stored: no load waits behind the stores (stores count in vmcnt on gfx950).
-template <int BM, int BN, int WGM, int WGN, int EPI, int ACT, bool BIASGRAD>
-__device__ __forceinline__ void gemm_epilogue(const GemmParams& p,
-                                              f32x4 (&acc)[BM / WGM / 16][BN / WGN / 16],
-                                              f32x4 (&accb)[BM / WGM / 16], bool do_bg, int m0, int n0,
-                                              int wm, int wn, int lane, int split) {
-  constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 16, NJ = WN / 16;
-  int mrow[MI];
-  int ncol[NJ];
-#pragma unroll
-  for (int i = 0; i < MI; ++i) mrow[i] = m0 + wm * WM + i * 16 + (lane & 15);
-#pragma unroll
-  for (int j = 0; j < NJ; ++j) ncol[j] = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
+// mrow[i]: this lane's output row of fragment row i; ncol[j]: first of its 4 output columns of
+// fragment column j.
+template <int MI, int NJ, int EPI, int ACT, bool BIASGRAD>
+__device__ __forceinline__ void epilogue_store(const GemmParams& p, f32x4 (&acc)[MI][NJ],
+                                               f32x4 (&accb)[MI], bool do_bg, const int (&mrow)[MI],
+                                               const int (&ncol)[NJ], int lane, int split) {
   if constexpr (EPI == EPI_BIAS_ACT) {
     f32x4 bias[NJ];
     // unconditional (clamped) loads: no per-element branch -> no vmcnt(0) per element
@@ -162,6 +189,11 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p,
 #pragma unroll
       for (int j = 0; j < NJ; ++j) bias[j] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    // Retire the operand loads explicitly BEFORE the first store: stores count in vmcnt too,
+    // and behind the predicated (branchy) store sequence the compiler's own count goes
+    // conservative -- it otherwise emits vmcnt(0/1) in front of every store, serialising
+    // each store behind the previous one's completion.
+    wait_vm<0>();
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       if (mrow[i] >= p.M) continue;
@@ -183,6 +215,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p,
       for (int j = 0; j < NJ; ++j)
         aux[i][j] = *reinterpret_cast<const bf16x4*>(p.aux + (long long)min(mrow[i], p.M - 1) * p.ldaux +
                                                      min(ncol[j], p.N - 4));
+    wait_vm<0>();   // see EPI_BIAS_ACT
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       if (mrow[i] >= p.M) continue;
@@ -208,14 +241,31 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p,
     }
   }
   if constexpr (BIASGRAD) {
+    // accb[i] = rowsum(A) of fragment row i; lane l < 16 holds the sum of row mrow[i] (= base + l)
     if (do_bg && (lane >> 4) == 0) {
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
-        const int m = m0 + wm * WM + i * 16 + lane;
+        const int m = mrow[i];
         if (m < p.M) p.bias_grad[split * p.bg_split_stride + m] = accb[i][0];
       }
     }
   }
+}
+
+// Standard wave-grid epilogue: wave (wm, wn) owns the contiguous WM x WN sub-tile.
+template <int BM, int BN, int WGM, int WGN, int EPI, int ACT, bool BIASGRAD>
+__device__ __forceinline__ void gemm_epilogue(const GemmParams& p,
+                                              f32x4 (&acc)[BM / WGM / 16][BN / WGN / 16],
+                                              f32x4 (&accb)[BM / WGM / 16], bool do_bg, int m0, int n0,
+                                              int wm, int wn, int lane, int split) {
+  constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 16, NJ = WN / 16;
+  int mrow[MI];
+  int ncol[NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) mrow[i] = m0 + wm * WM + i * 16 + (lane & 15);
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) ncol[j] = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
+  epilogue_store<MI, NJ, EPI, ACT, BIASGRAD>(p, acc, accb, do_bg, mrow, ncol, lane, split);
 }
 
 template <int BM, int BN, int LA, int LB, int EPI, int ACT, bool BIASGRAD>
@@ -310,12 +360,6 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_kernel(GemmParams p) {
 // ------------------------------------------------------------------------------------------
 constexpr unsigned DMA_OOB = 0x7FFFFFF0u;
 
-__device__ __forceinline__ constexpr int waitcnt_vm(int n) {
-  return (n & 15) | ((n >> 4) << 14) | (7 << 4) | (15 << 8);
-}
-
-template <int N>
-__device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(waitcnt_vm(N)); }
 
 template <int BX, int LAYOUT, int NW>
 struct DmaPlan {
@@ -459,6 +503,191 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_dma_kernel(GemmParam
   const int gx = gridDim.x, gy = gridDim.y;
   const int bid = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy);
   dma_gemm_tile<BM, BN, WGM, WGN, LA, LB, EPI, ACT, BIASGRAD, NS>(p, smem, bid % gx, bid / gx, blockIdx.z);
+}
+
+// ------------------------------------------------------------------------------------------
+// Large-shape kernel: 256x256 tile, 8 waves as 2 (M) x 4 (N), "ping-pong" phase schedule
+// (cdna_hip_programming.md §5, 256² 8-phase template; structure re-derived here for our operand
+// layouts).
+//
+// Each operand's K-tile is split into two HALVES of 128 contiguous x (A rows / B columns) x 64
+// k: every half is an ordinary 128-wide swizzled image (16 KiB, full 128-B source lines for
+// both operand layouts), filled by DmaPlan<128>.  Wave (wm, wn) owns rows
+// {h*128 + wm*64 + [0, 64)} and columns {h*128 + wn*32 + [0, 32)} of both halves h, so its
+// 128x64 output splits into four 64x32 QUADRANTS (A half, B half), computed in four PHASES
+// per K-tile: P1 (A0, B0), P2 (A0, B1), P3 (A1, B1), P4 (A1, B0).  Every half is read into
+// registers ONCE per K-tile -- P1 A0, P2 B1, P3 A1, P4 the NEXT K-tile's B0 (second register
+// set) -- so the memory sections are balanced (8 | 4 | 8 | 4 fragment reads); then the phase
+// issues its share of LDS-DMA for later K-tiles and runs its 16 MFMAs at raised priority.
+// Wave row 1 runs one barrier behind wave row 0, so on every SIMD one wave's memory section
+// overlaps the other's MFMA section.
+//
+// LDS: 2 K-tile buffers x {A0, A1, B0, B1} x 16 KiB = 128 KiB.  While computing K-tile t:
+// P1 issues A1(t+1), P3 A0(t+2) + B0(t+2), P4 B1(t+2) -- each half restaged two phases after
+// its single read (WAR) and issued ~six phases before it is read.  Before each barrier a
+// counted `vmcnt` retires exactly the half the NEXT phase reads (RAW: "read a staged buffer one
+// phase AFTER the wait that retires it").  Past the end of K the DMAs carry an out-of-range
+// offset (zero fill, no traffic) so every wave's vmcnt arithmetic stays uniform.
+// ------------------------------------------------------------------------------------------
+constexpr int PP_HALF = 16384;             // bytes of one half image
+constexpr int PP_BUF = 4 * PP_HALF;        // one K-tile: A0 A1 B0 B1
+constexpr int PP_SMEM = 2 * PP_BUF;        // 128 KiB
+constexpr int PP_THREADS = 512;
+
+template <int LA, int LB, int EPI, int ACT, bool BIASGRAD>
+__global__ void __launch_bounds__(PP_THREADS) gemm_bf16_pp256_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  constexpr int BK = GEMM_BK;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 2, wn = w & 3;
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int bid = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy);
+  const int tx = bid % gx, ty = bid / gx;
+  const int split = blockIdx.z;
+  const int m0 = ty * 256, n0 = tx * 256;
+  const int kbeg = split * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int nt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)p.b_bytes, 0x00020000);
+  DmaPlan<128, LA, 8> pa0, pa1;
+  DmaPlan<128, LB, 8> pb0, pb1;
+  pa0.init(w, lane, m0, p.M, p.lda);
+  pa1.init(w, lane, m0 + 128, p.M, p.lda);
+  pb0.init(w, lane, n0, p.N, p.ldb);
+  pb1.init(w, lane, n0 + 128, p.N, p.ldb);
+  auto A0 = [&](int b) { return smem + b * PP_BUF; };
+  auto A1 = [&](int b) { return smem + b * PP_BUF + PP_HALF; };
+  auto B0 = [&](int b) { return smem + b * PP_BUF + 2 * PP_HALF; };
+  auto B1 = [&](int b) { return smem + b * PP_BUF + 3 * PP_HALF; };
+  auto kof = [&](int t) { return kbeg + t * BK; };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float rsum[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rsum[i] = 0.f;
+  const bool do_bg = BIASGRAD && tx == 0 && wn == 0;
+
+  // prologue: K-tile 0 whole, K-tile 1's A0, B0, B1 (the steady-state issue order); retire
+  // K-tile 0's A0 + B0 (five newer halves may stay in flight)
+  pa0.issue(rsA, A0(0), w, kof(0), kend);
+  pb0.issue(rsB, B0(0), w, kof(0), kend);
+  pb1.issue(rsB, B1(0), w, kof(0), kend);
+  pa1.issue(rsA, A1(0), w, kof(0), kend);
+  pa0.issue(rsA, A0(1), w, kof(1), kend);
+  pb0.issue(rsB, B0(1), w, kof(1), kend);
+  pb1.issue(rsB, B1(1), w, kof(1), kend);
+  wait_vm<10>();
+  __builtin_amdgcn_s_barrier();
+
+  bf16x8 af[4][2], b0f[2][2], b0n[2][2], b1f[2][2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) b0n[jj][kk] = read_frag_async<128, LB>(B0(0), wn * 32 + jj * 16, kk, lane);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  if (wm == 1) __builtin_amdgcn_s_barrier();   // wave row 1 runs one barrier behind
+
+  for (int t = 0; t < nt; ++t) {
+    const int b = t & 1, nb = b ^ 1;
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      // ---- memory section: new fragments, DMA, retire the half the next phase reads ----
+      // Every half is read ONCE per K-tile: P1 A0, P2 B1, P3 A1, P4 B0 of the NEXT K-tile
+      // (into a second register set; this K-tile's B0 is still needed by P4's MFMAs).
+      if (ph == 0 || ph == 2) {
+        const char* ai = ph ? A1(b) : A0(b);
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) af[i][kk] = read_frag_async<128, LA>(ai, wm * 64 + i * 16, kk, lane);
+      }
+      if (ph == 0) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) b0f[jj][kk] = b0n[jj][kk];
+      } else if (ph == 1) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) b1f[jj][kk] = read_frag_async<128, LB>(B1(b), wn * 32 + jj * 16, kk, lane);
+      } else if (ph == 3) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) b0n[jj][kk] = read_frag_async<128, LB>(B0(nb), wn * 32 + jj * 16, kk, lane);
+      }
+      // issue: P1 A1(t+1) | P3 A0(t+2), B0(t+2) | P4 B1(t+2); retire: P1 -> B1(t) [vmcnt 10],
+      // P2 -> A1(t) [8], P3 -> A0 + B0 (t+1) [8] (read in P4 and in the next P1)
+      if (ph == 0) {
+        pa1.issue(rsA, A1(nb), w, kof(t + 1), kend);
+        wait_vm<10>();
+      } else if (ph == 1) {
+        wait_vm<8>();
+      } else if (ph == 2) {
+        pa0.issue(rsA, A0(b), w, kof(t + 2), kend);
+        pb0.issue(rsB, B0(b), w, kof(t + 2), kend);
+        wait_vm<8>();
+      } else {
+        pb1.issue(rsB, B1(b), w, kof(t + 2), kend);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      // ---- MFMA section: quadrant (hA, hB) ----
+      const int hA = ph >> 1;                        // P1,P2 -> A0; P3,P4 -> A1
+      const int hB = (ph == 1 || ph == 2) ? 1 : 0;   // P1,P4 -> B0; P2,P3 -> B1
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+            acc[hA * 4 + i][hB * 2 + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                hB ? b1f[jj][kk] : b0f[jj][kk], af[i][kk], acc[hA * 4 + i][hB * 2 + jj], 0, 0, 0);
+      if constexpr (BIASGRAD) {
+        // bias gradient = row sums of A: VALU partial sums of the A fragments this lane holds
+        // (rows lane&15, 16 of the 64 k), combined across the 4 lane groups at the end
+        if (do_bg && (ph == 0 || ph == 2)) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+              for (int e = 0; e < 8; ++e) rsum[hA * 4 + i] += (float)af[i][kk][e];
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();   // balance the stagger
+  wait_vm<0>();                                  // trailing out-of-range DMAs
+  f32x4 accb[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    float v = rsum[i];
+    if constexpr (BIASGRAD) {
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+    }
+    accb[i] = f32x4{v, v, v, v};
+  }
+  int mrow[8], ncol[4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) mrow[i] = m0 + (i >> 2) * 128 + wm * 64 + (i & 3) * 16 + (lane & 15);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ncol[j] = n0 + (j >> 1) * 128 + wn * 32 + (j & 1) * 16 + (lane >> 4) * 4;
+  epilogue_store<8, 4, EPI, ACT, BIASGRAD>(p, acc, accb, do_bg, mrow, ncol, lane, split);
 }
 
 // Deterministic split-K / partial-slab combine (the three jobs a backward needs), 512-thread
@@ -662,8 +891,18 @@ void set_gemm_variant(int v) { g_variant = v; }
 template <int BM, int BN, int LA, int LB, int EPI, int ACT, bool BG>
 static hipError_t launch_t(GemmParams p, int splits, hipStream_t s) {
   if constexpr (BM == 256 && BN == 256) {
-    // large shapes: 256x256 tile, 8 waves (each 128x64), 2-stage ring = 128 KiB LDS, 1 block/CU
-    return launch_dma<256, 256, 2, 4, 2, LA, LB, EPI, ACT, BG>(p, splits, s);
+    // large shapes: 256x256 tile, 8 waves (each 128x64), 128 KiB LDS, 1 block/CU
+    if (g_variant == 9) return launch_dma<256, 256, 2, 4, 2, LA, LB, EPI, ACT, BG>(p, splits, s);
+    dim3 grid((p.N + 255) / 256, (p.M + 255) / 256, splits);
+    set_extents<LA, LB>(p);
+    auto kfn = gemm_bf16_pp256_kernel<LA, LB, EPI, ACT, BG>;
+    static bool attr = false;
+    if (!attr) {
+      (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, PP_SMEM);
+      attr = true;
+    }
+    hipLaunchKernelGGL(kfn, grid, dim3(PP_THREADS), PP_SMEM, s, p);
+    return hipGetLastError();
   } else {
   if (gemm_impl() == 2) {
     if constexpr (BM == 128 && BN == 128) {

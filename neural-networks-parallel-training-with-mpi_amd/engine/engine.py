@@ -95,6 +95,11 @@ class MLPEngine:
         self._graphs: Dict[tuple, object] = {}
         self.inv_count = 1.0
         self.loss_scale = 1.0
+        self.timer = None   # utils.metrics.EventTimer: per-phase breakdown (steps run eagerly)
+
+    def _mark(self, name: str):
+        if self.timer is not None:
+            self.timer.mark(name, self.stream)
 
     # ------------------------------------------------------------------------------------
     def _validate(self):
@@ -177,9 +182,11 @@ class MLPEngine:
             return
         x = self.X[:rows]
         h = self._forward(x)
+        self._mark("fwd")
         last = L - 1
         dz = self._dzl(last - 1, rows) if L > 1 else None
         self._head(h, dz)
+        self._mark("head")
         self.sync.ready(last)
         for i in range(L - 2, -1, -1):
             x_in = self.acts[i - 1][:rows] if i > 0 else x
@@ -189,6 +196,7 @@ class MLPEngine:
                 dz_next = self._dzl(i - 1, rows)
                 ops.linear_dgrad(dz, ar.compute_weight(i), self.acts[i - 1][:rows], self.act, dz_next)
                 dz = dz_next
+        self._mark("bwd")
 
     def _forward(self, x):
         h = x
@@ -209,12 +217,16 @@ class MLPEngine:
                       self.loss_scale, ws=self.ws, **kw)
 
     def _step_body(self, first: bool):
+        self._mark("start")
         if self.overlap:
-            return self._step_body_overlap(first)
-        self.sync.begin()
-        self.forward_backward()
-        self.sync.finish()
-        self.ops.sgd(self.arena, self.hp, self.nesterov, first)
+            self._step_body_overlap(first)
+        else:
+            self.sync.begin()
+            self.forward_backward()
+            self.sync.finish()
+            self._mark("comm")
+            self.ops.sgd(self.arena, self.hp, self.nesterov, first)
+        self._mark("update")
 
     # ---------------- comm-overlapped schedule (GPU) -----------------------------------------
     # Compute stays on ONE stream (measured: splitting wgrad onto a side stream only adds
@@ -235,9 +247,11 @@ class MLPEngine:
         self._first = first
         x = self.X[:rows]
         h = self._forward(x)
+        self._mark("fwd")
         last = L - 1
         dz = self._dzl(last - 1, rows) if L > 1 else None
         self._head(h, dz)
+        self._mark("head")
         main.record_event(self.ev_wfree[last])
         self._layer_done(last, main)
         for i in range(L - 2, -1, -1):
@@ -249,7 +263,9 @@ class MLPEngine:
                 dz = dz_next
             main.record_event(self.ev_wfree[i])
             self._layer_done(i, main)
+        self._mark("bwd")
         self.sync.finish()   # joins the comm stream into main
+        self._mark("comm")
         rest = [b for b in ar.buckets if b.index not in self._sgd_done]
         if len(rest) == len(ar.buckets):
             ops.sgd(ar, self.hp, self.nesterov, first)      # one pass over the whole arena
@@ -265,6 +281,7 @@ class MLPEngine:
         fz = ops.sgd_fusion(ar, self.hp, self.nesterov, first)
         x = self.X[:rows]
         h = self._forward(x)
+        self._mark("fwd")
         last = L - 1
         dz = self._dzl(last - 1, rows) if L > 1 else None
         unfused = []
@@ -273,6 +290,7 @@ class MLPEngine:
         else:
             self._head(h, dz)
             unfused.append(last)
+        self._mark("head")
         for i in range(L - 2, -1, -1):
             x_in = self.acts[i - 1][:rows] if i > 0 else x
             dz_i = dz
@@ -286,6 +304,7 @@ class MLPEngine:
             else:
                 ops.linear_wgrad(dz_i, x_in, ar.grad_weight(i), ar.grad_bias(i), ws=self.ws)
                 unfused.append(i)
+        self._mark("bwd")
         for i in unfused:
             s, e = ar.layer_range[i]
             ops.sgd(ar, self.hp, self.nesterov, first, offset=s, numel=e - s)
@@ -300,6 +319,7 @@ class MLPEngine:
         fz = ops.sgd_fusion(ar, self.hp, self.nesterov, first) if self.fuse_sgd else None
         x = self.X[:rows]
         h = self._forward(x)
+        self._mark("fwd")
         last = L - 1
         dz = self._dzl(last - 1, rows)
         unfused = []
@@ -312,6 +332,7 @@ class MLPEngine:
             self._head(h, dz)
             pending = None
             unfused.append(last)
+        self._mark("head")
         for i in range(L - 2, -1, -1):
             x_in = self.acts[i - 1][:rows] if i > 0 else x
             dgrad = None
@@ -327,6 +348,7 @@ class MLPEngine:
                                             self.ws_pair[(last - i) % 2]),
                                     fz if fuse else None, pending)
         ops.slab_reduce(pending)
+        self._mark("bwd")
         if fz is not None:
             for i in unfused:
                 s, e = ar.layer_range[i]
@@ -336,6 +358,7 @@ class MLPEngine:
         for b in ar.buckets:
             self.sync.launch_bucket(b, self.stream)
         self.sync.finish()
+        self._mark("comm")
         ops.sgd(ar, self.hp, self.nesterov, first)
 
     def _layer_done(self, layer: int, stream):
@@ -359,7 +382,7 @@ class MLPEngine:
             self._step_body(first)
         else:
             with torch.cuda.stream(self.stream):
-                if first or not self.use_graph:
+                if first or not self.use_graph or self.timer is not None:
                     self._step_body(first)
                 else:
                     # scales are baked into the captured launches -> part of the key

@@ -57,6 +57,7 @@ class TrainResult:
     rows: int = 0
     epoch_times: List[float] = field(default_factory=list)
     steps: int = 0
+    phase_ms: Optional[dict] = None   # --profile_steps: mean ms per step per phase
 
 
 def dist_train(args) -> Optional[TrainResult]:
@@ -217,9 +218,11 @@ def make_sync(j: Job, arena: Arena):
             raise ValueError("--sync root is only provided on the torch.distributed path")
         inline = (cfg.comm_mode == "inline" or
                   (cfg.comm_mode == "auto" and arena.numel * 4 <= INLINE_MAX_GRAD_BYTES))
-        return NativeRcclSync(arena, j.native_comm, j.world, inline=inline)
+        return NativeRcclSync(arena, j.native_comm, j.world, inline=inline,
+                              grad_dtype=cfg.grad_dtype)
     group = j.pg.nccl if (j.device.type == "cuda" and j.pg.nccl is not None) else j.pg.gloo
-    return TorchDistSync(arena, group, j.world, mode=cfg.sync, overlap=cfg.overlap)
+    return TorchDistSync(arena, group, j.world, mode=cfg.sync, overlap=cfg.overlap,
+                         grad_dtype=cfg.grad_dtype)
 
 
 def make_ops(j: Job):
@@ -279,6 +282,9 @@ def _run(j: Job) -> TrainResult:
                     dampening=cfg.dampening, weight_decay=cfg.weight_decay,
                     nesterov=cfg.nesterov, use_graph=cfg.graph, overlap=cfg.overlap)
     eng.steps_done = steps_done
+    if cfg.profile_steps:
+        from ..utils.metrics import EventTimer
+        eng.timer = EventTimer(j.device.type)
     Xc = X.to(dtype)
     metrics = MetricsWriter(cfg.metrics_json if rank == 0 else None)
     seqchk = SequenceChecker(j.pg) if cfg.seqcheck else None
@@ -334,6 +340,11 @@ def _run(j: Job) -> TrainResult:
                 j.pg.barrier()
         eng.synchronize()
         res.steps = eng.steps_done
+        if eng.timer is not None:
+            res.phase_ms = eng.timer.summary_ms()
+            _print(cfg, rank, "[profile] mean ms per step: " +
+                   ", ".join(f"{k} {v:.4f}" for k, v in res.phase_ms.items()))
+            metrics.write(profile_ms_per_step=res.phase_ms, rank=rank)
         if cfg.checkpoint and rank == 0:
             ckpt.save(cfg.checkpoint, arena, cfg.nepochs, eng.steps_done, cfg)
         res.final_params = arena.flat_params_forward_order().detach().cpu().clone()

@@ -68,17 +68,26 @@ class NoSync(GradSync):
 
 
 class TorchDistSync(GradSync):
-    def __init__(self, arena, group, world: int, mode: str = "allreduce", overlap: bool = True):
+    """``grad_dtype="bf16"``: the payload is rounded to bf16 before and after the reduction
+    (the gloo/CPU rendition of the compressed all-reduce; the native path reduces in bf16)."""
+
+    def __init__(self, arena, group, world: int, mode: str = "allreduce", overlap: bool = True,
+                 grad_dtype: str = "fp32"):
         super().__init__(arena)
         self.group = group
         self.world = world
         self.mode = mode
-        self.overlap = overlap
+        self.overlap = overlap and grad_dtype == "fp32"
+        self.bf16 = grad_dtype == "bf16"
         self._works: List = []
+        self._rounded: List = []
 
     def _launch(self, bucket):
         view = self.arena.grad[bucket.offset:bucket.offset + bucket.numel]
         self.seq += 1
+        if self.bf16:
+            view.copy_(view.to(torch.bfloat16))
+            self._rounded.append(view)
         if self.mode == "root":
             # reference pattern: everything through rank 0 (reduce to root, then fan out)
             dist.reduce(view, dst=0, group=self.group)
@@ -92,6 +101,9 @@ class TorchDistSync(GradSync):
         for w in self._works:
             w.wait()
         self._works.clear()
+        for v in self._rounded:
+            v.copy_(v.to(torch.bfloat16))
+        self._rounded.clear()
 
 
 class NativeRcclSync(GradSync):
@@ -101,9 +113,14 @@ class NativeRcclSync(GradSync):
     several queues, so for small (latency-bound) gradient volumes the serial inline form is
     faster than overlap; large volumes use the overlapped comm stream."""
 
-    def __init__(self, arena, native_comm, world: int, priority: int = -1, inline: bool = False):
+    def __init__(self, arena, native_comm, world: int, priority: int = -1, inline: bool = False,
+                 grad_dtype: str = "fp32"):
         super().__init__(arena)
         self.inline = bool(inline)
+        # bf16 payload: half the bytes on xGMI (bandwidth-bound regime, e.g. the 8192-wide
+        # model); the gradient is cast into a bf16 staging arena before and back after the
+        # reduction, on the stream that owns that step.
+        self.bf16 = grad_dtype == "bf16"
         if self.inline and len(arena.buckets) > 1:
             # serial all-reduce: one call over the whole arena amortises the collective latency
             arena.buckets = arena._plan_buckets(float(1 << 62), 4)
@@ -113,18 +130,27 @@ class NativeRcclSync(GradSync):
         self.world = world
         self.gs = native.lib().GradSync(native_comm, len(arena.buckets), priority)
         self._launched = False
-
-        import torch
+        self.gbuf = (torch.empty(arena.numel, dtype=torch.bfloat16, device=arena.grad.device)
+                     if self.bf16 else None)
         self._comm_stream = torch.cuda.ExternalStream(self.gs.comm_stream)
 
     def _launch(self, bucket, stream=None):
         view = self.arena.grad[bucket.offset:bucket.offset + bucket.numel]
         self.seq += 1
         h = int(stream.cuda_stream) if stream is not None else self.native.stream_handle()
+        lib = self.native.lib()
+        ptr, dt = view.data_ptr(), 0
+        if self.bf16:
+            ptr, dt = self.gbuf[bucket.offset:].data_ptr(), 1
+            lib.cast_f32_bf16(view.data_ptr(), ptr, bucket.numel, h)
         if self.inline:
-            self.comm.allreduce(view.data_ptr(), bucket.numel, 0, 0, h)
+            self.comm.allreduce(ptr, bucket.numel, dt, 0, h)
+            if self.bf16:
+                lib.cast_bf16_f32(ptr, view.data_ptr(), bucket.numel, h)
             return
-        self.gs.bucket_ready(bucket.index, view.data_ptr(), bucket.numel, 0, h)
+        self.gs.bucket_ready(bucket.index, ptr, bucket.numel, dt, h)
+        if self.bf16:   # back to fp32 on the comm stream, ahead of the bucket's update there
+            lib.cast_bf16_f32(ptr, view.data_ptr(), bucket.numel, self.gs.comm_stream)
         self._launched = True
 
     def launch_bucket(self, bucket, stream):

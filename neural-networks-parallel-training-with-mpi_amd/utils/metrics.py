@@ -31,25 +31,44 @@ class MetricsWriter:
 
 
 class EventTimer:
-    """Named HIP-event intervals on a stream; read once at the end (no per-step host sync)."""
+    """Named device-side intervals of a step (HIP events on the engine's stream; on the CPU
+    path the ops are synchronous, so wall-clock marks).  Marks accumulate over steps and are
+    read once at the end (no per-step host sync): ``summary_ms()`` gives the mean time per
+    step of every consecutive phase pair, e.g. ``{"start->fwd": 0.031, "fwd->head": ...}``."""
 
-    def __init__(self, enabled: bool = True):
-        self.enabled = enabled and torch.cuda.is_available()
+    def __init__(self, device: str = "cuda"):
+        self.cuda = device.startswith("cuda") and torch.cuda.is_available()
         self.marks = []
+        self.steps = 0
 
     def mark(self, name: str, stream=None):
-        if not self.enabled:
-            return
-        e = torch.cuda.Event(enable_timing=True)
-        e.record(stream)
-        self.marks.append((name, e))
+        if self.cuda:
+            e = torch.cuda.Event(enable_timing=True)
+            e.record(stream)
+            self.marks.append((name, e))
+        else:
+            self.marks.append((name, time.perf_counter()))
+        if name == "start":
+            self.steps += 1
+
+    def _elapsed_ms(self, a, b) -> float:
+        return a.elapsed_time(b) if self.cuda else (b - a) * 1e3
 
     def intervals_ms(self):
+        """Total ms per phase pair over all recorded steps (pairs that cross a step boundary,
+        i.e. the host gap between steps, are skipped)."""
         if not self.marks:
             return {}
-        self.marks[-1][1].synchronize()
+        if self.cuda:
+            self.marks[-1][1].synchronize()
         out = {}
         for (n0, e0), (n1, e1) in zip(self.marks, self.marks[1:]):
+            if n1 == "start":
+                continue
             key = f"{n0}->{n1}"
-            out[key] = out.get(key, 0.0) + e0.elapsed_time(e1)
+            out[key] = out.get(key, 0.0) + self._elapsed_ms(e0, e1)
         return out
+
+    def summary_ms(self):
+        n = max(self.steps, 1)
+        return {k: v / n for k, v in self.intervals_ms().items()}

@@ -45,7 +45,7 @@ for s in $STEPS; do
       done
       cat gpurun_out/ab_group.json ;;
     gemmwide)
-      timeout -k 10 300 python scripts/gemm_bench.py --rows 4096 --inf 8192 --outf 8192 --rounds 3 --iters 5 --impls 0,2 --tiles 0,128,256 > gpurun_out/gemm_wide.json 2> gpurun_out/gemm_wide.err
+      timeout -k 10 300 python scripts/gemm_bench.py --rows 4096 --inf 8192 --outf 8192 --rounds 3 --iters 5 --impls 0,2 --tiles 0,128,256 --variants 0,9 > gpurun_out/gemm_wide.json 2> gpurun_out/gemm_wide.err
       ok_or_stop $? gemmwide
       timeout -k 10 300 python scripts/gemm_bench.py --rows 8192 --inf 1024 --outf 1024 --rounds 5 --iters 10 --impls 0,2 --tiles 0,128,256 >> gpurun_out/gemm_wide.json 2>> gpurun_out/gemm_wide.err
       ok_or_stop $? gemmmnist

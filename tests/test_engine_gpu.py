@@ -160,3 +160,20 @@ def test_grouped_backward_xent_head_bitwise_equal():
     b = _run_ungrouped(cfg)
     assert a.losses == b.losses
     assert torch.equal(a.final_params, b.final_params)
+
+
+@pytest.mark.parametrize("mode", ["inline", "overlap"])
+def test_native_rccl_bf16_gradient_payload(mode):
+    """bf16 all-reduce payload through the native communicator (cast kernels + ncclBfloat16),
+    inline and on the comm stream: tracks the fp32-payload run within bf16 rounding."""
+    a = trainer.run_worker(_cfg(device="cuda", comm="native", grad_dtype="bf16", comm_mode=mode,
+                                nepochs=5))
+    b = trainer.run_worker(_cfg(device="cuda", comm="native", comm_mode=mode, nepochs=5))
+    assert all(x == x for x in a.losses)
+    torch.testing.assert_close(a.final_params, b.final_params, rtol=2e-2, atol=1e-3)
+
+
+def test_profile_steps_gpu_breakdown():
+    res = trainer.run_worker(_cfg(device="cuda", nepochs=3, profile_steps=True))
+    assert {"start->fwd", "fwd->head", "head->bwd"} <= set(res.phase_ms)
+    assert res.phase_ms["start->fwd"] > 0

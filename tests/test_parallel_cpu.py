@@ -140,3 +140,14 @@ def test_self_spawn_cli():
                        timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "loss in worker 1: 2835.11" in r.stdout
+
+
+def test_bf16_gradient_payload_trains_close_to_fp32():
+    """--grad_dtype bf16: the all-reduce payload is rounded to bf16 (half the xGMI bytes);
+    replicas stay identical and the run tracks the fp32-payload run closely."""
+    cfg = dict(print_rank="none", n_samples=64, nepochs=5, lr=0.01)
+    a = run_ranks(TrainConfig(grad_dtype="bf16", **cfg), 2)
+    b = run_ranks(TrainConfig(grad_dtype="fp32", **cfg), 2)
+    assert torch.equal(a[0]["final"], a[1]["final"])
+    torch.testing.assert_close(a[0]["final"], b[0]["final"], rtol=2e-2, atol=2e-3)
+    assert not torch.equal(a[0]["final"], b[0]["final"])   # the rounding really happened

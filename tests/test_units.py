@@ -187,3 +187,14 @@ def test_sequence_checker_detects_mismatch():
             return [obj, (obj[0], obj[1] + 1)]
     with pytest.raises(CollectiveMismatch):
         SequenceChecker(FakePG()).check(0, 3)
+
+
+def test_profile_steps_phase_breakdown(capsys):
+    from nnmpi_amd.engine import trainer
+    cfg = TrainConfig(print_rank="all", widths=[20, 16, 1], n_features=20, n_samples=64,
+                      nepochs=3, profile_steps=True)
+    res = trainer.run_worker(cfg)
+    assert set(res.phase_ms) == {"start->fwd", "fwd->head", "head->bwd", "bwd->comm",
+                                 "comm->update"}
+    assert all(v >= 0 for v in res.phase_ms.values())
+    assert "[profile] mean ms per step" in capsys.readouterr().out
