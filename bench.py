@@ -59,6 +59,8 @@ def parse():
     p.add_argument("--no_group", action="store_true",
                    help="separate dgrad / wgrad / combine launches instead of the grouped one")
     p.add_argument("--even", action="store_true", help="no uneven extra rows")
+    p.add_argument("--graph_chunk", type=int, default=16,
+                   help="steps per replayed hipGraph (1 = one graph launch per step)")
     p.add_argument("--lr", type=float, default=1e-5)
     p.add_argument("--comm_mode", choices=["auto", "overlap", "inline"], default="auto",
                    help="overlap: comm stream + per-bucket SGD; inline: all-reduce on the compute "
@@ -153,13 +155,15 @@ def main():
         pg.barrier()
         torch.cuda.synchronize()
 
-    for _ in range(a.warmup):
-        eng.step()
+    # graph mode: steps replayed as hipGraphs of `chunk` complete consecutive steps (one
+    # replay's fixed cost per chunk); every graph is captured before the timed region
+    chunk = max(1, a.graph_chunk)
+    eng.run_steps(a.warmup, chunk)
+    eng.prepare_steps(a.steps, chunk)
     loss0 = eng.loss()
     barrier()
     t0 = time.perf_counter()
-    for _ in range(a.steps):
-        eng.step()
+    eng.run_steps(a.steps, chunk)
     eng.synchronize()
     torch.cuda.synchronize()
     t1 = time.perf_counter()
@@ -193,7 +197,8 @@ def main():
                        "parallelism": f"dp{world}", "rows_per_gpu": rows_pg,
                        "uneven_split": (not a.even and world > 1),
                        "comm": a.comm if (world > 1 or a.force_comm) else "none",
-                       "graph": not a.no_graph, "overlap": not a.no_overlap, "grouped": not a.no_group,
+                       "graph": not a.no_graph, "graph_chunk": a.graph_chunk, "overlap": not a.no_overlap,
+                       "grouped": not a.no_group,
                        "comm_mode": (("inline" if sync.inline else "overlap")
                                      if hasattr(sync, "inline") else None),
                        "bucket_mb": a.bucket_mb},

@@ -404,7 +404,11 @@ struct DmaPlan {
 
 // One output tile (tx, ty) of K-split `split` — the body shared by the standalone GEMM launch
 // and the grouped backward launch (bwd_group_kernel).
-template <int BM, int BN, int WGM, int WGN, int LA, int LB, int EPI, int ACT, bool BIASGRAD, int NS>
+// ASYNC_TR: transposed-operand fragments through asm reads + one explicit lgkmcnt per k-step
+// (more VGPRs: the whole stage's fragments are held at once).  The grouped backward launch keeps
+// the compiler-scheduled reads so it stays at 2 blocks per CU.
+template <int BM, int BN, int WGM, int WGN, int LA, int LB, int EPI, int ACT, bool BIASGRAD, int NS,
+          bool ASYNC_TR = true>
 __device__ __forceinline__ void dma_gemm_tile(const GemmParams& p, char* smem, int tx, int ty,
                                               int split) {
   constexpr int NW = WGM * WGN;
@@ -471,23 +475,54 @@ __device__ __forceinline__ void dma_gemm_tile(const GemmParams& p, char* smem, i
       db.issue(rsB, st + A_BYTES, w, kbeg + (t + NS - 1) * BK, kend);
     }
     const char* cur = smem + (t % NS) * STAGE;
+    if constexpr (ASYNC_TR && (LA == XMAJ || LB == XMAJ)) {
+      // transposed operands: all fragments of the stage through asm reads (read_frag_async),
+      // one explicit lgkmcnt(0), then the MFMAs -- keeps the compiler from draining the
+      // in-flight DMA ring (vmcnt(0)) in front of every ds_read_b64_tr_b16
+      bf16x8 af[MI][BK / 32], bfr[NJ][BK / 32];
 #pragma unroll
-    for (int kk = 0; kk < BK / 32; ++kk) {
-      bf16x8 af[MI], bfr[NJ];
+      for (int kk = 0; kk < BK / 32; ++kk) {
 #pragma unroll
-      for (int i = 0; i < MI; ++i) af[i] = read_frag<BM, LA>(cur, wm * WM + i * 16, kk, lane);
+        for (int i = 0; i < MI; ++i) af[i][kk] = read_frag_async<BM, LA>(cur, wm * WM + i * 16, kk, lane);
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) bfr[j] = read_frag<BN, LB>(cur + A_BYTES, wn * WN + j * 16, kk, lane);
+        for (int j = 0; j < NJ; ++j) bfr[j][kk] = read_frag_async<BN, LB>(cur + A_BYTES, wn * WN + j * 16, kk, lane);
+      }
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
-      for (int i = 0; i < MI; ++i)
+      for (int kk = 0; kk < BK / 32; ++kk) {
 #pragma unroll
-        for (int j = 0; j < NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-      if constexpr (BIASGRAD) {
-        if (do_bg) {
+        for (int i = 0; i < MI; ++i)
 #pragma unroll
-          for (int i = 0; i < MI; ++i)
-            accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[i], accb[i], 0, 0, 0);
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j][kk], af[i][kk], acc[i][j], 0, 0, 0);
+        if constexpr (BIASGRAD) {
+          if (do_bg) {
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+              accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[i][kk], accb[i], 0, 0, 0);
+          }
+        }
+      }
+    } else {
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        bf16x8 af[MI], bfr[NJ];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) af[i] = read_frag<BM, LA>(cur, wm * WM + i * 16, kk, lane);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bfr[j] = read_frag<BN, LB>(cur + A_BYTES, wn * WN + j * 16, kk, lane);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        if constexpr (BIASGRAD) {
+          if (do_bg) {
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+              accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[i], accb[i], 0, 0, 0);
+          }
         }
       }
     }
@@ -827,7 +862,7 @@ __global__ void __launch_bounds__(GRP_THREADS) bwd_group_kernel(BwdGroupParams g
   if (bid < g.dg_blocks) {
     const int l = xcd_remap(bid, g.dg_blocks);
     if (l >= g.dg_n) return;
-    dma_gemm_tile<GRP_BM, GRP_BN, GRP_WGM, GRP_WGN, KMAJ, XMAJ, EPI_DACT, ACT, false, GRP_NS>(
+    dma_gemm_tile<GRP_BM, GRP_BN, GRP_WGM, GRP_WGN, KMAJ, XMAJ, EPI_DACT, ACT, false, GRP_NS, false>(
         g.dg, smem, l % g.dg_gx, l / g.dg_gx, 0);
     return;
   }
@@ -836,7 +871,7 @@ __global__ void __launch_bounds__(GRP_THREADS) bwd_group_kernel(BwdGroupParams g
     const int l = xcd_remap(bid, g.wg_blocks);
     if (l >= g.wg_n) return;
     const int split = l / g.wg_tiles, t = l % g.wg_tiles;
-    dma_gemm_tile<GRP_BM, GRP_BN, GRP_WGM, GRP_WGN, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, GRP_NS>(
+    dma_gemm_tile<GRP_BM, GRP_BN, GRP_WGM, GRP_WGN, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, GRP_NS, false>(
         g.wg, smem, t % g.wg_gx, t / g.wg_gx, split);
     return;
   }

@@ -403,13 +403,59 @@ class MLPEngine:
                     g.launch(int(self.stream.cuda_stream))
         self.steps_done += 1
 
-    def _capture(self):
+    # ---------------- multi-step graphs ------------------------------------------------------
+    # A hipGraph replay has a fixed cost (~8 us measured between consecutive replays on MI355X,
+    # MI355X_MICROARCH.md "graph-replay-floor"), which is ~8 % of a 512-wide step.  When the
+    # host has nothing to do between steps (a timed loop, full-batch epochs without per-step
+    # output) the engine can replay graphs holding `chunk` complete consecutive steps.
+    def _chunks(self, n: int, chunk: int):
+        out = []
+        while n > 0:
+            c = min(chunk, n)
+            out.append(c)
+            n -= c
+        return out
+
+    def prepare_steps(self, n: int, chunk: int = 16):
+        """Capture (without running) every graph that run_steps(n, chunk) will replay."""
+        if not (self.is_cuda and self.use_graph and self.timer is None and self.steps_done > 0):
+            return
+        with torch.cuda.stream(self.stream):
+            for c in set(self._chunks(n, chunk)):
+                key = (self.rows, self.inv_count, self.loss_scale, c)
+                if key not in self._graphs:
+                    self._graphs[key] = self._capture(c)
+
+    def run_steps(self, n: int, chunk: int = 16):
+        """n optimizer steps (asynchronous on the GPU).  In graph mode the steps are replayed as
+        graphs of up to `chunk` consecutive steps; results are identical to n step() calls."""
+        if not (self.is_cuda and self.use_graph and self.timer is None):
+            for _ in range(n):
+                self.step()
+            return
+        if n > 0 and self.steps_done == 0:
+            self.step()          # eager first step (momentum initialisation semantics)
+            n -= 1
+        try:
+            self.prepare_steps(n, chunk)
+        except RuntimeError:
+            for _ in range(n):   # capture unavailable: step() falls back to eager by itself
+                self.step()
+            return
+        with torch.cuda.stream(self.stream):
+            for c in self._chunks(n, chunk):
+                self._graphs[(self.rows, self.inv_count, self.loss_scale, c)].launch(
+                    int(self.stream.cuda_stream))
+                self.steps_done += c
+
+    def _capture(self, nsteps: int = 1):
         from .. import native
         g = native.lib().GraphRunner()
         s = int(self.stream.cuda_stream)
         g.begin(s)
         try:
-            self._step_body(False)
+            for _ in range(nsteps):
+                self._step_body(False)
         except Exception:
             try:
                 g.end()

@@ -50,6 +50,12 @@ for s in $STEPS; do
       timeout -k 10 300 python scripts/gemm_bench.py --rows 8192 --inf 1024 --outf 1024 --rounds 5 --iters 10 --impls 0,2 --tiles 0,128,256 >> gpurun_out/gemm_wide.json 2>> gpurun_out/gemm_wide.err
       ok_or_stop $? gemmmnist
       cat gpurun_out/gemm_wide.json ;;
+    variants)
+      timeout -k 10 300 python scripts/gemm_bench.py --impls 2 --tiles 128 --variants 0,1,2,3,8 > gpurun_out/variants.json 2> gpurun_out/variants.err
+      ok_or_stop $? variants512
+      timeout -k 10 300 python scripts/gemm_bench.py --inf 1024 --outf 1024 --impls 2 --tiles 128 --variants 0,1,2,3,8 >> gpurun_out/variants.json 2>> gpurun_out/variants.err
+      ok_or_stop $? variants1024
+      cat gpurun_out/variants.json ;;
     benchall)
       for c in proxy512 mnist wide8192 ref; do
         timeout -k 10 300 python bench.py --config $c --steps 50 --warmup 5 >> gpurun_out/bench_all.json 2>> gpurun_out/bench_all.err

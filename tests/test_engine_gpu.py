@@ -177,3 +177,31 @@ def test_profile_steps_gpu_breakdown():
     res = trainer.run_worker(_cfg(device="cuda", nepochs=3, profile_steps=True))
     assert {"start->fwd", "fwd->head", "head->bwd"} <= set(res.phase_ms)
     assert res.phase_ms["start->fwd"] > 0
+
+
+def test_multi_step_graph_equals_single_steps():
+    """run_steps(n, chunk) replays graphs of `chunk` whole steps: bitwise equal to n step()s."""
+    outs = []
+    for chunk in (1, 3):
+        import torch as _t
+        from nnmpi_amd.engine.arena import Arena
+        from nnmpi_amd.engine.engine import MLPEngine
+        from nnmpi_amd.models.mlp import MLPSpec, reference_init
+        from nnmpi_amd.ops.hip_ops import HipOps
+        from nnmpi_amd.parallel.sync import NoSync
+        from nnmpi_amd.data import synth
+        widths = [256, 256, 256, 1]
+        spec = MLPSpec(tuple(widths), "relu", "mse")
+        ar = Arena([spec.layer_shape(i) for i in range(spec.n_layers)], "cuda",
+                   shadow_dtype=_t.bfloat16)
+        ar.bind_model(reference_init(widths, "relu", seed=0))
+        eng = MLPEngine(spec, ar, HipOps("cuda"), NoSync(ar), device="cuda", dtype=_t.bfloat16,
+                        rows_capacity=1024, lr=1e-4, momentum=0.9)
+        X, Y = synth.chunked_regression(0, 1024, 256, device="cuda")
+        eng.load_batch(X.to(_t.bfloat16), Y)
+        eng.set_scales(1 / 1024, 1 / 1024, 1.0)
+        eng.run_steps(10, chunk)
+        eng.synchronize()
+        outs.append(ar.master.clone())
+        assert eng.steps_done == 10
+    assert _t.equal(outs[0], outs[1])
