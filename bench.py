@@ -4,8 +4,11 @@ Config (BASELINE.json / BASELINE.md): the reference algorithm's 512-wide proxy â
 512 -> 512 -> 512 -> 512 -> 1 (ReLU, MSE), 8192 rows per GPU, full-shard batch (one optimizer
 step per epoch, as the reference's DataLoader does, ref.py:146), SGD momentum 0.9, bf16 compute
 with fp32 master weights; synthetic make_regression-style data generated on device, random
-init.  Weak scaling: every GPU keeps 8192 rows (plus one extra row on the first N-1 ranks so the
-split is uneven, BASELINE config 3), gradients are all-reduced over RCCL (xGMI) every step.
+init.  Weak scaling: every GPU keeps 8192 rows, except that with N > 1 the global row count is
+8192*N - 1, so the split is uneven (BASELINE config 3: the last rank holds one row less).  The
+short rank only leaves a partial last tile; a LONG rank (8192 + 1 rows) would add a whole extra
+row of GEMM tiles on that rank and, since the step time is the max over ranks, slow every rank
+down.  Gradients are all-reduced over RCCL (xGMI) every step.
 
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
@@ -67,6 +70,9 @@ def parse():
                         "stream (auto: inline when the gradient volume is small)")
     p.add_argument("--force_comm", action="store_true",
                    help="use the RCCL gradient path even with one rank (smoke-tests comm overlap)")
+    p.add_argument("--fwd_variant", type=int, default=-1, help="forward GEMM variant (experiments)")
+    p.add_argument("--group_async", type=int, default=-1,
+                   help="grouped-backward LDS read mode (experiments)")
     return p.parse_args()
 
 
@@ -89,6 +95,8 @@ def main():
 
     job = pdist.detect_job()
     rank, world = job.rank, job.world
+    native.lib().set_fwd_variant(a.fwd_variant)
+    native.lib().set_group_async(a.group_async)
     torch.cuda.set_device(job.local_rank % torch.cuda.device_count())
     dev = torch.device("cuda", torch.cuda.current_device())
     pg = pdist.ProcessGroupContext(job, 600.0, want_nccl=(a.comm == "torch" and world > 1))
@@ -97,7 +105,7 @@ def main():
     spec = MLPSpec(tuple(widths), "relu", c["loss"])
     rows_pg = a.rows or c["rows"]
     if a.scaling == "weak":
-        n_global = rows_pg * world + (0 if a.even else world - 1)
+        n_global = rows_pg * world - (0 if (a.even or world == 1) else 1)
     else:
         n_global = rows_pg
     part = partition_rows(n_global, world)

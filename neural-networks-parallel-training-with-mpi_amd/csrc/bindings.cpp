@@ -76,6 +76,9 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
   m.def("get_gemm_impl", &get_gemm_impl);
   m.def("set_gemm_tile", &set_gemm_tile);
   m.def("set_gemm_variant", &set_gemm_variant);
+  m.def("set_fwd_variant", &set_fwd_variant);
+  m.def("set_group_async", &set_group_async);
+  m.def("set_wgrad_splits", &set_wgrad_splits);
   m.def("wgrad_workspace_bytes", &wgrad_workspace_bytes);
   m.def("wgrad_splits", &wgrad_splits);
   m.def("linear_wgrad_bf16", [](uptr dZ, int lddz, uptr X, int ldx, uptr dW, uptr db, int M, int N,

@@ -404,11 +404,16 @@ struct DmaPlan {
 
 // One output tile (tx, ty) of K-split `split` — the body shared by the standalone GEMM launch
 // and the grouped backward launch (bwd_group_kernel).
-// ASYNC_TR: transposed-operand fragments through asm reads + one explicit lgkmcnt per k-step
-// (more VGPRs: the whole stage's fragments are held at once).  The grouped backward launch keeps
-// the compiler-scheduled reads so it stays at 2 blocks per CU.
+// ASYNC_TR (only matters when an operand is XMAJ, i.e. read with ds_read_b64_tr_b16):
+//   0  compiler-scheduled reads -- hipcc cannot prove the tr-read builtin independent of the
+//      in-flight LDS-DMA and drains vmcnt(0) in front of it, so the DMA ring degenerates to
+//      load-then-compute inside the block;
+//   1  the whole stage's fragments through asm reads + ONE explicit lgkmcnt per k-step (most
+//      VGPRs: every fragment of the stage is live at once);
+//   2  asm reads + explicit lgkmcnt per 32-deep k-half (half the fragment registers of 1, so
+//      the 512-thread grouped launch keeps 2 blocks per CU).
 template <int BM, int BN, int WGM, int WGN, int LA, int LB, int EPI, int ACT, bool BIASGRAD, int NS,
-          bool ASYNC_TR = true>
+          int ASYNC_TR = 1>
 __device__ __forceinline__ void dma_gemm_tile(const GemmParams& p, char* smem, int tx, int ty,
                                               int split) {
   constexpr int NW = WGM * WGN;
@@ -475,7 +480,31 @@ __device__ __forceinline__ void dma_gemm_tile(const GemmParams& p, char* smem, i
       db.issue(rsB, st + A_BYTES, w, kbeg + (t + NS - 1) * BK, kend);
     }
     const char* cur = smem + (t % NS) * STAGE;
-    if constexpr (ASYNC_TR && (LA == XMAJ || LB == XMAJ)) {
+    constexpr bool TR = (LA == XMAJ || LB == XMAJ);
+    if constexpr (ASYNC_TR == 2 && TR) {
+#pragma unroll
+      for (int kk = 0; kk < BK / 32; ++kk) {
+        bf16x8 af[MI], bfr[NJ];
+#pragma unroll
+        for (int i = 0; i < MI; ++i) af[i] = read_frag_async<BM, LA>(cur, wm * WM + i * 16, kk, lane);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bfr[j] = read_frag_async<BN, LB>(cur + A_BYTES, wn * WN + j * 16, kk, lane);
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+        if constexpr (BIASGRAD) {
+          if (do_bg) {
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+              accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[i], accb[i], 0, 0, 0);
+          }
+        }
+      }
+    } else if constexpr (ASYNC_TR == 1 && TR) {
       // transposed operands: all fragments of the stage through asm reads (read_frag_async),
       // one explicit lgkmcnt(0), then the MFMAs -- keeps the compiler from draining the
       // in-flight DMA ring (vmcnt(0)) in front of every ds_read_b64_tr_b16
@@ -855,14 +884,17 @@ constexpr int GRP_BM = 128, GRP_BN = 128, GRP_WGM = 2, GRP_WGN = 4, GRP_NS = 2;
 constexpr int GRP_THREADS = 64 * GRP_WGM * GRP_WGN;
 constexpr int GRP_SMEM = GRP_NS * (GRP_BM + GRP_BN) * GEMM_BK * 2;
 
-template <int ACT>
-__global__ void __launch_bounds__(GRP_THREADS) bwd_group_kernel(BwdGroupParams g) {
+// GA: LDS read mode of the two GEMM jobs (dma_gemm_tile ASYNC_TR).  Two 64 KiB / 512-thread
+// blocks per CU (4 waves per SIMD) is what lets one block's DMA wait hide behind the other's
+// MFMAs, so the register budget is pinned to 128 VGPRs (launch bound: 4 waves per SIMD).
+template <int ACT, int GA>
+__global__ void __launch_bounds__(GRP_THREADS, 4) bwd_group_kernel(BwdGroupParams g) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   int bid = blockIdx.x;
   if (bid < g.dg_blocks) {
     const int l = xcd_remap(bid, g.dg_blocks);
     if (l >= g.dg_n) return;
-    dma_gemm_tile<GRP_BM, GRP_BN, GRP_WGM, GRP_WGN, KMAJ, XMAJ, EPI_DACT, ACT, false, GRP_NS, false>(
+    dma_gemm_tile<GRP_BM, GRP_BN, GRP_WGM, GRP_WGN, KMAJ, XMAJ, EPI_DACT, ACT, false, GRP_NS, GA>(
         g.dg, smem, l % g.dg_gx, l / g.dg_gx, 0);
     return;
   }
@@ -871,7 +903,7 @@ __global__ void __launch_bounds__(GRP_THREADS) bwd_group_kernel(BwdGroupParams g
     const int l = xcd_remap(bid, g.wg_blocks);
     if (l >= g.wg_n) return;
     const int split = l / g.wg_tiles, t = l % g.wg_tiles;
-    dma_gemm_tile<GRP_BM, GRP_BN, GRP_WGM, GRP_WGN, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, GRP_NS, false>(
+    dma_gemm_tile<GRP_BM, GRP_BN, GRP_WGM, GRP_WGN, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, GRP_NS, GA>(
         g.wg, smem, t % g.wg_gx, t / g.wg_gx, split);
     return;
   }
@@ -923,11 +955,22 @@ static hipError_t launch_dma(GemmParams p, int splits, hipStream_t s) {
 static int g_variant = 0;
 void set_gemm_variant(int v) { g_variant = v; }
 
+// Kernel-selection knobs of the training step (scripts/step_ab.py A/Bs them; -1 / 0 = default).
+static int g_fwd_variant = -1;    // forward GEMM main-loop variant (launch_t's switch)
+static int g_group_async = -1;    // grouped-backward LDS read mode (dma_gemm_tile ASYNC_TR)
+static int g_wgrad_splits = 0;    // > 0: upper bound on the weight-gradient split-K factor
+constexpr int FWD_VARIANT_DEFAULT = 0;
+constexpr int GROUP_ASYNC_DEFAULT = 0;
+void set_fwd_variant(int v) { g_fwd_variant = v; }
+void set_group_async(int m) { g_group_async = m; }
+void set_wgrad_splits(int s) { g_wgrad_splits = s; }
+
 template <int BM, int BN, int LA, int LB, int EPI, int ACT, bool BG>
-static hipError_t launch_t(GemmParams p, int splits, hipStream_t s) {
+static hipError_t launch_t(GemmParams p, int splits, hipStream_t s, int variant = -1) {
+  if (variant < 0) variant = g_variant;
   if constexpr (BM == 256 && BN == 256) {
     // large shapes: 256x256 tile, 8 waves (each 128x64), 128 KiB LDS, 1 block/CU
-    if (g_variant == 9) return launch_dma<256, 256, 2, 4, 2, LA, LB, EPI, ACT, BG>(p, splits, s);
+    if (variant == 9) return launch_dma<256, 256, 2, 4, 2, LA, LB, EPI, ACT, BG>(p, splits, s);
     dim3 grid((p.N + 255) / 256, (p.M + 255) / 256, splits);
     set_extents<LA, LB>(p);
     auto kfn = gemm_bf16_pp256_kernel<LA, LB, EPI, ACT, BG>;
@@ -941,7 +984,7 @@ static hipError_t launch_t(GemmParams p, int splits, hipStream_t s) {
   } else {
   if (gemm_impl() == 2) {
     if constexpr (BM == 128 && BN == 128) {
-      switch (g_variant) {
+      switch (variant) {
         case 1: return launch_dma<128, 128, 2, 2, 3, LA, LB, EPI, ACT, BG>(p, splits, s);
         case 2: return launch_dma<128, 128, 2, 4, 4, LA, LB, EPI, ACT, BG>(p, splits, s);
         case 3: return launch_dma<128, 128, 4, 2, 4, LA, LB, EPI, ACT, BG>(p, splits, s);
@@ -970,11 +1013,13 @@ static hipError_t launch_t(GemmParams p, int splits, hipStream_t s) {
 }
 
 template <int BM, int BN, int LA, int LB, int EPI, bool BG>
-static hipError_t launch_act(const GemmParams& p, int act, int splits, hipStream_t s) {
+static hipError_t launch_act(const GemmParams& p, int act, int splits, hipStream_t s,
+                             int variant = -1) {
+  const int v = variant >= 0 ? variant : g_variant;
   switch (act) {
-    case ACT_RELU: return launch_t<BM, BN, LA, LB, EPI, ACT_RELU, BG>(p, splits, s);
-    case ACT_TANH: return launch_t<BM, BN, LA, LB, EPI, ACT_TANH, BG>(p, splits, s);
-    default: return launch_t<BM, BN, LA, LB, EPI, ACT_NONE, BG>(p, splits, s);
+    case ACT_RELU: return launch_t<BM, BN, LA, LB, EPI, ACT_RELU, BG>(p, splits, s, v);
+    case ACT_TANH: return launch_t<BM, BN, LA, LB, EPI, ACT_TANH, BG>(p, splits, s, v);
+    default: return launch_t<BM, BN, LA, LB, EPI, ACT_NONE, BG>(p, splits, s, v);
   }
 }
 
@@ -999,7 +1044,10 @@ hipError_t linear_fwd_bf16(const bf16* X, int ldx, const bf16* W, int ldw, const
   p.C = Y; p.ldc = ldy; p.bias = bias;
   const int t = pick_tile(M, N);
   if (t == 256) return launch_act<256, 256, KMAJ, KMAJ, EPI_BIAS_ACT, false>(p, act, 1, s);
-  if (t == 128) return launch_act<128, 128, KMAJ, KMAJ, EPI_BIAS_ACT, false>(p, act, 1, s);
+  if (t == 128) {
+    const int v = g_variant != 0 ? g_variant : g_fwd_variant >= 0 ? g_fwd_variant : FWD_VARIANT_DEFAULT;
+    return launch_act<128, 128, KMAJ, KMAJ, EPI_BIAS_ACT, false>(p, act, 1, s, v);
+  }
   return launch_act<64, 64, KMAJ, KMAJ, EPI_BIAS_ACT, false>(p, act, 1, s);
 }
 
@@ -1030,6 +1078,7 @@ int wgrad_splits(int M, int N, int K) {
   const int ksteps = (K + GEMM_BK - 1) / GEMM_BK;
   int s = 1;
   while (tiles * s < 256 && ksteps / (s * 2) >= 4 && s < 64) s *= 2;
+  if (g_wgrad_splits > 0 && g_wgrad_splits < s) s = g_wgrad_splits;  // experiments: fewer slabs
   return s;
 }
 
@@ -1216,13 +1265,18 @@ hipError_t bwd_group(const DgradArgs* dg, const WgradArgs* wg, const SlabReduce*
   const int nb = g.dg_blocks + g.wg_blocks + nbr;
   if (nb == 0) return hipSuccess;
   const int act = dg ? dg->act : ACT_NONE;
-  auto kfn = act == ACT_RELU ? bwd_group_kernel<ACT_RELU>
-           : act == ACT_TANH ? bwd_group_kernel<ACT_TANH> : bwd_group_kernel<ACT_NONE>;
-  static bool attr[3] = {false, false, false};
+  const int ga = g_group_async >= 0 ? std::min(g_group_async, 2) : GROUP_ASYNC_DEFAULT;
+  using GrpFn = void (*)(BwdGroupParams);
+  static const GrpFn fns[3][3] = {
+      {bwd_group_kernel<ACT_RELU, 0>, bwd_group_kernel<ACT_RELU, 1>, bwd_group_kernel<ACT_RELU, 2>},
+      {bwd_group_kernel<ACT_TANH, 0>, bwd_group_kernel<ACT_TANH, 1>, bwd_group_kernel<ACT_TANH, 2>},
+      {bwd_group_kernel<ACT_NONE, 0>, bwd_group_kernel<ACT_NONE, 1>, bwd_group_kernel<ACT_NONE, 2>}};
+  static bool attr[3][3] = {};
   const int ai = act == ACT_RELU ? 0 : act == ACT_TANH ? 1 : 2;
-  if (!attr[ai]) {
+  const GrpFn kfn = fns[ai][ga];
+  if (!attr[ai][ga]) {
     (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, GRP_SMEM);
-    attr[ai] = true;
+    attr[ai][ga] = true;
   }
   hipLaunchKernelGGL(kfn, dim3(nb), dim3(GRP_THREADS), GRP_SMEM, s, g);
   if (!wg_pending && wg && pend.S > 0) {   // caller does not defer: combine right away

@@ -68,15 +68,20 @@ __device__ __forceinline__ void store8(TA* p, const float (&v)[8]) {
 // visits; the 4 waves are combined through LDS in wave order and every block writes one partial
 // slab (gW [in], gb, loss) for the deterministic reducer.  All per-element conditions are
 // expressed as predicates/clamps (no branches around loads or shuffles).
-template <typename TA, int CMAX, int LOSS, int ACT, bool FUSE, int RPW, int OUTM>
-__global__ void __launch_bounds__(256) head_fwd_kernel(HeadArgs p, float* __restrict__ wslab,
-                                                       float* __restrict__ bslab) {
+//
+// HW waves per block: 16 for rows of <= 1024 features (a few rows per wave keep 2-4 waves on
+// every SIMD, so the row loads of the whole chip are in flight at once), 4 for wider rows (their
+// per-lane register footprint only fits at low occupancy).
+template <typename TA, int CMAX, int LOSS, int ACT, bool FUSE, int RPW, int OUTM, int HW>
+__global__ void __launch_bounds__(64 * HW) head_fwd_kernel(HeadArgs p, float* __restrict__ wslab,
+                                                           float* __restrict__ bslab) {
   extern __shared__ __attribute__((aligned(16))) float wl[];  // [out][in] (+ [in] if FUSE)
+  constexpr int NT = 64 * HW;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nW = p.out * p.in;
-  for (int i = tid * 4; i < nW; i += 256 * 4)
+  for (int i = tid * 4; i < nW; i += NT * 4)
     *reinterpret_cast<float4*>(wl + i) = *reinterpret_cast<const float4*>(p.W + i);
-  __shared__ float red[4][2];
+  __shared__ float red[HW][2];
   __syncthreads();
 
   const int nch = p.in >> 3;
@@ -109,7 +114,7 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(HeadArgs p, float* __rest
 #pragma unroll
   for (int o = 0; o < OUTM; ++o) bias[o] = p.b[min(o, nout - 1)];
 
-  const int gw = blockIdx.x * 4 + w, nwaves = gridDim.x * 4;
+  const int gw = blockIdx.x * HW + w, nwaves = gridDim.x * HW;
   for (int r0 = gw * RPW; r0 < p.rows; r0 += nwaves * RPW) {
     float av[RPW][CMAX][8];
     float yv[RPW][OUTM];
@@ -235,9 +240,9 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(HeadArgs p, float* __rest
     red[w][1] = gbacc;
   }
   if constexpr (FUSE) {
-    // combine the 4 waves' column partials in wave order through LDS (after the W image)
+    // combine the waves' column partials in wave order through LDS (after the W image)
     float* gl = wl + nW;
-    for (int ww = 0; ww < 4; ++ww) {
+    for (int ww = 0; ww < HW; ++ww) {
       __syncthreads();
       if (w == ww) {
 #pragma unroll
@@ -254,39 +259,50 @@ __global__ void __launch_bounds__(256) head_fwd_kernel(HeadArgs p, float* __rest
     }
     __syncthreads();
     float* dst = wslab + (long long)blockIdx.x * p.in;
-    for (int i = tid * 4; i < p.in; i += 256 * 4)
+    for (int i = tid * 4; i < p.in; i += NT * 4)
       *reinterpret_cast<float4*>(dst + i) = *reinterpret_cast<const float4*>(gl + i);
   }
   __syncthreads();
-  if (tid == 0) {
-    p.loss_part[blockIdx.x] = ((red[0][0] + red[1][0]) + red[2][0]) + red[3][0];
-    if constexpr (FUSE) bslab[blockIdx.x] = ((red[0][1] + red[1][1]) + red[2][1]) + red[3][1];
+  if (tid == 0) {   // wave partials in wave order
+    float l = red[0][0], b = red[0][1];
+#pragma unroll
+    for (int k = 1; k < HW; ++k) {
+      l += red[k][0];
+      b += red[k][1];
+    }
+    p.loss_part[blockIdx.x] = l;
+    if constexpr (FUSE) bslab[blockIdx.x] = b;
   }
 }
 
+// Block geometry by row width: (waves per block, rows per wave-iteration of the out == 1 heads).
+// Rows per block stay 64 / 32 / 16 / 4, so the number of partial slabs (blocks) is unchanged
+// from the 4-wave layout while 4x more waves are resident.
+static int head_waves(int in) { return in / 8 <= 128 ? 16 : 4; }
 static int head_rpw(int in) {
   const int nch = in / 8;
-  return nch <= 64 ? 16 : nch <= 128 ? 8 : nch <= 256 ? 4 : 1;
+  return nch <= 64 ? 4 : nch <= 128 ? 2 : nch <= 256 ? 4 : 1;
 }
 
-// one wave-iteration per wave where possible: blocks = rows / (4 waves * RPW), capped at 256
+// one wave-iteration per wave where possible: blocks = rows / (waves * RPW), capped at 256
 int head_fwd_parts(int rows, int in) {
-  const int per_block = 4 * head_rpw(in);
+  const int per_block = head_waves(in) * head_rpw(in);
   return std::max(1, std::min((rows + per_block - 1) / per_block, 256));
 }
 
-template <typename TA, int CMAX, int LOSS, bool FUSE, int RPW, int OUTM>
+template <typename TA, int CMAX, int LOSS, bool FUSE, int RPW, int OUTM, int HW>
 static hipError_t head_launch_act(const HeadArgs& a, int act, int blocks, size_t smem, float* wslab,
                                   float* bslab, hipStream_t s) {
+  const dim3 g(blocks), t(64 * HW);
   switch (act) {
     case ACT_RELU:
-      hipLaunchKernelGGL((head_fwd_kernel<TA, CMAX, LOSS, ACT_RELU, FUSE, RPW, OUTM>), dim3(blocks), dim3(256), smem, s, a, wslab, bslab);
+      hipLaunchKernelGGL((head_fwd_kernel<TA, CMAX, LOSS, ACT_RELU, FUSE, RPW, OUTM, HW>), g, t, smem, s, a, wslab, bslab);
       break;
     case ACT_TANH:
-      hipLaunchKernelGGL((head_fwd_kernel<TA, CMAX, LOSS, ACT_TANH, FUSE, RPW, OUTM>), dim3(blocks), dim3(256), smem, s, a, wslab, bslab);
+      hipLaunchKernelGGL((head_fwd_kernel<TA, CMAX, LOSS, ACT_TANH, FUSE, RPW, OUTM, HW>), g, t, smem, s, a, wslab, bslab);
       break;
     default:
-      hipLaunchKernelGGL((head_fwd_kernel<TA, CMAX, LOSS, ACT_NONE, FUSE, RPW, OUTM>), dim3(blocks), dim3(256), smem, s, a, wslab, bslab);
+      hipLaunchKernelGGL((head_fwd_kernel<TA, CMAX, LOSS, ACT_NONE, FUSE, RPW, OUTM, HW>), g, t, smem, s, a, wslab, bslab);
   }
   return hipGetLastError();
 }
@@ -295,12 +311,12 @@ template <typename TA, int LOSS, bool FUSE, int OM>
 static hipError_t head_launch_c(const HeadArgs& a, int act, int blocks, size_t smem, float* wslab,
                                 float* bslab, hipStream_t s) {
   const int nch = a.in / 8;
-  // fused (out == 1) heads keep many rows in flight; wide heads one row (register budget)
+  // fused (out == 1) heads keep several rows in flight per wave; wide heads one row (registers)
   constexpr int D = (FUSE || OM == 1) ? 1 : 16;
-  if (nch <= 64) return head_launch_act<TA, 1, LOSS, FUSE, (16 / D > 0 ? 16 / D : 1), OM>(a, act, blocks, smem, wslab, bslab, s);
-  if (nch <= 128) return head_launch_act<TA, 2, LOSS, FUSE, (8 / D > 0 ? 8 / D : 1), OM>(a, act, blocks, smem, wslab, bslab, s);
-  if (nch <= 256) return head_launch_act<TA, 4, LOSS, FUSE, (4 / D > 0 ? 4 / D : 1), OM>(a, act, blocks, smem, wslab, bslab, s);
-  if (nch <= 1024) return head_launch_act<TA, 16, LOSS, FUSE, 1, OM>(a, act, blocks, smem, wslab, bslab, s);
+  if (nch <= 64) return head_launch_act<TA, 1, LOSS, FUSE, (4 / D > 0 ? 4 / D : 1), OM, 16>(a, act, blocks, smem, wslab, bslab, s);
+  if (nch <= 128) return head_launch_act<TA, 2, LOSS, FUSE, (2 / D > 0 ? 2 / D : 1), OM, 16>(a, act, blocks, smem, wslab, bslab, s);
+  if (nch <= 256) return head_launch_act<TA, 4, LOSS, FUSE, (4 / D > 0 ? 4 / D : 1), OM, 4>(a, act, blocks, smem, wslab, bslab, s);
+  if (nch <= 1024) return head_launch_act<TA, 16, LOSS, FUSE, 1, OM, 4>(a, act, blocks, smem, wslab, bslab, s);
   return hipErrorInvalidValue;
 }
 

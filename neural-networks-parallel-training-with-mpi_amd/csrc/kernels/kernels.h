@@ -55,6 +55,10 @@ void set_gemm_impl(int impl);  // 1 = register-staged main loop, 2 = LDS-DMA rin
 int get_gemm_impl();
 void set_gemm_tile(int t);     // 0 = heuristic, 64 / 128 = force (experiments)
 void set_gemm_variant(int v);  // DMA-path main-loop variant (experiments), 0 = default
+// step-level kernel-selection knobs (-1 / 0 = built-in default; scripts/step_ab.py)
+void set_fwd_variant(int v);   // forward GEMM (128x128 tiles) main-loop variant
+void set_group_async(int m);   // grouped backward LDS read mode: 0 compiler, 1 stage, 2 k-half
+void set_wgrad_splits(int s);  // upper bound on the weight-gradient split-K factor
 size_t wgrad_workspace_bytes(int M, int N, int K);
 hipError_t linear_wgrad_bf16(const bf16* dZ, int lddz, const bf16* X, int ldx, float* dW,
                              float* db, int M, int N, int K, float* ws, hipStream_t s,

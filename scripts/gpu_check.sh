@@ -18,13 +18,13 @@ ok_or_stop() {  # $1 = rc, $2 = name
 for s in $STEPS; do
   case "$s" in
     smoke)
-      timeout -k 10 400 python -c "import __graft_entry__ as g; g.build(); g.smoke()" > gpurun_out/smoke.log 2>&1
+      timeout -k 10 400 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1
       ok_or_stop $? smoke ;;
     tests)
-      timeout -k 10 900 python -m pytest tests -m gpu -q -x > gpurun_out/pytest_gpu.log 2>&1
+      timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
       ok_or_stop $? tests ;;
     testsall)
-      timeout -k 10 900 python -m pytest tests -m gpu -q > gpurun_out/pytest_gpu.log 2>&1
+      timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
       ok_or_stop $? testsall ;;
     gemm)
       timeout -k 10 300 python scripts/gemm_bench.py > gpurun_out/gemm_bench.json 2> gpurun_out/gemm_bench.err
@@ -56,6 +56,16 @@ for s in $STEPS; do
       timeout -k 10 300 python scripts/gemm_bench.py --inf 1024 --outf 1024 --impls 2 --tiles 128 --variants 0,1,2,3,8 >> gpurun_out/variants.json 2>> gpurun_out/variants.err
       ok_or_stop $? variants1024
       cat gpurun_out/variants.json ;;
+    sweep512)
+      # proxy-shape GEMMs: every 128/64-tile DMA variant vs hipBLASLt (impl 0), one process
+      timeout -k 10 300 python scripts/gemm_bench.py --rows 8192 --inf 512 --outf 512 --rounds 8 --iters 20 --impls 0,2 --tiles 0,128 --variants 0,1,2,3,5,6,7,8 > gpurun_out/sweep512.json 2> gpurun_out/sweep512.err
+      ok_or_stop $? sweep512
+      cat gpurun_out/sweep512.json ;;
+    stepab)
+      # whole-step knob A/B (forward variant, grouped-backward LDS read mode, wgrad splits)
+      timeout -k 10 400 python scripts/step_ab.py > gpurun_out/step_ab.json 2> gpurun_out/step_ab.err
+      ok_or_stop $? stepab
+      cat gpurun_out/step_ab.json ;;
     benchall)
       for c in proxy512 mnist wide8192 ref; do
         timeout -k 10 300 python bench.py --config $c --steps 50 --warmup 5 >> gpurun_out/bench_all.json 2>> gpurun_out/bench_all.err

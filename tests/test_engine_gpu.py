@@ -205,3 +205,42 @@ def test_multi_step_graph_equals_single_steps():
         outs.append(ar.master.clone())
         assert eng.steps_done == 10
     assert _t.equal(outs[0], outs[1])
+
+
+def _cfg512(**kw):
+    """Proxy-sized shapes (8192 x 512): the 128x128-tile forward and the grouped backward."""
+    return _cfg(device="cuda", widths=[512, 512, 512, 1], n_features=512, n_samples=8192,
+                lr=1e-5, **kw)
+
+
+@pytest.mark.parametrize("mode", [1, 2])
+def test_grouped_backward_async_lds_reads_bitwise_equal(mode):
+    """Grouped backward with asm transposed LDS reads (explicit lgkmcnt, DMA ring kept in
+    flight) == the compiler-scheduled reads, bit for bit."""
+    from nnmpi_amd import native
+    lib = native.lib()
+    try:
+        lib.set_group_async(0)
+        a = trainer.run_worker(_cfg512(nepochs=5))
+        lib.set_group_async(mode)
+        b = trainer.run_worker(_cfg512(nepochs=5))
+    finally:
+        lib.set_group_async(-1)
+    assert a.losses == b.losses
+    assert torch.equal(a.final_params, b.final_params)
+
+
+@pytest.mark.parametrize("variant", [1, 2, 5, 6, 8])
+def test_forward_variants_bitwise_equal(variant):
+    """Every forward main-loop variant accumulates each output in the same k order."""
+    from nnmpi_amd import native
+    lib = native.lib()
+    try:
+        lib.set_fwd_variant(0)
+        a = trainer.run_worker(_cfg512(nepochs=3))
+        lib.set_fwd_variant(variant)
+        b = trainer.run_worker(_cfg512(nepochs=3))
+    finally:
+        lib.set_fwd_variant(-1)
+    assert a.losses == b.losses
+    assert torch.equal(a.final_params, b.final_params)
