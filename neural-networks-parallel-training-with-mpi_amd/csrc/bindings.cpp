@@ -258,6 +258,9 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
       .def("allgather", [](RcclComm& c, uptr sb, uptr rb, size_t n, int dt, uptr s) {
         c.allgather(P<const void>(sb), P<void>(rb), n, dt, S(s));
       })
+      .def("reduce_scatter", [](RcclComm& c, uptr sb, uptr rb, size_t n, int dt, int op, uptr s) {
+        c.reduce_scatter(P<const void>(sb), P<void>(rb), n, dt, op, S(s));
+      })
       .def("scatterv", [](RcclComm& c, uptr sb, std::vector<long long> counts,
                           std::vector<long long> displs, uptr rb, int dt, int root, uptr s) {
         c.scatterv(P<const void>(sb), counts, displs, P<void>(rb), dt, root, S(s));

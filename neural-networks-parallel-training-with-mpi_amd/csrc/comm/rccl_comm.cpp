@@ -90,6 +90,11 @@ void RcclComm::allgather(const void* sendbuf, void* recvbuf, size_t count, int d
   NCCL_THROW(ncclAllGather(sendbuf, recvbuf, count, to_nccl(dtype), comm_, s));
 }
 
+void RcclComm::reduce_scatter(const void* sendbuf, void* recvbuf, size_t recvcount, int dtype,
+                              int op, hipStream_t s) {
+  NCCL_THROW(ncclReduceScatter(sendbuf, recvbuf, recvcount, to_nccl(dtype), to_op(op), comm_, s));
+}
+
 void RcclComm::scatterv(const void* sendbuf, const std::vector<long long>& counts,
                         const std::vector<long long>& displs, void* recvbuf, int dtype, int root,
                         hipStream_t s) {

@@ -8,7 +8,8 @@
 //                  gated by a "bucket ready" event recorded on the compute stream after that
 //                  layer's wgrad, joined back before the optimizer;
 //   * broadcast  — initial parameters from rank 0 (ncclBroadcast);
-//   * scatterv   — grouped ncclSend/ncclRecv with per-rank counts (uneven splits, fixes D1-D3).
+//   * scatterv   — grouped ncclSend/ncclRecv with per-rank counts (uneven splits, fixes D1-D3);
+//   * reduce_scatter / allgather — the sharded-optimizer (ZeRO-1) gradient and parameter legs.
 // Every call is asynchronous and hipGraph-capturable (no host sync inside).
 #pragma once
 #include <hip/hip_runtime.h>
@@ -39,6 +40,10 @@ class RcclComm {
                 const std::vector<long long>& displs, void* recvbuf, int dtype, int root,
                 hipStream_t s);
   void allgather(const void* sendbuf, void* recvbuf, size_t count, int dtype, hipStream_t s);
+  // rank r receives the reduction of elements [r*recvcount, (r+1)*recvcount) of every sendbuf
+  // (in place when recvbuf == sendbuf + r*recvcount)
+  void reduce_scatter(const void* sendbuf, void* recvbuf, size_t recvcount, int dtype, int op,
+                      hipStream_t s);
   // Returns the RCCL async error code (0 = ok); aborts the communicator on error if asked.
   int poll_error(bool abort_on_error);
   void abort();

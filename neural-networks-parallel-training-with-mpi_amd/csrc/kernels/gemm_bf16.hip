@@ -960,7 +960,7 @@ static int g_fwd_variant = -1;    // forward GEMM main-loop variant (launch_t's 
 static int g_group_async = -1;    // grouped-backward LDS read mode (dma_gemm_tile ASYNC_TR)
 static int g_wgrad_splits = 0;    // > 0: upper bound on the weight-gradient split-K factor
 constexpr int FWD_VARIANT_DEFAULT = 0;
-constexpr int GROUP_ASYNC_DEFAULT = 0;
+constexpr int GROUP_ASYNC_DEFAULT = 2;   // measured: 102.3 -> 97.9 us/step (proxy512, step_ab)
 void set_fwd_variant(int v) { g_fwd_variant = v; }
 void set_group_async(int m) { g_group_async = m; }
 void set_wgrad_splits(int s) { g_wgrad_splits = s; }

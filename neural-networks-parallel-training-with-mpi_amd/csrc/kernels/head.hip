@@ -65,13 +65,13 @@ __device__ __forceinline__ void store8(TA* p, const float (&v)[8]) {
 // butterfly reductions are all issued together, so no shuffle or load latency is exposed per
 // row).  With FUSE (out == 1 heads) the head weights live in registers and each lane also
 // accumulates the head's weight/bias gradient for its own 8*CMAX columns across all rows it
-// visits; the 4 waves are combined through LDS in wave order and every block writes one partial
+// visits; the waves are combined through LDS in wave order and every block writes one partial
 // slab (gW [in], gb, loss) for the deterministic reducer.  All per-element conditions are
 // expressed as predicates/clamps (no branches around loads or shuffles).
 //
-// HW waves per block: 16 for rows of <= 1024 features (a few rows per wave keep 2-4 waves on
-// every SIMD, so the row loads of the whole chip are in flight at once), 4 for wider rows (their
-// per-lane register footprint only fits at low occupancy).
+// HW waves per block: 16 / 8 for rows of <= 512 / 1024 features (a few rows per wave keep several
+// waves on every SIMD, so the row loads of the whole chip are in flight at once), 4 for wider rows
+// (their per-lane register footprint only fits at low occupancy).
 template <typename TA, int CMAX, int LOSS, int ACT, bool FUSE, int RPW, int OUTM, int HW>
 __global__ void __launch_bounds__(64 * HW) head_fwd_kernel(HeadArgs p, float* __restrict__ wslab,
                                                            float* __restrict__ bslab) {
@@ -240,27 +240,25 @@ __global__ void __launch_bounds__(64 * HW) head_fwd_kernel(HeadArgs p, float* __
     red[w][1] = gbacc;
   }
   if constexpr (FUSE) {
-    // combine the waves' column partials in wave order through LDS (after the W image)
-    float* gl = wl + nW;
-    for (int ww = 0; ww < HW; ++ww) {
-      __syncthreads();
-      if (w == ww) {
+    // every wave parks its column partials in its own LDS row (16-B stores), then each thread
+    // sums one column over the waves in wave order (one barrier, no serial wave rounds)
+    float* gl = wl + nW;   // [HW][in]
 #pragma unroll
-        for (int c = 0; c < CMAX; ++c) {
-          if (cmask[c] != 0.f) {
-#pragma unroll
-            for (int e = 0; e < 8; ++e) {
-              float* d = gl + chc[c] * 8 + e;
-              *d = (ww == 0) ? gacc[c][e] : *d + gacc[c][e];
-            }
-          }
-        }
+    for (int c = 0; c < CMAX; ++c) {
+      if (cmask[c] != 0.f) {
+        float* d = gl + w * p.in + chc[c] * 8;
+        *reinterpret_cast<float4*>(d) = make_float4(gacc[c][0], gacc[c][1], gacc[c][2], gacc[c][3]);
+        *reinterpret_cast<float4*>(d + 4) = make_float4(gacc[c][4], gacc[c][5], gacc[c][6], gacc[c][7]);
       }
     }
     __syncthreads();
     float* dst = wslab + (long long)blockIdx.x * p.in;
-    for (int i = tid * 4; i < p.in; i += NT * 4)
-      *reinterpret_cast<float4*>(dst + i) = *reinterpret_cast<const float4*>(gl + i);
+    for (int i = tid; i < p.in; i += NT) {
+      float t = gl[i];
+#pragma unroll
+      for (int k = 1; k < HW; ++k) t += gl[k * p.in + i];
+      dst[i] = t;
+    }
   }
   __syncthreads();
   if (tid == 0) {   // wave partials in wave order
@@ -276,12 +274,13 @@ __global__ void __launch_bounds__(64 * HW) head_fwd_kernel(HeadArgs p, float* __
 }
 
 // Block geometry by row width: (waves per block, rows per wave-iteration of the out == 1 heads).
-// Rows per block stay 64 / 32 / 16 / 4, so the number of partial slabs (blocks) is unchanged
-// from the 4-wave layout while 4x more waves are resident.
-static int head_waves(int in) { return in / 8 <= 128 ? 16 : 4; }
+// 32 / 16 / 16 / 4 rows per block: 8192 rows of <= 512 features give 256 blocks, one per CU (a
+// 128-block grid left half the chip idle: 9.5 us for 16 MB of traffic, PMC-measured).  LDS per
+// fused block: W row + HW gradient rows = (1 + HW) * in floats <= 64 KiB.
+static int head_waves(int in) { return in / 8 <= 64 ? 16 : in / 8 <= 128 ? 8 : 4; }
 static int head_rpw(int in) {
   const int nch = in / 8;
-  return nch <= 64 ? 4 : nch <= 128 ? 2 : nch <= 256 ? 4 : 1;
+  return nch <= 64 ? 2 : nch <= 128 ? 2 : nch <= 256 ? 4 : 1;
 }
 
 // one wave-iteration per wave where possible: blocks = rows / (waves * RPW), capped at 256
@@ -313,8 +312,8 @@ static hipError_t head_launch_c(const HeadArgs& a, int act, int blocks, size_t s
   const int nch = a.in / 8;
   // fused (out == 1) heads keep several rows in flight per wave; wide heads one row (registers)
   constexpr int D = (FUSE || OM == 1) ? 1 : 16;
-  if (nch <= 64) return head_launch_act<TA, 1, LOSS, FUSE, (4 / D > 0 ? 4 / D : 1), OM, 16>(a, act, blocks, smem, wslab, bslab, s);
-  if (nch <= 128) return head_launch_act<TA, 2, LOSS, FUSE, (2 / D > 0 ? 2 / D : 1), OM, 16>(a, act, blocks, smem, wslab, bslab, s);
+  if (nch <= 64) return head_launch_act<TA, 1, LOSS, FUSE, (2 / D > 0 ? 2 / D : 1), OM, 16>(a, act, blocks, smem, wslab, bslab, s);
+  if (nch <= 128) return head_launch_act<TA, 2, LOSS, FUSE, (2 / D > 0 ? 2 / D : 1), OM, 8>(a, act, blocks, smem, wslab, bslab, s);
   if (nch <= 256) return head_launch_act<TA, 4, LOSS, FUSE, (4 / D > 0 ? 4 / D : 1), OM, 4>(a, act, blocks, smem, wslab, bslab, s);
   if (nch <= 1024) return head_launch_act<TA, 16, LOSS, FUSE, 1, OM, 4>(a, act, blocks, smem, wslab, bslab, s);
   return hipErrorInvalidValue;
@@ -326,7 +325,7 @@ static hipError_t head_fwd_impl(const void* a, int a_bf16, int rows, int in, con
                                 float* dlogits, float* loss_part, bool fuse, float* wslab,
                                 float* bslab, hipStream_t s) {
   if (out < 1 || out > HEAD_OMAX || in % 8 != 0 || in > 8192) return hipErrorInvalidValue;
-  const size_t smem = (size_t)(out * in + (fuse ? in : 0)) * sizeof(float);
+  const size_t smem = (size_t)(out * in + (fuse ? head_waves(in) * in : 0)) * sizeof(float);
   if (smem > 65536 + 32768) return hipErrorInvalidValue;
   HeadArgs h{a, rows, in, W, b, out, y, labels, inv_count, act_prev, dz_prev, dlogits, loss_part};
   const int blocks = head_fwd_parts(rows, in);

@@ -51,7 +51,9 @@ class Bucket:
 
 class Arena:
     def __init__(self, layer_shapes: List[Tuple[int, int]], device, shadow_dtype=None,
-                 bucket_bytes: float = 25 * 2 ** 20, grad_elem_bytes: int = 4):
+                 bucket_bytes: float = 25 * 2 ** 20, grad_elem_bytes: int = 4, pad_to: int = ALIGN):
+        """``pad_to``: the total length is rounded up to this multiple (a multiple of ALIGN) --
+        the sharded optimizer uses ``world * ALIGN`` so every rank owns an equal, aligned shard."""
         self.layer_shapes = list(layer_shapes)
         self.n_layers = len(layer_shapes)
         self.device = torch.device(device)
@@ -68,7 +70,7 @@ class Arena:
             self.layer_range[li] = (start, off)
         self.slots = slots
         self.by_name = {s.name: s for s in slots}
-        self.numel = off
+        self.numel = _align(off, max(ALIGN, int(pad_to)))
         z = lambda dt: torch.zeros(self.numel, dtype=dt, device=self.device)  # noqa: E731
         self.master = z(torch.float32)
         self.grad = z(torch.float32)

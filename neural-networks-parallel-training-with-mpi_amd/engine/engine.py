@@ -84,7 +84,9 @@ class MLPEngine:
         # grouped backward (bf16 GPU): dgrad_i + wgrad_i + combine_{i+1} in one launch.  Layer
         # i's slabs live in ws_pair[(L-1-i) % 2] so they never alias the pending combine's.
         from ..parallel.sync import NativeRcclSync
-        inline_sync = isinstance(sync, NoSync) or (isinstance(sync, NativeRcclSync) and sync.inline)
+        self.sharded = bool(getattr(sync, "sharded", False))
+        inline_sync = (isinstance(sync, NoSync) or self.sharded or
+                       (isinstance(sync, NativeRcclSync) and sync.inline))
         self.grouped = (bool(grouped) and self.overlap and dtype == torch.bfloat16 and inline_sync
                         and hasattr(ops, "bwd_group") and L > 1)
         self.ws_pair = [self.ws, torch.zeros_like(self.ws)] if self.grouped else [self.ws, self.ws]
@@ -170,6 +172,7 @@ class MLPEngine:
         rows, ops, ar, L = self.rows, self.ops, self.arena, self.L
         if rows == 0:  # empty shard: contributes a zero gradient, still joins every collective
             self.loss_out.zero_()
+            ar.grad.zero_()
             for i in reversed(range(L)):
                 self.sync.ready(i)
             return
@@ -225,8 +228,15 @@ class MLPEngine:
             self.forward_backward()
             self.sync.finish()
             self._mark("comm")
-            self.ops.sgd(self.arena, self.hp, self.nesterov, first)
+            self._update(first)
         self._mark("update")
+
+    def _update(self, first: bool):
+        """Optimizer update of the whole arena (or, sharded, of this rank's slice + gathers)."""
+        if self.sharded:
+            self.sync.update(self.ops, self.hp, self.nesterov, first)
+        else:
+            self.ops.sgd(self.arena, self.hp, self.nesterov, first)
 
     # ---------------- comm-overlapped schedule (GPU) -----------------------------------------
     # Compute stays on ONE stream (measured: splitting wgrad onto a side stream only adds
@@ -268,7 +278,7 @@ class MLPEngine:
         self._mark("comm")
         rest = [b for b in ar.buckets if b.index not in self._sgd_done]
         if len(rest) == len(ar.buckets):
-            ops.sgd(ar, self.hp, self.nesterov, first)      # one pass over the whole arena
+            self._update(first)                             # one pass over the whole arena
         else:
             for b in rest:
                 ops.sgd(ar, self.hp, self.nesterov, first, offset=b.offset, numel=b.numel)
@@ -353,6 +363,9 @@ class MLPEngine:
             for i in unfused:
                 s, e = ar.layer_range[i]
                 ops.sgd(ar, self.hp, self.nesterov, first, offset=s, numel=e - s)
+            return
+        if self.sharded:
+            self._update(first)
             return
         self.sync.begin()
         for b in ar.buckets:

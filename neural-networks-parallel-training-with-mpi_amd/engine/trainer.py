@@ -30,7 +30,7 @@ from ..data.dataset import RegressionDataset, scale_features
 from ..data.partition import partition_rows
 from ..models.mlp import MLP, MLPSpec, reference_init
 from ..parallel import dist as pdist
-from ..parallel.sync import NativeRcclSync, NoSync, TorchDistSync
+from ..parallel.sync import NativeRcclSync, NoSync, ShardedSync, TorchDistSync
 from ..utils import checkpoint as ckpt
 from ..utils.config import TrainConfig, config_from_args
 from ..utils.metrics import MetricsWriter
@@ -162,7 +162,11 @@ def build_shard(j: Job):
 
 
 def _scatter_rows(j: Job, XY, part, width: int) -> np.ndarray:
-    """Reference Scatter/Scatterv (ref.py:108,138) over gloo: padded equal chunks, trimmed."""
+    """Reference Scatter/Scatterv (ref.py:108,138): over RCCL (grouped ncclSend/ncclRecv with
+    per-rank int64 counts and displacements, device to device) when the native communicator is
+    up, else over gloo (padded equal chunks, trimmed)."""
+    if j.native_comm is not None:
+        return _scatter_rows_native(j, XY, part, width)
     import torch.distributed as dist
     mx = max(1, part.max_rows)
     recv = torch.zeros(mx, width, dtype=torch.float64)
@@ -178,6 +182,21 @@ def _scatter_rows(j: Job, XY, part, width: int) -> np.ndarray:
             chunks.append(c)
     dist.scatter(recv, chunks, src=0, group=j.pg.gloo)
     return recv[: part.rows(j.rank)].numpy()
+
+
+def _scatter_rows_native(j: Job, XY, part, width: int) -> np.ndarray:
+    counts = [part.rows(r) * width for r in range(j.world)]
+    displs = [part.start(r) * width for r in range(j.world)]
+    recv = torch.zeros(max(1, counts[j.rank]), dtype=torch.float64, device=j.device)
+    if j.rank == 0:
+        send = torch.from_numpy(np.ascontiguousarray(XY)).to(j.device).reshape(-1)
+    else:
+        send = recv          # not read on non-root ranks
+    s = torch.cuda.current_stream()
+    j.native_comm.scatterv(send.data_ptr(), counts, displs, recv.data_ptr(), 2, 0,
+                           int(s.cuda_stream))
+    s.synchronize()
+    return recv[:counts[j.rank]].view(-1, width).cpu().numpy()
 
 
 def init_model(j: Job, spec: MLPSpec) -> MLP:
@@ -213,13 +232,19 @@ def make_sync(j: Job, arena: Arena):
     cfg = j.cfg
     if j.comm_kind == "none":
         return NoSync(arena)
+    if cfg.shard_optimizer:
+        if cfg.sync == "root" or cfg.grad_dtype != "fp32":
+            raise ValueError("--shard_optimizer reduce-scatters fp32 gradients "
+                             "(no --sync root / --grad_dtype bf16)")
+        if j.comm_kind == "native":
+            return ShardedSync(arena, j.world, j.rank, native_comm=j.native_comm)
+        group = j.pg.nccl if (j.device.type == "cuda" and j.pg.nccl is not None) else j.pg.gloo
+        return ShardedSync(arena, j.world, j.rank, group=group)
     if j.comm_kind == "native":
-        if cfg.sync == "root":
-            raise ValueError("--sync root is only provided on the torch.distributed path")
         inline = (cfg.comm_mode == "inline" or
                   (cfg.comm_mode == "auto" and arena.numel * 4 <= INLINE_MAX_GRAD_BYTES))
         return NativeRcclSync(arena, j.native_comm, j.world, inline=inline,
-                              grad_dtype=cfg.grad_dtype)
+                              grad_dtype=cfg.grad_dtype, mode=cfg.sync)
     group = j.pg.nccl if (j.device.type == "cuda" and j.pg.nccl is not None) else j.pg.gloo
     return TorchDistSync(arena, group, j.world, mode=cfg.sync, overlap=cfg.overlap,
                          grad_dtype=cfg.grad_dtype)
@@ -244,6 +269,13 @@ def loss_scales(cfg: TrainConfig, rows_local: int, rows_all: List[int], out_f: i
     return loss_scale, loss_scale, 1.0 / nonempty
 
 
+def _gather_state(eng, sync):
+    """Sharded optimizer: re-assemble the full fp32 master + momentum on every rank (collective)."""
+    if getattr(sync, "sharded", False):
+        eng.synchronize()
+        sync.gather_state()
+
+
 def _print(cfg: TrainConfig, rank: int, msg: str):
     if cfg.print_rank == "all" or (cfg.print_rank == "0" and rank == 0):
         print(msg, flush=True)
@@ -264,9 +296,10 @@ def _run(j: Job) -> TrainResult:
     rows_local = X.shape[0]
     model = init_model(j, spec)
     dtype = _compute_dtype(cfg)
+    sharded = cfg.shard_optimizer and j.comm_kind != "none"
     arena = Arena([spec.layer_shape(i) for i in range(spec.n_layers)], j.device,
                   shadow_dtype=torch.bfloat16 if dtype == torch.bfloat16 else None,
-                  bucket_bytes=cfg.bucket_mb * 2 ** 20)
+                  bucket_bytes=cfg.bucket_mb * 2 ** 20, pad_to=64 * world if sharded else 64)
     arena.bind_model(model)
     broadcast_params(j, arena)
     start_epoch, steps_done = 0, 0
@@ -335,6 +368,7 @@ def _run(j: Job) -> TrainResult:
             metrics.write(epoch=epoch, loss=loss, epoch_s=dt, steps=steps_per_epoch,
                           samples_per_s=sum(part.counts) / dt if dt > 0 else None, world=world)
             if cfg.checkpoint and cfg.checkpoint_every and (epoch + 1) % cfg.checkpoint_every == 0:
+                _gather_state(eng, sync)
                 if rank == 0:
                     ckpt.save(cfg.checkpoint, arena, epoch + 1, eng.steps_done, cfg)
                 j.pg.barrier()
@@ -345,6 +379,7 @@ def _run(j: Job) -> TrainResult:
             _print(cfg, rank, "[profile] mean ms per step: " +
                    ", ".join(f"{k} {v:.4f}" for k, v in res.phase_ms.items()))
             metrics.write(profile_ms_per_step=res.phase_ms, rank=rank)
+        _gather_state(eng, sync)
         if cfg.checkpoint and rank == 0:
             ckpt.save(cfg.checkpoint, arena, cfg.nepochs, eng.steps_done, cfg)
         res.final_params = arena.flat_params_forward_order().detach().cpu().clone()

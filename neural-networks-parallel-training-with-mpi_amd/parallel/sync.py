@@ -17,7 +17,10 @@ Implementations
   handles per bucket.  ``mode="root"`` reproduces the reference's centralised pattern (reduce to
   rank 0 + broadcast) for comparison.
 * :class:`NativeRcclSync` — the C++ runtime: ncclAllReduce per bucket on a dedicated HIP comm
-  stream gated by per-bucket events (capturable in the step's hipGraph).
+  stream gated by per-bucket events (capturable in the step's hipGraph); ``mode="root"`` is the
+  reference's centralised pattern over RCCL (ncclReduce to rank 0 + ncclBroadcast).
+* :class:`ShardedSync` — sharded optimizer state (ZeRO-1): reduce-scatter of the gradient, SGD
+  on the rank's own 1/P slice of the arena only, all-gather of the updated parameters.
 """
 from __future__ import annotations
 
@@ -114,9 +117,11 @@ class NativeRcclSync(GradSync):
     faster than overlap; large volumes use the overlapped comm stream."""
 
     def __init__(self, arena, native_comm, world: int, priority: int = -1, inline: bool = False,
-                 grad_dtype: str = "fp32"):
+                 grad_dtype: str = "fp32", mode: str = "allreduce"):
         super().__init__(arena)
-        self.inline = bool(inline)
+        self.mode = mode
+        # the root pattern is a serial reduce + broadcast: always on the compute stream
+        self.inline = bool(inline) or mode == "root"
         # bf16 payload: half the bytes on xGMI (bandwidth-bound regime, e.g. the 8192-wide
         # model); the gradient is cast into a bf16 staging arena before and back after the
         # reduction, on the stream that owns that step.
@@ -144,7 +149,12 @@ class NativeRcclSync(GradSync):
             ptr, dt = self.gbuf[bucket.offset:].data_ptr(), 1
             lib.cast_f32_bf16(view.data_ptr(), ptr, bucket.numel, h)
         if self.inline:
-            self.comm.allreduce(ptr, bucket.numel, dt, 0, h)
+            if self.mode == "root":
+                # reference pattern (ref.py:185-203): everything through rank 0
+                self.comm.reduce(ptr, bucket.numel, dt, 0, 0, h)
+                self.comm.broadcast(ptr, bucket.numel, dt, 0, h)
+            else:
+                self.comm.allreduce(ptr, bucket.numel, dt, 0, h)
             if self.bf16:
                 lib.cast_bf16_f32(ptr, view.data_ptr(), bucket.numel, h)
             return
@@ -161,3 +171,87 @@ class NativeRcclSync(GradSync):
         if self._launched:
             self.gs.join(self.native.stream_handle())
         self._launched = False
+
+
+class ShardedSync(GradSync):
+    """Sharded optimizer state, ZeRO stage 1 ("optional stretch: reduce-scatter +
+    sharded SGD + all-gather").
+
+    The flat arena (padded to a multiple of ``world * 64`` elements) is cut into ``world`` equal
+    contiguous slices; rank r owns slice r.  Per step, after the whole backward:
+
+    1. the gradient is reduce-scattered: rank r receives the SUM over ranks of its slice only
+       (RCCL ncclReduceScatter in place; gloo has no reduce-scatter, so the CPU path all-reduces
+       and uses its slice -- the same sums);
+    2. only the owner applies SGD-momentum to its slice (1/P folded in, as usual), so the
+       momentum of the other slices is never read or written;
+    3. the updated parameters are all-gathered: the bf16 compute shadow when there is one (half
+       the bytes of fp32; the fp32 master of foreign slices then goes stale until
+       :meth:`gather_state`), else the fp32 master.
+
+    Bytes on the wire per step: reduce-scatter fp32 + all-gather bf16 = 3/4 of an fp32
+    all-reduce.  :meth:`gather_state` re-assembles the full fp32 master and momentum (collective:
+    every rank calls it) before checkpoints and the final state_dict.
+    """
+    sharded = True
+
+    def __init__(self, arena, world: int, rank: int, native_comm=None, group=None):
+        super().__init__(arena)
+        if arena.numel % (world * 64):
+            raise ValueError("ShardedSync needs an arena padded to a multiple of world*64 "
+                             f"(numel={arena.numel}, world={world})")
+        self.world, self.rank = world, rank
+        self.shard = arena.numel // world
+        self.off = rank * self.shard
+        self.comm = native_comm
+        self.group = group
+        if native_comm is not None:
+            from .. import native
+            self.native = native
+
+    def ready(self, layer: int):
+        pass   # nothing moves until the whole gradient exists
+
+    def launch_bucket(self, bucket, stream):
+        return None
+
+    def _views(self, buf):
+        return [buf[r * self.shard:(r + 1) * self.shard] for r in range(self.world)]
+
+    def update(self, ops, hp, nesterov: bool, first: bool):
+        """Reduce-scatter -> owner SGD -> all-gather, on the current (compute) stream."""
+        ar = self.arena
+        self.seq += 1
+        if self.comm is not None:
+            h = self.native.stream_handle()
+            g = ar.grad.data_ptr()
+            self.comm.reduce_scatter(g, g + 4 * self.off, self.shard, 0, 0, h)
+        else:
+            dist.all_reduce(ar.grad, group=self.group)
+        ops.sgd(ar, hp, nesterov, first, offset=self.off, numel=self.shard)
+        if self.comm is not None:
+            if ar.shadow is not None:
+                s = ar.shadow.data_ptr()
+                self.comm.allgather(s + 2 * self.off, s, self.shard, 1, h)
+            else:
+                m = ar.master.data_ptr()
+                self.comm.allgather(m + 4 * self.off, m, self.shard, 0, h)
+        else:
+            dist.all_gather(self._views(ar.master),
+                            ar.master[self.off:self.off + self.shard].clone(), group=self.group)
+            if ar.shadow is not None:
+                ar.shadow.copy_(ar.master)
+
+    def gather_state(self):
+        """Full fp32 master + momentum on every rank (checkpoint / final parameters)."""
+        ar = self.arena
+        for buf in (ar.master, ar.momentum):
+            own = buf[self.off:self.off + self.shard]
+            if self.comm is not None:
+                import torch as _t
+                s = _t.cuda.current_stream()
+                p = buf.data_ptr()
+                self.comm.allgather(p + 4 * self.off, p, self.shard, 0, int(s.cuda_stream))
+                s.synchronize()
+            else:
+                dist.all_gather(self._views(buf), own.clone(), group=self.group)

@@ -72,6 +72,7 @@ class TrainConfig:
     overlap: bool = True
     graph: bool = True                # capture the steady-state step in a HIP graph
     grad_dtype: str = "fp32"          # fp32 | bf16 (all-reduce payload dtype)
+    shard_optimizer: bool = False     # ZeRO-1: reduce-scatter grads, SGD on own 1/P, all-gather
     deterministic: bool = True
     # --- IO / observability ---
     print_rank: str = "all"           # all | 0 | none
@@ -141,6 +142,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--no_overlap", dest="overlap", action="store_false")
     p.add_argument("--no_graph", dest="graph", action="store_false")
     p.add_argument("--grad_dtype", choices=["fp32", "bf16"], default="fp32")
+    p.add_argument("--shard_optimizer", "--zero1", dest="shard_optimizer", action="store_true",
+                   help="sharded optimizer state (ZeRO-1): reduce-scatter gradients, SGD on this "
+                        "rank's 1/P of the parameters, all-gather the updated parameters")
     p.add_argument("--nondeterministic", dest="deterministic", action="store_false")
     p.add_argument("--print_rank", choices=["all", "0", "none"], default="all")
     p.add_argument("--global_loss", action="store_true")

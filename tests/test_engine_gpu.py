@@ -244,3 +244,33 @@ def test_forward_variants_bitwise_equal(variant):
         lib.set_fwd_variant(-1)
     assert a.losses == b.losses
     assert torch.equal(a.final_params, b.final_params)
+
+
+def test_native_root_sync_single_rank_matches_local():
+    """--sync root over RCCL (ncclReduce to rank 0 + ncclBroadcast, the reference's pattern)."""
+    a = trainer.run_worker(_cfg(device="cuda", comm="native", sync="root", nepochs=4))
+    b = trainer.run_worker(_cfg(device="cuda", comm="none", nepochs=4))
+    assert a.losses == b.losses
+    assert torch.equal(a.final_params, b.final_params)
+
+
+def test_native_sharded_optimizer_single_rank_matches_local():
+    """ZeRO-1 through the native communicator (in-place ncclReduceScatter, owner SGD, in-place
+    bf16 ncclAllGather, final fp32 gather) == the communication-free run."""
+    a = trainer.run_worker(_cfg(device="cuda", comm="native", shard_optimizer=True, nepochs=4))
+    b = trainer.run_worker(_cfg(device="cuda", comm="none", nepochs=4))
+    assert a.losses == b.losses
+    assert torch.equal(a.final_params, b.final_params)
+
+
+def test_native_scatterv_single_rank():
+    """RcclComm.scatterv (grouped ncclSend/ncclRecv; the root's own chunk is a device copy)."""
+    from nnmpi_amd import native
+    lib = native.lib()
+    comm = native.make_comm(lib.rccl_unique_id(), 1, 0, torch.cuda.current_device())
+    src = torch.arange(30, dtype=torch.float64, device="cuda")
+    dst = torch.zeros(12, dtype=torch.float64, device="cuda")
+    s = torch.cuda.current_stream()
+    comm.scatterv(src.data_ptr(), [12], [6], dst.data_ptr(), 2, 0, int(s.cuda_stream))
+    s.synchronize()
+    assert torch.equal(dst, src[6:18])
