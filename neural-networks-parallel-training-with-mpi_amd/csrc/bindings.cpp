@@ -149,6 +149,7 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
       .def("pending", [](const SlabReduce& r) { return r.S > 0 || r.loss_out != nullptr; });
   m.def("slab_reduce", [](const SlabReduce& r, uptr s) { check(slab_reduce(r, S(s)), "slab_reduce"); });
   m.def("set_bwd_group", &set_bwd_group);
+  m.def("bwd_group_supported", &bwd_group_supported);
   m.def("head_fused_deferred", [](uptr a, int a_bf16, int rows, int in, uptr W, uptr b, uptr y,
                                   float inv_count, int act_prev, uptr dz, uptr gW, uptr gb, uptr ws,
                                   uptr lp, float lscale, uptr lout, uptr s, py::object sgd) {
@@ -203,7 +204,8 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
   m.def("tiny_mlp_workspace_bytes", &tiny_mlp_workspace_bytes);
   m.def("tiny_mlp_step", [](std::vector<int> widths, std::vector<int> w_off, std::vector<int> b_off,
                             int act, int loss, uptr params, uptr X, uptr y, uptr labels, int rows,
-                            float inv_count, uptr grad, int numel, uptr ws, uptr lout, uptr s) {
+                            float inv_count, uptr grad, int numel, uptr ws, uptr lout, uptr s,
+                            py::object sgd) {
     TinyMLPDesc d{};
     d.n_layers = (int)widths.size() - 1;
     if (d.n_layers < 1 || d.n_layers > 4 || (int)w_off.size() != d.n_layers || (int)b_off.size() != d.n_layers)
@@ -212,10 +214,16 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
     for (int i = 0; i < d.n_layers; ++i) { d.w_off[i] = w_off[i]; d.b_off[i] = b_off[i]; }
     d.act = act;
     d.loss = loss;
+    SgdFuse f{};
+    const bool fu = to_sgd(sgd, f);
     check(tiny_mlp_step(d, P<const float>(params), P<const float>(X), P<const float>(y),
                         P<const int64_t>(labels), rows, inv_count, P<float>(grad), numel, P<float>(ws),
-                        P<float>(lout), S(s)), "tiny_mlp_step");
-  });
+                        P<float>(lout), S(s), fu ? &f : nullptr), "tiny_mlp_step");
+  }, py::arg("widths"), py::arg("w_off"), py::arg("b_off"), py::arg("act"), py::arg("loss"),
+     py::arg("params"), py::arg("X"), py::arg("y"), py::arg("labels"), py::arg("rows"),
+     py::arg("inv_count"), py::arg("grad"), py::arg("numel"), py::arg("ws"), py::arg("lout"),
+     py::arg("s"), py::arg("sgd") = py::none());
+  m.def("tiny_mlp_can_fuse_sgd", &tiny_mlp_can_fuse_sgd);
 
   // ---- optimizer / elementwise ----
   m.def("sgd_momentum", [](uptr p, uptr g, uptr buf, uptr shadow, long long n, uptr hp, int nesterov,

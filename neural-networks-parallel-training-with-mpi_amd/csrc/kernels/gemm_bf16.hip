@@ -50,6 +50,7 @@ struct GemmParams {
   float* bias_grad;
   long long bg_split_stride;
   unsigned a_bytes, b_bytes;  // extents of A / B storage (buffer-resource range, DMA path)
+  SgdFuse sg;                 // EPI_F32 without split-K: apply the optimizer instead of storing
 };
 
 // s_waitcnt with only the vector-memory counter constrained (lgkm/exp counters left free).
@@ -175,14 +176,19 @@ __device__ __forceinline__ bf16x8 read_frag_async(const char* lds, int xb, int k
 // finished and stored: no load waits behind the stores (stores count in vmcnt on gfx950).
 // mrow[i]: this lane's output row of fragment row i; ncol[j]: first of its 4 output columns of
 // fragment column j.
+// bias_pre: the bias fragments already loaded at kernel start (EPI_BIAS_ACT; null: load here).
 template <int MI, int NJ, int EPI, int ACT, bool BIASGRAD>
 __device__ __forceinline__ void epilogue_store(const GemmParams& p, f32x4 (&acc)[MI][NJ],
                                                f32x4 (&accb)[MI], bool do_bg, const int (&mrow)[MI],
-                                               const int (&ncol)[NJ], int lane, int split) {
+                                               const int (&ncol)[NJ], int lane, int split,
+                                               const f32x4* bias_pre = nullptr) {
   if constexpr (EPI == EPI_BIAS_ACT) {
     f32x4 bias[NJ];
     // unconditional (clamped) loads: no per-element branch -> no vmcnt(0) per element
-    if (p.bias) {
+    if (bias_pre) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bias[j] = bias_pre[j];
+    } else if (p.bias) {
 #pragma unroll
       for (int j = 0; j < NJ; ++j) bias[j] = *reinterpret_cast<const f32x4*>(p.bias + min(ncol[j], p.N - 4));
     } else {
@@ -230,13 +236,18 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& p, f32x4 (&acc)
     }
   } else {
     float* cbase = reinterpret_cast<float*>(p.C) + split * p.c_split_stride;
+    // a final (un-split) weight gradient on a single rank: the optimizer update is applied
+    // here, in the epilogue -- no gradient store and no separate optimizer pass over it
+    const bool fuse = p.sg.g_base != nullptr;
 #pragma unroll
     for (int i = 0; i < MI; ++i) {
       if (mrow[i] >= p.M) continue;
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         if (ncol[j] >= p.N) continue;
-        *reinterpret_cast<f32x4*>(cbase + (long long)mrow[i] * p.ldc + ncol[j]) = acc[i][j];
+        float* g = cbase + (long long)mrow[i] * p.ldc + ncol[j];
+        if (fuse) sgd_fused_store4(p.sg, g, acc[i][j]);
+        else *reinterpret_cast<f32x4*>(g) = acc[i][j];
       }
     }
   }
@@ -246,7 +257,10 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& p, f32x4 (&acc)
 #pragma unroll
       for (int i = 0; i < MI; ++i) {
         const int m = mrow[i];
-        if (m < p.M) p.bias_grad[split * p.bg_split_stride + m] = accb[i][0];
+        if (m >= p.M) continue;
+        float* g = p.bias_grad + split * p.bg_split_stride + m;
+        if (p.sg.g_base) sgd_fused_store(p.sg, g, accb[i][0]);
+        else *g = accb[i][0];
       }
     }
   }
@@ -257,7 +271,8 @@ template <int BM, int BN, int WGM, int WGN, int EPI, int ACT, bool BIASGRAD>
 __device__ __forceinline__ void gemm_epilogue(const GemmParams& p,
                                               f32x4 (&acc)[BM / WGM / 16][BN / WGN / 16],
                                               f32x4 (&accb)[BM / WGM / 16], bool do_bg, int m0, int n0,
-                                              int wm, int wn, int lane, int split) {
+                                              int wm, int wn, int lane, int split,
+                                              const f32x4* bias_pre = nullptr) {
   constexpr int WM = BM / WGM, WN = BN / WGN, MI = WM / 16, NJ = WN / 16;
   int mrow[MI];
   int ncol[NJ];
@@ -265,7 +280,7 @@ __device__ __forceinline__ void gemm_epilogue(const GemmParams& p,
   for (int i = 0; i < MI; ++i) mrow[i] = m0 + wm * WM + i * 16 + (lane & 15);
 #pragma unroll
   for (int j = 0; j < NJ; ++j) ncol[j] = n0 + wn * WN + j * 16 + (lane >> 4) * 4;
-  epilogue_store<MI, NJ, EPI, ACT, BIASGRAD>(p, acc, accb, do_bg, mrow, ncol, lane, split);
+  epilogue_store<MI, NJ, EPI, ACT, BIASGRAD>(p, acc, accb, do_bg, mrow, ncol, lane, split, bias_pre);
 }
 
 template <int BM, int BN, int LA, int LB, int EPI, int ACT, bool BIASGRAD>
@@ -430,6 +445,17 @@ __device__ __forceinline__ void dma_gemm_tile(const GemmParams& p, char* smem, i
   const int kend = min(p.K, kbeg + p.k_per_split);
   const int nt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
 
+  // The epilogue's bias is fetched before the main loop (it is the oldest load, so the ring's
+  // counted vmcnt waits retire it first): no dependent L2 round trip between the last MFMA and
+  // the first output store.
+  f32x4 bias_pre[EPI == EPI_BIAS_ACT ? NJ : 1];
+  if constexpr (EPI == EPI_BIAS_ACT) {
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int c = min(n0 + wn * WN + j * 16 + (lane >> 4) * 4, p.N - 4);
+      bias_pre[j] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+  }
   const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)p.a_bytes, 0x00020000);
   const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)p.b_bytes, 0x00020000);
   DmaPlan<BM, LA, NW> da;
@@ -558,7 +584,8 @@ __device__ __forceinline__ void dma_gemm_tile(const GemmParams& p, char* smem, i
     // all of this wave's LDS reads of stage t are consumed before the next barrier
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
   }
-  gemm_epilogue<BM, BN, WGM, WGN, EPI, ACT, BIASGRAD>(p, acc, accb, do_bg, m0, n0, wm, wn, lane, split);
+  gemm_epilogue<BM, BN, WGM, WGN, EPI, ACT, BIASGRAD>(p, acc, accb, do_bg, m0, n0, wm, wn, lane, split,
+                                                      EPI == EPI_BIAS_ACT ? bias_pre : nullptr);
 }
 
 template <int BM, int BN, int WGM, int WGN, int LA, int LB, int EPI, int ACT, bool BIASGRAD, int NS>
@@ -1102,6 +1129,7 @@ static int make_wgrad(const WgradArgs& a, GemmParams& p, SlabReduce& pending) {
   if (splits == 1) {
     p.C = a.dW; p.ldc = N; p.c_split_stride = 0;
     p.bias_grad = a.db; p.bg_split_stride = 0;
+    p.sg = a.sg;          // (g_base null: plain gradient store)
     return splits;
   }
   p.C = a.ws; p.ldc = N; p.c_split_stride = (long long)M * N;
@@ -1210,6 +1238,12 @@ static bool group_enabled() {
   return g_group == 1;
 }
 
+bool bwd_group_supported(int rows, int out_f, int in_f) {
+  // the grouped kernel covers the 128x128 tile shapes of the default DMA main loop
+  return group_enabled() && gemm_impl() == 2 && g_variant == 0 && pick_tile(rows, in_f) == 128 &&
+         wgrad_tile(out_f, in_f) == 128;
+}
+
 hipError_t bwd_group(const DgradArgs* dg, const WgradArgs* wg, const SlabReduce* red,
                      SlabReduce* wg_pending, hipStream_t s) {
   if (wg_pending) *wg_pending = SlabReduce{};
@@ -1219,6 +1253,9 @@ hipError_t bwd_group(const DgradArgs* dg, const WgradArgs* wg, const SlabReduce*
   SlabReduce pend{};
   int splits = 0;
   if (wg) splits = make_wgrad(*wg, pw, pend);
+  // an un-split wgrad would apply the optimizer in its epilogue while dgrad_i (same launch, or
+  // earlier in the fallback) still reads W_i: refuse instead of racing
+  if (dg && wg && splits == 1 && wg->sg.g_base) return hipErrorInvalidValue;
   // the grouped kernel covers the 128x128 tile shapes of the default DMA main loop
   bool ok = group_enabled() && gemm_impl() == 2 && g_variant == 0;
   if (dg) ok = ok && pick_tile(dg->M, dg->N) == 128;

@@ -75,12 +75,19 @@ __device__ __forceinline__ void store8(TA* p, const float (&v)[8]) {
 template <typename TA, int CMAX, int LOSS, int ACT, bool FUSE, int RPW, int OUTM, int HW>
 __global__ void __launch_bounds__(64 * HW) head_fwd_kernel(HeadArgs p, float* __restrict__ wslab,
                                                            float* __restrict__ bslab) {
-  extern __shared__ __attribute__((aligned(16))) float wl[];  // [out][in] (+ [in] if FUSE)
+  // W image [out][2][in/8][4]: element (o, k = 8c + 4h + j) at o*in + h*(in/2) + 4c + j, so the
+  // 64 lanes of a wave, each owning the 8 consecutive columns of chunk c, read one half h as ONE
+  // 16-byte word at consecutive addresses (the plain [out][in] image put lanes 32 B apart:
+  // 8-way bank conflicts on every weight read, 58.7M of 70.3M LDS cycles of the MNIST head)
+  extern __shared__ __attribute__((aligned(16))) float wl[];  // W image (+ [HW][in] if FUSE)
   constexpr int NT = 64 * HW;
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
   const int nW = p.out * p.in;
-  for (int i = tid * 4; i < nW; i += NT * 4)
-    *reinterpret_cast<float4*>(wl + i) = *reinterpret_cast<const float4*>(p.W + i);
+  const int nch8 = p.in >> 3;
+  for (int i = tid; i < nW; i += NT) {
+    const int o = i / p.in, k = i - o * p.in;
+    wl[o * p.in + ((k >> 2) & 1) * (nch8 * 4) + (k >> 3) * 4 + (k & 3)] = p.W[i];
+  }
   __shared__ float red[HW][2];
   __syncthreads();
 
@@ -108,7 +115,7 @@ __global__ void __launch_bounds__(64 * HW) head_fwd_kernel(HeadArgs p, float* __
 #pragma unroll
     for (int c = 0; c < CMAX; ++c)
 #pragma unroll
-      for (int e = 0; e < 8; ++e) wreg[c][e] = wl[chc[c] * 8 + e] * cmask[c];
+      for (int e = 0; e < 8; ++e) wreg[c][e] = wl[(e >> 2) * (nch8 * 4) + chc[c] * 4 + (e & 3)] * cmask[c];
   }
   float bias[OUTM];
 #pragma unroll
@@ -116,6 +123,12 @@ __global__ void __launch_bounds__(64 * HW) head_fwd_kernel(HeadArgs p, float* __
 
   const int gw = blockIdx.x * HW + w, nwaves = gridDim.x * HW;
   for (int r0 = gw * RPW; r0 < p.rows; r0 += nwaves * RPW) {
+    // Multi-output heads read W from LDS for every row: an offset the compiler cannot see
+    // through keeps it from hoisting all OUTM x CMAX x 8 weights into registers across the row
+    // loop (256 VGPRs + 128 spilled for out = 10, in = 1024 -> 135 us; PMC/resource-usage).
+    int wo = 0;
+    if constexpr (!FUSE) asm volatile("" : "+v"(wo));
+    const float* wlo = wl + wo;
     float av[RPW][CMAX][8];
     float yv[RPW][OUTM];
     int labv[RPW];
@@ -144,10 +157,13 @@ __global__ void __launch_bounds__(64 * HW) head_fwd_kernel(HeadArgs p, float* __
 #pragma unroll
             for (int e = 0; e < 8; ++e) sacc += av[q][c][e] * wreg[c][e];
           } else {
-            const float* wr = wl + min(o, nout - 1) * p.in + chc[c] * 8;
-            float t = 0.f;
-#pragma unroll
-            for (int e = 0; e < 8; ++e) t += av[q][c][e] * wr[e];
+            if (o >= nout) continue;   // uniform: no work for the padding outputs
+            const float* wr = wlo + o * p.in + chc[c] * 4;
+            const float4 w0 = *reinterpret_cast<const float4*>(wr);
+            const float4 w1 = *reinterpret_cast<const float4*>(wr + nch8 * 4);
+            const float t = av[q][c][0] * w0.x + av[q][c][1] * w0.y + av[q][c][2] * w0.z +
+                            av[q][c][3] * w0.w + av[q][c][4] * w1.x + av[q][c][5] * w1.y +
+                            av[q][c][6] * w1.z + av[q][c][7] * w1.w;
             sacc += t * cmask[c];
           }
         }
@@ -158,7 +174,8 @@ __global__ void __launch_bounds__(64 * HW) head_fwd_kernel(HeadArgs p, float* __
 #pragma unroll
       for (int q = 0; q < RPW; ++q)
 #pragma unroll
-        for (int o = 0; o < OUTM; ++o) part[q][o] += __shfl_xor(part[q][o], sh, 64);
+        for (int o = 0; o < OUTM; ++o)
+          if (o < nout) part[q][o] += __shfl_xor(part[q][o], sh, 64);
 
 #pragma unroll
     for (int q = 0; q < RPW; ++q) {
@@ -223,9 +240,12 @@ __global__ void __launch_bounds__(64 * HW) head_fwd_kernel(HeadArgs p, float* __
 #pragma unroll
               for (int e = 0; e < 8; ++e) g[e] += dl[o] * wreg[c][e];
             } else {
-              const float* wr = wl + min(o, nout - 1) * p.in + chc[c] * 8;
-#pragma unroll
-              for (int e = 0; e < 8; ++e) g[e] += dl[o] * wr[e];
+              if (o >= nout) continue;
+              const float* wr = wlo + o * p.in + chc[c] * 4;
+              const float4 w0 = *reinterpret_cast<const float4*>(wr);
+              const float4 w1 = *reinterpret_cast<const float4*>(wr + nch8 * 4);
+              g[0] += dl[o] * w0.x; g[1] += dl[o] * w0.y; g[2] += dl[o] * w0.z; g[3] += dl[o] * w0.w;
+              g[4] += dl[o] * w1.x; g[5] += dl[o] * w1.y; g[6] += dl[o] * w1.z; g[7] += dl[o] * w1.w;
             }
           }
 #pragma unroll
@@ -377,15 +397,21 @@ hipError_t head_fused(const void* a, int a_bf16, int rows, int in, const float* 
 
 // ---- head weight gradient: gW[o][i] = sum_r dl[r][o] a[r][i], gb[o] = sum_r dl[r][o] ----
 template <typename TA, int OMAX>
-__global__ void __launch_bounds__(64) head_wgrad_kernel(const TA* __restrict__ a, int rows, int in,
-                                                        const float* __restrict__ dl, int out,
-                                                        int rows_per_split, float* __restrict__ ws,
-                                                        float* __restrict__ wsb) {
-  const int lane = threadIdx.x;
+__global__ void __launch_bounds__(256) head_wgrad_kernel(const TA* __restrict__ a, int rows, int in,
+                                                         const float* __restrict__ dl, int out,
+                                                         int rows_per_split, float* __restrict__ ws,
+                                                         float* __restrict__ wsb) {
+  // 4 waves per block share one (512-column, split) job: wave w takes the w-th quarter of the
+  // split's rows, and the waves are combined through LDS in wave order (deterministic)
+  __shared__ __attribute__((aligned(16))) float cmb[OMAX * 512 + OMAX];
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
   const int c0 = blockIdx.x * 512 + lane * 8;
   const int split = blockIdx.y;
-  const int r0 = split * rows_per_split;
-  const int r1 = min(rows, r0 + rows_per_split);
+  const int s0 = split * rows_per_split;
+  const int s1 = min(rows, s0 + rows_per_split);
+  const int q4 = (s1 - s0 + 3) / 4;
+  const int r0 = s0 + w * q4;
+  const int r1 = min(s1, r0 + q4);
   float acc[OMAX][8];
   float accb[OMAX];
 #pragma unroll
@@ -395,34 +421,61 @@ __global__ void __launch_bounds__(64) head_wgrad_kernel(const TA* __restrict__ a
     for (int e = 0; e < 8; ++e) acc[o][e] = 0.f;
   }
   const bool active = c0 < in;
-  for (int r = r0; r < r1; ++r) {
-    float av[8];
-    if (active) load8<TA>(a + (long long)r * in + c0, av);
+  const int cc = active ? c0 : 0;   // clamped column: loads stay unconditional
+  // rows in batches of RB: every load of the batch is issued before the first FMA (a single
+  // row per iteration exposed one dependent L2 round trip per row: 59 us for 8192 x 1024)
+  constexpr int RB = 4;
+  for (int r = r0; r < r1; r += RB) {
+    float av[RB][8];
+    float dv[RB][OMAX];
 #pragma unroll
-    for (int o = 0; o < OMAX; ++o) {
-      if (o < out) {
-        const float d = dl[(long long)r * out + o];
-        accb[o] += d;
-        if (active) {
+    for (int q = 0; q < RB; ++q) {
+      const int rr = min(r + q, r1 - 1);
+      const float live = (r + q) < r1 ? 1.f : 0.f;
+      load8<TA>(a + (long long)rr * in + cc, av[q]);
 #pragma unroll
-          for (int e = 0; e < 8; ++e) acc[o][e] += d * av[e];
+      for (int o = 0; o < OMAX; ++o) dv[q][o] = dl[(long long)rr * out + min(o, out - 1)] * live;
+    }
+#pragma unroll
+    for (int q = 0; q < RB; ++q)
+#pragma unroll
+      for (int o = 0; o < OMAX; ++o) {
+        if (o < out) {
+          accb[o] += dv[q][o];
+#pragma unroll
+          for (int e = 0; e < 8; ++e) acc[o][e] += dv[q][o] * av[q][e];
         }
       }
-    }
   }
-  if (active) {
+  for (int ww = 0; ww < 4; ++ww) {
+    if (w == ww) {
+#pragma unroll
+      for (int o = 0; o < OMAX; ++o) {
+        float* d = cmb + o * 512 + lane * 8;
+#pragma unroll
+        for (int e = 0; e < 8; ++e) d[e] = ww ? d[e] + acc[o][e] : acc[o][e];
+      }
+      if (lane == 0) {
+#pragma unroll
+        for (int o = 0; o < OMAX; ++o) cmb[OMAX * 512 + o] = ww ? cmb[OMAX * 512 + o] + accb[o] : accb[o];
+      }
+    }
+    __syncthreads();
+  }
+  if (w == 0 && active) {
 #pragma unroll
     for (int o = 0; o < OMAX; ++o) {
       if (o < out) {
         float* dst = ws + ((long long)split * out + o) * in + c0;
-        *reinterpret_cast<float4*>(dst) = make_float4(acc[o][0], acc[o][1], acc[o][2], acc[o][3]);
-        *reinterpret_cast<float4*>(dst + 4) = make_float4(acc[o][4], acc[o][5], acc[o][6], acc[o][7]);
+        const float* src = cmb + o * 512 + lane * 8;
+        *reinterpret_cast<float4*>(dst) = *reinterpret_cast<const float4*>(src);
+        *reinterpret_cast<float4*>(dst + 4) = *reinterpret_cast<const float4*>(src + 4);
       }
     }
   }
-  if (blockIdx.x == 0 && lane == 0) {
+  if (blockIdx.x == 0 && threadIdx.x == 0) {
 #pragma unroll
-    for (int o = 0; o < OMAX; ++o) if (o < out) wsb[(long long)split * out + o] = accb[o];
+    for (int o = 0; o < OMAX; ++o) if (o < out) wsb[(long long)split * out + o] = cmb[OMAX * 512 + o];
   }
 }
 
@@ -448,14 +501,14 @@ hipError_t head_wgrad(const void* a, int a_bf16, int rows, int in, const float* 
   dim3 grid((in + 511) / 512, S);
   if (a_bf16) {
     const bf16* A = reinterpret_cast<const bf16*>(a);
-    if (out == 1) hipLaunchKernelGGL((head_wgrad_kernel<bf16, 1>), grid, dim3(64), 0, s, A, rows, in, dlogits, out, rps, ws, wsb);
-    else if (out <= 4) hipLaunchKernelGGL((head_wgrad_kernel<bf16, 4>), grid, dim3(64), 0, s, A, rows, in, dlogits, out, rps, ws, wsb);
-    else hipLaunchKernelGGL((head_wgrad_kernel<bf16, 16>), grid, dim3(64), 0, s, A, rows, in, dlogits, out, rps, ws, wsb);
+    if (out == 1) hipLaunchKernelGGL((head_wgrad_kernel<bf16, 1>), grid, dim3(256), 0, s, A, rows, in, dlogits, out, rps, ws, wsb);
+    else if (out <= 4) hipLaunchKernelGGL((head_wgrad_kernel<bf16, 4>), grid, dim3(256), 0, s, A, rows, in, dlogits, out, rps, ws, wsb);
+    else hipLaunchKernelGGL((head_wgrad_kernel<bf16, 16>), grid, dim3(256), 0, s, A, rows, in, dlogits, out, rps, ws, wsb);
   } else {
     const float* A = reinterpret_cast<const float*>(a);
-    if (out == 1) hipLaunchKernelGGL((head_wgrad_kernel<float, 1>), grid, dim3(64), 0, s, A, rows, in, dlogits, out, rps, ws, wsb);
-    else if (out <= 4) hipLaunchKernelGGL((head_wgrad_kernel<float, 4>), grid, dim3(64), 0, s, A, rows, in, dlogits, out, rps, ws, wsb);
-    else hipLaunchKernelGGL((head_wgrad_kernel<float, 16>), grid, dim3(64), 0, s, A, rows, in, dlogits, out, rps, ws, wsb);
+    if (out == 1) hipLaunchKernelGGL((head_wgrad_kernel<float, 1>), grid, dim3(256), 0, s, A, rows, in, dlogits, out, rps, ws, wsb);
+    else if (out <= 4) hipLaunchKernelGGL((head_wgrad_kernel<float, 4>), grid, dim3(256), 0, s, A, rows, in, dlogits, out, rps, ws, wsb);
+    else hipLaunchKernelGGL((head_wgrad_kernel<float, 16>), grid, dim3(256), 0, s, A, rows, in, dlogits, out, rps, ws, wsb);
   }
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;

@@ -91,6 +91,7 @@ struct WgradArgs {
   float* ws; SgdFuse sg;
 };
 void set_bwd_group(int on);   // 1 = grouped kernel (default), 0 = separate launches (A/B)
+bool bwd_group_supported(int rows, int out_f, int in_f);   // this layer shape runs grouped
 hipError_t bwd_group(const DgradArgs* dg, const WgradArgs* wg, const SlabReduce* red,
                      SlabReduce* wg_pending, hipStream_t s);
 
@@ -133,9 +134,13 @@ struct TinyMLPDesc {
   int loss;
 };
 size_t tiny_mlp_workspace_bytes(int rows, int arena_numel);
+// sgd != nullptr (single block, i.e. rows <= 256, single rank): the kernel applies the optimizer
+// update itself instead of storing the gradient (the whole step is ONE launch).
 hipError_t tiny_mlp_step(const TinyMLPDesc& d, const float* params, const float* X,
                          const float* y, const int64_t* labels, int rows, float inv_count,
-                         float* grad, int arena_numel, float* ws, float* loss_out, hipStream_t s);
+                         float* grad, int arena_numel, float* ws, float* loss_out, hipStream_t s,
+                         const SgdFuse* sgd = nullptr);
+bool tiny_mlp_can_fuse_sgd(int rows);
 
 // ---- optimizer / elementwise (optim.hip) ----
 // hp = {lr, momentum, dampening, weight_decay, grad_scale}

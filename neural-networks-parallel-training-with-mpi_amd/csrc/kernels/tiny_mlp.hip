@@ -19,16 +19,23 @@ constexpr int TW = 16;
 constexpr int TL = 4;
 
 template <int ACT, int LOSS>
-__global__ void __launch_bounds__(256) tiny_mlp_kernel(TinyMLPDesc d, const float* __restrict__ P,
+__global__ void __launch_bounds__(256) tiny_mlp_kernel(TinyMLPDesc d, const float* P,
                                                        const float* __restrict__ X,
                                                        const float* __restrict__ Y,
                                                        const int64_t* __restrict__ labels, int rows,
                                                        float inv_count, float* __restrict__ gout,
                                                        long long slab, int numel,
-                                                       float* __restrict__ loss_part) {
-  extern __shared__ __attribute__((aligned(16))) float wsum[];  // [4][numel]
+                                                       float* __restrict__ loss_part,
+                                                       float loss_scale, float* __restrict__ loss_out,
+                                                       SgdFuse sg) {
+  extern __shared__ __attribute__((aligned(16))) float wsum[];  // [4][numel] + params [numel]
   const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6;
+  // the model's parameters are staged in LDS by one coalesced pass: every later weight read is
+  // an LDS read instead of a dependent global round trip inside the unrolled layer loops
+  const int pbase = d.w_off[d.n_layers - 1];
+  float* PL = wsum + 4 * numel - pbase;      // PL[arena offset] for offsets in [pbase, +numel)
   for (int i = tid; i < 4 * numel; i += 256) wsum[i] = 0.f;
+  for (int i = tid; i < numel; i += 256) PL[pbase + i] = P[pbase + i];
   __shared__ float red[4];
   __syncthreads();
   const int L = d.n_layers;
@@ -45,8 +52,8 @@ __global__ void __launch_bounds__(256) tiny_mlp_kernel(TinyMLPDesc d, const floa
     for (int l = 0; l < TL; ++l) {
       if (l < L) {
         const int win = d.widths[l], wout = d.widths[l + 1];
-        const float* W = P + d.w_off[l];
-        const float* B = P + d.b_off[l];
+        const float* W = PL + d.w_off[l];
+        const float* B = PL + d.b_off[l];
 #pragma unroll
         for (int o = 0; o < TW; ++o) {
           float z = 0.f;
@@ -96,7 +103,7 @@ __global__ void __launch_bounds__(256) tiny_mlp_kernel(TinyMLPDesc d, const floa
     for (int l = TL - 1; l >= 0; --l) {
       if (l < L) {
         const int win = d.widths[l], wout = d.widths[l + 1];
-        const float* W = P + d.w_off[l];
+        const float* W = PL + d.w_off[l];
         float* gw = wsum + w * numel + d.w_off[l] - d.w_off[L - 1];
         float* gb = wsum + w * numel + d.b_off[l] - d.w_off[L - 1];
 #pragma unroll
@@ -135,12 +142,20 @@ __global__ void __launch_bounds__(256) tiny_mlp_kernel(TinyMLPDesc d, const floa
   // arena region covered by this model starts at the last layer's W (reverse layout)
   float* dst = gout + (long long)blockIdx.x * slab;
   for (int i = tid; i < numel; i += 256) {
-    dst[i] = ((wsum[i] + wsum[numel + i]) + wsum[2 * numel + i]) + wsum[3 * numel + i];
+    const float g = ((wsum[i] + wsum[numel + i]) + wsum[2 * numel + i]) + wsum[3 * numel + i];
+    // single block + single rank: the gradient is final -> optimizer update right here (every
+    // read of the parameters happened before the barrier above); else store it
+    if (sg.g_base) sgd_fused_store(sg, dst + i, g);
+    else dst[i] = g;
   }
   wave_loss = wave_sum(wave_loss);  // lanes own different rows here
   if (lane == 0) red[w] = wave_loss;
   __syncthreads();
-  if (tid == 0) loss_part[blockIdx.x] = red[0] + red[1] + red[2] + red[3];
+  if (tid == 0) {
+    const float t = red[0] + red[1] + red[2] + red[3];
+    loss_part[blockIdx.x] = t;
+    if (loss_out) *loss_out = t * loss_scale;   // one block: no separate loss reduce
+  }
 }
 
 static int tiny_blocks(int rows) { return std::max(1, std::min((rows + 255) / 256, 256)); }
@@ -153,7 +168,8 @@ size_t tiny_mlp_workspace_bytes(int rows, int arena_numel) {
 
 hipError_t tiny_mlp_step(const TinyMLPDesc& d, const float* params, const float* X,
                          const float* y, const int64_t* labels, int rows, float inv_count,
-                         float* grad, int arena_numel, float* ws, float* loss_out, hipStream_t s) {
+                         float* grad, int arena_numel, float* ws, float* loss_out, hipStream_t s,
+                         const SgdFuse* sgd) {
   if (d.n_layers < 1 || d.n_layers > TL) return hipErrorInvalidValue;
   for (int l = 0; l <= d.n_layers; ++l)
     if (d.widths[l] < 1 || d.widths[l] > TW) return hipErrorInvalidValue;
@@ -161,15 +177,20 @@ hipError_t tiny_mlp_step(const TinyMLPDesc& d, const float* params, const float*
   // the model occupies arena[w_off[L-1] .. arena_numel) (reverse layer order, W_{L-1} first)
   const int base = d.w_off[d.n_layers - 1];
   const int numel = arena_numel - base;
-  const size_t smem = (size_t)4 * numel * sizeof(float);
+  const size_t smem = (size_t)5 * numel * sizeof(float);
   if (smem > 150 * 1024) return hipErrorInvalidValue;
   float* loss_part = ws;
   float* slabs = ws + ((nb + 3) & ~3) + 4;  // keep 16-byte alignment for the vector reducer
   float* gout = nb > 1 ? slabs : grad + base;
   const long long slab = nb > 1 ? numel : 0;
+  const float loss_scale = d.loss == LOSS_XENT ? 1.f / rows : 1.f / ((float)rows * d.widths[d.n_layers]);
+  // one block: loss written and (single rank) optimizer applied in-kernel -> ONE launch per step
+  SgdFuse sg{};
+  if (nb == 1 && sgd) sg = *sgd;
+  float* lout = nb == 1 ? loss_out : nullptr;
 #define TINY_LAUNCH(A, LS)                                                                   \
   hipLaunchKernelGGL((tiny_mlp_kernel<A, LS>), dim3(nb), dim3(256), smem, s, d, params, X, y, \
-                     labels, rows, inv_count, gout, slab, numel, loss_part)
+                     labels, rows, inv_count, gout, slab, numel, loss_part, loss_scale, lout, sg)
   if (d.loss == LOSS_XENT) {
     if (d.act == ACT_TANH) TINY_LAUNCH(ACT_TANH, LOSS_XENT);
     else TINY_LAUNCH(ACT_RELU, LOSS_XENT);
@@ -180,13 +201,14 @@ hipError_t tiny_mlp_step(const TinyMLPDesc& d, const float* params, const float*
 #undef TINY_LAUNCH
   hipError_t e = hipGetLastError();
   if (e != hipSuccess) return e;
-  const float loss_scale = d.loss == LOSS_XENT ? 1.f / rows : 1.f / ((float)rows * d.widths[d.n_layers]);
   if (nb > 1) {
+    if (sgd) return hipErrorInvalidValue;   // the optimizer fusion needs the single-block form
     return splitk_reduce(slabs, nb, numel, 1, numel, grad + base, numel, nullptr, 0, nullptr,
                          loss_part, nb, loss_scale, loss_out, s);
   }
-  return splitk_reduce(nullptr, 0, 0, 0, 4, nullptr, 4, nullptr, 0, nullptr, loss_part, 1,
-                       loss_scale, loss_out, s);
+  return hipSuccess;
 }
+
+bool tiny_mlp_can_fuse_sgd(int rows) { return tiny_blocks(rows) == 1; }
 
 }  // namespace nnmpi

@@ -79,6 +79,10 @@ class MLPEngine:
         from ..parallel.sync import NoSync
         self.fuse_sgd = (bool(fuse_sgd) and self.overlap and isinstance(sync, NoSync)
                          and dtype == torch.bfloat16 and hasattr(ops, "sgd_fusion"))
+        # tiny single-rank model: the one-block kernel applies SGD itself (one launch per step)
+        self.tiny_fused = (bool(fuse_sgd) and self.use_tiny and isinstance(sync, NoSync)
+                           and hasattr(ops, "tiny_can_fuse_sgd") and ops.tiny_can_fuse_sgd(self.R))
+        self._first = True
         self.ws = torch.zeros(max(1, self._workspace_bytes() // 4 + 64), dtype=torch.float32,
                               device=dev)
         # grouped backward (bf16 GPU): dgrad_i + wgrad_i + combine_{i+1} in one launch.  Layer
@@ -87,8 +91,12 @@ class MLPEngine:
         self.sharded = bool(getattr(sync, "sharded", False))
         inline_sync = (isinstance(sync, NoSync) or self.sharded or
                        (isinstance(sync, NativeRcclSync) and sync.inline))
+        # (shapes the grouped kernel does not cover -- e.g. the 256x256-tile 8192-wide layers --
+        # take the sequential fused schedule, whose un-split wgrads apply SGD in their epilogue)
         self.grouped = (bool(grouped) and self.overlap and dtype == torch.bfloat16 and inline_sync
-                        and hasattr(ops, "bwd_group") and L > 1)
+                        and hasattr(ops, "bwd_group") and L > 1 and
+                        all(ops.bwd_group_supported(self.R, *spec.layer_shape(i))
+                            for i in range(L - 1)))
         self.ws_pair = [self.ws, torch.zeros_like(self.ws)] if self.grouped else [self.ws, self.ws]
         if self.is_cuda:
             self.ev_wfree = [torch.cuda.Event(enable_timing=False) for _ in range(L)]
@@ -177,9 +185,11 @@ class MLPEngine:
                 self.sync.ready(i)
             return
         if self.use_tiny:
+            fz = (ops.sgd_fusion(ar, self.hp, self.nesterov, self._first)
+                  if self.tiny_fused else None)
             ops.tiny_step(self.spec, ar, self.X[:rows], self.Y[:rows] if self.Y is not None else None,
                           self.labels[:rows] if self.labels is not None else None,
-                          self.inv_count, self.loss_out, self.ws)
+                          self.inv_count, self.loss_out, self.ws, sgd=fz)
             for i in reversed(range(L)):
                 self.sync.ready(i)
             return
@@ -224,11 +234,13 @@ class MLPEngine:
         if self.overlap:
             self._step_body_overlap(first)
         else:
+            self._first = first
             self.sync.begin()
             self.forward_backward()
             self.sync.finish()
             self._mark("comm")
-            self._update(first)
+            if not self.tiny_fused:
+                self._update(first)
         self._mark("update")
 
     def _update(self, first: bool):
@@ -309,7 +321,9 @@ class MLPEngine:
                 ops.linear_dgrad(dz_i, ar.compute_weight(i), self.acts[i - 1][:rows], self.act, dz_next)
                 dz = dz_next
             out_f, in_f = self.spec.layer_shape(i)
-            if ops.wgrad_can_fuse_sgd(rows, out_f, in_f, self.dtype):
+            # dgrad_i was issued above: nothing reads W_i any more, so even an un-split wgrad
+            # may update it in its epilogue
+            if ops.wgrad_can_fuse_sgd(rows, out_f, in_f, self.dtype, epilogue=True):
                 ops.linear_wgrad(dz_i, x_in, ar.grad_weight(i), ar.grad_bias(i), ws=self.ws, sgd=fz)
             else:
                 ops.linear_wgrad(dz_i, x_in, ar.grad_weight(i), ar.grad_bias(i), ws=self.ws)

@@ -71,9 +71,13 @@ class HipOps:
             return int(self.lib.wgrad_workspace_bytes(out_f, in_f, rows))
         return int(self.lib.wgrad_f32_workspace_bytes(out_f, in_f, rows))
 
-    def wgrad_can_fuse_sgd(self, rows, out_f, in_f, dtype) -> bool:
-        """True when the wgrad's split-K reducer can apply the optimizer update itself."""
-        return dtype == torch.bfloat16 and bool(self.lib.wgrad_will_split(out_f, in_f, rows))
+    def wgrad_can_fuse_sgd(self, rows, out_f, in_f, dtype, epilogue: bool = False) -> bool:
+        """True when the wgrad can apply the optimizer update itself: in its split-K reducer, or
+        (``epilogue=True``: the caller guarantees nothing reads this layer's weights afterwards)
+        in the GEMM epilogue when there is no split."""
+        if dtype != torch.bfloat16:
+            return False
+        return epilogue or bool(self.lib.wgrad_will_split(out_f, in_f, rows))
 
     @staticmethod
     def sgd_fusion(arena, hp, nesterov: bool, first: bool):
@@ -146,6 +150,9 @@ class HipOps:
                                             _p(gW), _p(gb), _p(ws[off:]), _p(ws[:parts]),
                                             float(loss_scale), _p(loss_out), self.stream, sgd)
 
+    def bwd_group_supported(self, rows, out_f, in_f) -> bool:
+        return bool(self.lib.bwd_group_supported(rows, out_f, in_f))
+
     def bwd_group(self, dgrad, wgrad, sgd, pending):
         """One grouped launch: dgrad of layer i (``(dz, W, a_prev, act, out)`` or None), wgrad of
         layer i (``(dz, x, gW, gb, ws)`` or None, optional optimizer fusion ``sgd``) and the
@@ -175,14 +182,17 @@ class HipOps:
     def tiny_workspace_bytes(self, rows, numel) -> int:
         return int(self.lib.tiny_mlp_workspace_bytes(rows, numel))
 
-    def tiny_step(self, spec, arena, X, y, labels, inv_count, loss_out, ws):
+    def tiny_can_fuse_sgd(self, rows: int) -> bool:
+        return bool(self.lib.tiny_mlp_can_fuse_sgd(rows))
+
+    def tiny_step(self, spec, arena, X, y, labels, inv_count, loss_out, ws, sgd=None):
         L = spec.n_layers
         w_off = [arena.by_name[f"layers.{2 * i}.weight"].offset for i in range(L)]
         b_off = [arena.by_name[f"layers.{2 * i}.bias"].offset for i in range(L)]
         self.lib.tiny_mlp_step(list(spec.widths), w_off, b_off, ACT_CODES[spec.activation],
                                LOSS_CODES[spec.loss], _p(arena.master), _p(X), _p(y), _p(labels),
                                X.shape[0], float(inv_count), _p(arena.grad), arena.numel,
-                               _p(ws), _p(loss_out), self.stream)
+                               _p(ws), _p(loss_out), self.stream, sgd)
 
     # ---------------- optimizer ----------------
     def sgd(self, arena, hp, nesterov: bool, first: bool, zero_grad: bool = True, offset: int = 0,

@@ -72,6 +72,13 @@ for s in $STEPS; do
         ok_or_stop $? "bench $c"
       done
       cat gpurun_out/bench_all.json ;;
+    profcfg)
+      # per-kernel stats of the other bench configs (mnist / ref / wide8192)
+      for c in mnist ref wide8192; do
+        rm -rf gpurun_out/prof_$c
+        timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof_$c -o run -- python3 bench.py --config $c --steps 20 --warmup 3 > gpurun_out/prof_$c.log 2>&1
+        ok_or_stop $? "prof $c"
+      done ;;
     prof)
       rm -rf gpurun_out/prof
       timeout -k 10 400 rocprofv3 --kernel-trace --stats --output-format csv -d gpurun_out/prof -o run -- python3 bench.py --steps 50 --warmup 5 > gpurun_out/prof.log 2>&1
