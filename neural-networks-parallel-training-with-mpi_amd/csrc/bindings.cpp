@@ -244,6 +244,13 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
     check(checksum_f32(P<const float>(x), n, P<double>(out), S(s)), "checksum_f32");
   });
 
+  // ---- data ----
+  m.def("gather_rows", [](uptr src, uptr dst, uptr idx, int n, long long row_bytes, long long n_src,
+                          uptr s) {
+    check(gather_rows(P<const void>(src), P<void>(dst), P<const int64_t>(idx), n, row_bytes, n_src,
+                      S(s)), "gather_rows");
+  });
+
   // ---- RCCL runtime ----
   m.def("rccl_unique_id", []() { return py::bytes(RcclComm::get_unique_id()); });
   py::class_<RcclComm>(m, "RcclComm")

@@ -151,4 +151,9 @@ hipError_t scale_f32(float* x, long long n, float a, hipStream_t s);
 hipError_t cast_bf16_f32(const bf16* x, float* y, long long n, hipStream_t s);
 hipError_t checksum_f32(const float* x, long long n, double* out, hipStream_t s);
 
+// ---- data (data.hip) ----
+// dst[r] = src[idx[r]] for r < n, rows of row_bytes (multiple of 4); indices clamped to n_src
+hipError_t gather_rows(const void* src, void* dst, const int64_t* idx, int n, long long row_bytes,
+                       long long n_src, hipStream_t s);
+
 }  // namespace nnmpi

@@ -166,6 +166,23 @@ class MLPEngine:
                 self.labels[:n].copy_(labels, non_blocking=True)
         self.rows = n
 
+    def load_batch_indexed(self, X: torch.Tensor, Y: Optional[torch.Tensor],
+                           labels: Optional[torch.Tensor], idx: torch.Tensor):
+        """Mini-batch ``idx`` (int64, on the engine's device) of a resident shard, gathered
+        straight into the persistent input buffers (HIP: one gather launch per tensor; the
+        reference's DataLoader shuffle + per-row __getitem__ + collate, ref.py:146,155)."""
+        n = idx.numel()
+        if n > self.R:
+            raise ValueError(f"batch of {n} rows exceeds capacity {self.R}")
+        ctx = torch.cuda.stream(self.stream) if self.is_cuda else _nullctx()
+        with ctx, torch.no_grad():
+            self.ops.gather_rows(X, idx, self.X)
+            if self.Y is not None and Y is not None:
+                self.ops.gather_rows(Y.reshape(Y.shape[0], self.Y.shape[1]), idx, self.Y)
+            if self.labels is not None and labels is not None:
+                self.ops.gather_rows(labels, idx, self.labels)
+        self.rows = n
+
     # ------------------------------------------------------------------------------------
     def _dz(self, k: int, rows: int, width: int) -> torch.Tensor:
         return self.dzbuf[k][: rows * width].view(rows, width)
@@ -491,6 +508,52 @@ class MLPEngine:
             raise
         g.end()
         return g
+
+    # ---------------- evaluation (forward only) ---------------------------------------------
+    def evaluate(self, X: torch.Tensor, Y: Optional[torch.Tensor] = None,
+                 labels: Optional[torch.Tensor] = None):
+        """Forward-only loss over held-out rows, chunked by the row capacity.  Parameters and
+        optimizer state are untouched (the head's gradient outputs go to scratch buffers and no
+        optimizer fusion is requested).  The training batch in the input buffers is overwritten:
+        reload it before the next step.  Returns (sum of per-row losses, rows); the reference's
+        validation/test hooks are dead code (ref.py:213-236)."""
+        n = X.shape[0]
+        if n == 0:
+            return 0.0, 0
+        out_f = self.spec.widths[-1]
+        per = out_f if self.loss_kind == "mse" else 1
+        if not hasattr(self, "_eval_gw"):
+            last = self.L - 1
+            self._eval_gw = torch.zeros_like(self.arena.grad_weight(last))
+            self._eval_gb = torch.zeros_like(self.arena.grad_bias(last))
+        total = 0.0
+        ctx = torch.cuda.stream(self.stream) if self.is_cuda else _nullctx()
+        for lo in range(0, n, self.R):
+            hi = min(n, lo + self.R)
+            self.load_batch(X[lo:hi], Y[lo:hi] if Y is not None else None,
+                            labels[lo:hi] if labels is not None else None)
+            rows = self.rows
+            with ctx, torch.no_grad():
+                if self.use_tiny:
+                    # the one-block kernel's mean loss (its gradient output is rewritten by the
+                    # next training step; no optimizer fusion here)
+                    self.ops.tiny_step(self.spec, self.arena, self.X[:rows],
+                                       self.Y[:rows] if self.Y is not None else None,
+                                       self.labels[:rows] if self.labels is not None else None,
+                                       1.0 / (rows * per), self.loss_out, self.ws, sgd=None)
+                    scale = rows * per
+                else:
+                    h = self._forward(self.X[:rows])
+                    last = self.L - 1
+                    self.ops.head(h, self.arena.weight(last), self.arena.bias(last),
+                                  self.Y[:rows] if self.Y is not None else None,
+                                  self.labels[:rows] if self.labels is not None else None,
+                                  self.loss_kind, 0.0, self.act if self.L > 1 else "none", None,
+                                  self._eval_gw, self._eval_gb, self.dlogits[:rows], self.loss_out,
+                                  1.0, ws=self.ws)
+                    scale = 1.0
+            total += self.loss() * scale
+        return total, n
 
     def loss(self) -> float:
         """Local (this rank's) mean loss of the last step (host sync)."""

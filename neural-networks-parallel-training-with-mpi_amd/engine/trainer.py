@@ -52,6 +52,7 @@ class TrainResult:
     world: int
     losses: List[float] = field(default_factory=list)        # local loss per epoch (printed)
     global_losses: List[float] = field(default_factory=list)
+    val_losses: List[float] = field(default_factory=list)      # global, per epoch
     final_params: Optional[torch.Tensor] = None               # forward-order flat, fp32 CPU
     state_dict: Optional[dict] = None
     rows: int = 0
@@ -293,6 +294,19 @@ def _run(j: Job) -> TrainResult:
     cfg, rank, world = j.cfg, j.rank, j.world
     spec = MLPSpec(tuple(cfg.widths), cfg.activation, cfg.loss)
     X, Y, labels, part = build_shard(j)
+    # held-out validation rows: the tail of every shard (same rule on every rank, so the
+    # training row counts used for loss scaling are known everywhere)
+    n_val = lambda c: int(round(c * cfg.val_fraction))  # noqa: E731
+    train_counts = [c - n_val(c) for c in part.counts]
+    nv = n_val(X.shape[0])
+    if nv:
+        cut = X.shape[0] - nv
+        Xv, Yv = X[cut:], (Y[cut:] if Y is not None else None)
+        Lv = labels[cut:] if labels is not None else None
+        X, Y = X[:cut], (Y[:cut] if Y is not None else None)
+        labels = labels[:cut] if labels is not None else None
+    else:
+        Xv = Yv = Lv = None
     rows_local = X.shape[0]
     model = init_model(j, spec)
     dtype = _compute_dtype(cfg)
@@ -308,7 +322,7 @@ def _run(j: Job) -> TrainResult:
     sync = make_sync(j, arena)
     ops = make_ops(j)
     bs = cfg.batch_size
-    max_rows = part.max_rows
+    max_rows = max(train_counts)
     cap = min(bs, max_rows) if bs else max_rows
     eng = MLPEngine(spec, arena, ops, sync, device=j.device, dtype=dtype,
                     rows_capacity=max(cap, 1), lr=cfg.lr, momentum=cfg.momentum,
@@ -340,13 +354,12 @@ def _run(j: Job) -> TrainResult:
                     if not full_loaded:  # full-shard batch: order-irrelevant, uploaded once (D10)
                         eng.load_batch(Xc, Y, labels)
                         full_loaded = True
-                    rows_all = list(part.counts)
+                    rows_all = list(train_counts)
                 else:
                     lo, hi = s * bs, min((s + 1) * bs, rows_local)
                     idx = perm[lo:hi] if perm is not None else torch.arange(lo, max(lo, hi), device=j.device)
-                    eng.load_batch(Xc[idx], Y[idx] if Y is not None else None,
-                                   labels[idx] if labels is not None else None)
-                    rows_all = [max(0, min(bs, c - s * bs)) for c in part.counts]
+                    eng.load_batch_indexed(Xc, Y, labels, idx.contiguous())
+                    rows_all = [max(0, min(bs, c - s * bs)) for c in train_counts]
                 inv, lsc, gsc = loss_scales(cfg, eng.rows, rows_all, cfg.widths[-1])
                 eng.set_scales(inv, lsc, gsc)
                 eng.step()
@@ -363,10 +376,21 @@ def _run(j: Job) -> TrainResult:
                 gl = float(t[0] / max(t[1], 1.0))
                 res.global_losses.append(gl)
                 _print(cfg, rank, f"global loss: {gl}") if rank == 0 else None
+            if cfg.val_fraction > 0:
+                vs, vn = eng.evaluate(Xv.to(dtype), Yv, Lv) if Xv is not None else (0.0, 0)
+                full_loaded = False          # evaluation reused the input buffers
+                per = cfg.widths[-1] if cfg.loss == "mse" else 1
+                t = torch.tensor([vs, float(vn)], dtype=torch.float64)
+                if world > 1:
+                    j.pg.allreduce_cpu(t)
+                vl = float(t[0] / max(float(t[1]) * per, 1.0))
+                res.val_losses.append(vl)
+                _print(cfg, rank, f"validation loss: {vl}") if rank == 0 else None
             if seqchk:
                 seqchk.check(epoch, sync.seq)
             metrics.write(epoch=epoch, loss=loss, epoch_s=dt, steps=steps_per_epoch,
-                          samples_per_s=sum(part.counts) / dt if dt > 0 else None, world=world)
+                          samples_per_s=sum(train_counts) / dt if dt > 0 else None, world=world,
+                          val_loss=res.val_losses[-1] if res.val_losses else None)
             if cfg.checkpoint and cfg.checkpoint_every and (epoch + 1) % cfg.checkpoint_every == 0:
                 _gather_state(eng, sync)
                 if rank == 0:

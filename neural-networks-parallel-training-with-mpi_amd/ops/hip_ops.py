@@ -194,6 +194,17 @@ class HipOps:
                                X.shape[0], float(inv_count), _p(arena.grad), arena.numel,
                                _p(ws), _p(loss_out), self.stream, sgd)
 
+    # ---------------- data ----------------
+    def gather_rows(self, src, idx, dst):
+        """dst[r] = src[idx[r]] (one launch; rows are copied as raw bytes)."""
+        n = idx.numel()
+        row_bytes = src[0].numel() * src.element_size() if src.shape[0] else 0
+        _check(src.is_contiguous() and dst.is_contiguous() and idx.dtype == torch.int64,
+               "gather_rows needs contiguous src/dst and int64 indices")
+        _check(dst.shape[0] >= n and dst[0].numel() * dst.element_size() == row_bytes,
+               "gather_rows: destination rows do not match the source rows")
+        self.lib.gather_rows(_p(src), _p(dst), _p(idx), n, row_bytes, src.shape[0], self.stream)
+
     # ---------------- optimizer ----------------
     def sgd(self, arena, hp, nesterov: bool, first: bool, zero_grad: bool = True, offset: int = 0,
             numel: int = None):

@@ -77,6 +77,9 @@ class TorchOps:
         if dz_out is not None:
             dz_out.copy_(dl.mm(W.float()) * act_bwd_from_out(af, act_prev))
 
+    def gather_rows(self, src, idx, dst):
+        dst[:idx.numel()].copy_(src.index_select(0, idx))
+
     def sgd(self, arena, hp, nesterov: bool, first: bool, zero_grad: bool = True, offset: int = 0,
             numel: int = None):
         lr, mom, damp, wd, gs = [float(v) for v in hp.tolist()[:5]]

@@ -62,6 +62,7 @@ class TrainConfig:
     scaling: str = "per_shard"        # per_shard (reference, D4) | global | none
     averaging: str = "unweighted"     # unweighted (reference, D5) | weighted
     shuffle: bool = True
+    val_fraction: float = 0.0         # held-out tail of every shard, evaluated after each epoch
     # --- runtime ---
     seed: int = 0                     # init seed (reference: torch.manual_seed(0) on rank 0)
     device: str = "cpu"               # cpu | cuda
@@ -133,6 +134,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--scaling", choices=["per_shard", "global", "none"], default="per_shard")
     p.add_argument("--averaging", choices=["unweighted", "weighted"], default="unweighted")
     p.add_argument("--no_shuffle", dest="shuffle", action="store_false")
+    p.add_argument("--val_fraction", type=float, default=0.0,
+                   help="hold out this fraction of every rank's rows and print the global "
+                        "validation loss after each epoch (the reference's dead x_val/y_val hook)")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--device", choices=["cpu", "cuda"], default="cpu")
     p.add_argument("--comm", choices=["auto", "torch", "native", "none"], default="auto")
@@ -219,3 +223,5 @@ def validate(cfg: TrainConfig) -> None:
         raise ValueError("batch_size must be positive")
     if cfg.n_samples <= 0:
         raise ValueError("n_samples must be positive")
+    if not 0.0 <= cfg.val_fraction < 1.0:
+        raise ValueError("val_fraction must be in [0, 1)")

@@ -22,7 +22,7 @@ def _entry(rank, world, port, cfg, outdir, fn_name):
     import nnmpi_amd  # noqa: F401
     from nnmpi_amd.engine import trainer
     res = getattr(trainer, fn_name)(cfg)
-    torch.save({"losses": res.losses, "global_losses": res.global_losses,
+    torch.save({"losses": res.losses, "global_losses": res.global_losses, "val": res.val_losses,
                 "final": res.final_params, "rows": res.rows, "steps": res.steps},
                os.path.join(outdir, f"r{rank}.pt"))
 

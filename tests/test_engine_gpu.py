@@ -4,6 +4,8 @@ import torch
 
 pytestmark = pytest.mark.gpu
 
+DEV = "cuda"
+
 from test_golden import GOLDEN_LOSSES, GOLDEN_PARAMS  # noqa: E402
 
 import nnmpi_amd  # noqa: E402
@@ -322,3 +324,35 @@ def test_unsplit_wgrad_epilogue_optimizer_is_bitwise_equal():
         eng_mod.MLPEngine.__init__ = orig
     assert a.losses == b.losses
     assert torch.equal(a.final_params, b.final_params)
+
+
+def test_validation_split_gpu_matches_cpu():
+    """Forward-only evaluation on GPU (tiny fp32 kernel, and the bf16 GEMM + head path)."""
+    a = trainer.run_worker(TrainConfig(device="cuda", print_rank="none", val_fraction=0.25))
+    b = trainer.run_worker(TrainConfig(device="cpu", print_rank="none", val_fraction=0.25))
+    assert a.val_losses == pytest.approx(b.val_losses, rel=1e-5)
+    c = trainer.run_worker(_cfg(device="cuda", val_fraction=0.2, nepochs=3))
+    assert len(c.val_losses) == 3 and all(v == v for v in c.val_losses)
+    assert c.losses[-1] < c.losses[0]
+
+
+def test_gather_rows_kernel():
+    from nnmpi_amd.ops.hip_ops import HipOps
+    ops = HipOps()
+    g = torch.Generator(device="cpu").manual_seed(3)
+    idx = torch.randint(0, 100, (77,), generator=g).to(DEV)
+    for src in (torch.randn(100, 37, device=DEV), torch.randn(100, 64, device=DEV).to(torch.bfloat16),
+                torch.arange(100, device=DEV)):
+        dst = torch.zeros((80,) + tuple(src.shape[1:]), dtype=src.dtype, device=DEV)
+        ops.gather_rows(src, idx, dst)
+        assert torch.equal(dst[:77], src[idx])
+
+
+def test_minibatch_training_gpu_matches_cpu():
+    kw = dict(widths=[64, 48, 32, 1], n_features=64, n_samples=512, dtype="fp32", nepochs=2,
+              print_rank="none", batch_size=96)
+    gpu = trainer.run_worker(TrainConfig(device="cuda", **kw))
+    cpu = trainer.run_worker(TrainConfig(device="cpu", **kw))
+    assert gpu.steps == cpu.steps == 2 * 6
+    assert gpu.losses == pytest.approx(cpu.losses, rel=1e-4)
+    assert torch.allclose(gpu.final_params, cpu.final_params, atol=1e-5, rtol=1e-4)

@@ -188,3 +188,32 @@ def test_sharded_optimizer_checkpoint_resume_is_exact(tmp_path):
     run_ranks(TrainConfig(nepochs=3, checkpoint=ck, **cfg), 2)
     res = run_ranks(TrainConfig(nepochs=5, resume=ck, **cfg), 2)
     assert torch.equal(res[0]["final"], full[0]["final"])
+
+
+def _reference_val_loss(res, n_val):
+    """MSE of the final model on the held-out tail, recomputed independently with torch."""
+    import numpy as np
+    from sklearn.preprocessing import StandardScaler
+    from nnmpi_amd.data import synth
+    from nnmpi_amd.models.mlp import MLP
+    X, y = synth.reference_regression()
+    Xs = StandardScaler().fit_transform(X)
+    Xv = torch.from_numpy(np.ascontiguousarray(Xs[-n_val:])).float()
+    yv = torch.from_numpy(np.ascontiguousarray(y[-n_val:])).float().reshape(-1, 1)
+    m = MLP()
+    m.load_state_dict(res.state_dict)
+    with torch.no_grad():
+        return float(((m(Xv) - yv) ** 2).mean())
+
+
+def test_validation_split_loss_matches_independent_eval():
+    res = trainer.run_worker(TrainConfig(print_rank="none", val_fraction=0.25, nepochs=4))
+    assert len(res.val_losses) == 4 and res.rows == 12
+    assert res.val_losses[-1] == pytest.approx(_reference_val_loss(res, 4), rel=1e-5)
+
+
+def test_validation_split_multirank_is_global():
+    out = run_ranks(TrainConfig(print_rank="none", val_fraction=0.25, n_samples=32, nepochs=2), 2)
+    assert [o["rows"] for o in out] == [12, 12]
+    assert out[0]["losses"] != out[1]["losses"]        # local training losses differ
+    assert out[0]["val"] == out[1]["val"] and len(out[0]["val"]) == 2   # one global value
