@@ -362,6 +362,106 @@ __global__ void __launch_bounds__(GEMM_THREADS) gemm_bf16_kernel(GemmParams p) {
 
 
 // ------------------------------------------------------------------------------------------
+// Row-contiguous epilogue for 128x128 tiles (LDS transpose).
+//
+// In fragment order a lane owns 4 consecutive columns of one row per fragment, so every store
+// instruction of a wave writes 16 separate 32-byte row pieces (and the dgrad epilogue READS its
+// saved activation the same way): a store-issue-bound tail of several microseconds per launch
+// (a 1-k-step 8192x512 forward still took 5.5 us).  Here the fp32 accumulators are parked in
+// the idle LDS ring as a swizzled [128][128] image (16-byte chunk c of row r at c ^ (r & 31):
+// conflict-free ds_write_b128 / ds_read_b128), read back 8 columns per lane, and every wave
+// instruction then stores (and loads its epilogue operands for) 4 whole output rows.  The
+// arithmetic is unchanged (same fp32 values, same bias / activation order): results are bitwise
+// identical to the fragment-order epilogue.
+// ------------------------------------------------------------------------------------------
+constexpr int LEPI_ROWS = 4;   // rows per wave-iteration (16 lanes x 8 columns per row)
+
+__device__ __forceinline__ int lepi_off(int r, int c4) { return r * 128 + ((c4 ^ (r & 31)) << 2); }
+
+template <int EPI>
+__device__ __forceinline__ bool lepi_ok(const GemmParams& p) {
+  // whole 16-byte column chunks, 16-byte aligned rows (the fragment epilogue covers the rest)
+  if (p.N % 8) return false;
+  if constexpr (EPI == EPI_F32) return (p.ldc % 4) == 0 && ((uintptr_t)p.C & 15) == 0;
+  else if constexpr (EPI == EPI_DACT)
+    return (p.ldc % 8) == 0 && ((uintptr_t)p.C & 15) == 0 && (p.ldaux % 8) == 0 &&
+           ((uintptr_t)p.aux & 15) == 0;
+  else return (p.ldc % 8) == 0 && ((uintptr_t)p.C & 15) == 0 && ((uintptr_t)p.bias & 15) == 0;
+}
+
+template <int WGM, int WGN, int EPI, int ACT>
+__device__ __forceinline__ void lds_epilogue(const GemmParams& p,
+                                             f32x4 (&acc)[128 / WGM / 16][128 / WGN / 16],
+                                             char* smem, int m0, int n0, int wm, int wn, int w,
+                                             int lane, int split) {
+  constexpr int NW = WGM * WGN, WM = 128 / WGM, WN = 128 / WGN, MI = WM / 16, NJ = WN / 16;
+  constexpr int ITER = 128 / (NW * LEPI_ROWS);
+  float* img = reinterpret_cast<float*>(smem);
+  const int q = lane & 15;                        // this lane's 8-column chunk of a row
+  const int gn = n0 + q * 8;
+  // epilogue operands first (their latency hides under the LDS staging below)
+  f32x4 b0 = {0.f, 0.f, 0.f, 0.f}, b1 = {0.f, 0.f, 0.f, 0.f};
+  bf16x8 aux[EPI == EPI_DACT ? ITER : 1];
+  if constexpr (EPI == EPI_BIAS_ACT) {
+    if (p.bias && gn < p.N) {
+      b0 = *reinterpret_cast<const f32x4*>(p.bias + gn);
+      b1 = *reinterpret_cast<const f32x4*>(p.bias + gn + 4);
+    }
+  } else if constexpr (EPI == EPI_DACT) {
+#pragma unroll
+    for (int it = 0; it < ITER; ++it) {
+      const int gm = min(m0 + (it * NW + w) * LEPI_ROWS + (lane >> 4), p.M - 1);
+      aux[it] = *reinterpret_cast<const bf16x8*>(p.aux + (long long)gm * p.ldaux + min(gn, p.N - 8));
+    }
+  }
+  // every wave is past its last read of the ring (and, with the final vmcnt(0), every DMA landed)
+  __builtin_amdgcn_s_barrier();
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int r = wm * WM + i * 16 + (lane & 15);
+      const int c4 = (wn * WN + j * 16) / 4 + (lane >> 4);
+      *reinterpret_cast<f32x4*>(img + lepi_off(r, c4)) = acc[i][j];
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  const bool fuse = (EPI == EPI_F32) && p.sg.g_base != nullptr;
+  float* cbase = reinterpret_cast<float*>(p.C) + (EPI == EPI_F32 ? split * p.c_split_stride : 0);
+#pragma unroll
+  for (int it = 0; it < ITER; ++it) {
+    const int r = (it * NW + w) * LEPI_ROWS + (lane >> 4);
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(img + lepi_off(r, 2 * q));
+    const f32x4 v1 = *reinterpret_cast<const f32x4*>(img + lepi_off(r, 2 * q + 1));
+    const int gm = m0 + r;
+    if (gm >= p.M || gn >= p.N) continue;
+    if constexpr (EPI == EPI_F32) {
+      float* g = cbase + (long long)gm * p.ldc + gn;
+      if (fuse) {
+        sgd_fused_store4(p.sg, g, v0);
+        sgd_fused_store4(p.sg, g + 4, v1);
+      } else {
+        *reinterpret_cast<f32x4*>(g) = v0;
+        *reinterpret_cast<f32x4*>(g + 4) = v1;
+      }
+    } else {
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        if constexpr (EPI == EPI_BIAS_ACT) {
+          o[e] = (bf16)act_fwd_t<ACT>(v0[e] + b0[e]);
+          o[e + 4] = (bf16)act_fwd_t<ACT>(v1[e] + b1[e]);
+        } else {
+          o[e] = (bf16)(v0[e] * act_bwd_t<ACT>((float)aux[it][e]));
+          o[e + 4] = (bf16)(v1[e] * act_bwd_t<ACT>((float)aux[it][e + 4]));
+        }
+      }
+      *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(p.C) + (long long)gm * p.ldc + gn) = o;
+    }
+  }
+}
+
+// ------------------------------------------------------------------------------------------
 // v2 main loop: LDS-DMA (buffer_load ... lds) into an NS-deep ring, counted vmcnt, raw barrier.
 //
 // The MLP GEMMs are short-K (K = 512..8192 per block) and, at one 256-thread block per CU, a
@@ -583,6 +683,25 @@ __device__ __forceinline__ void dma_gemm_tile(const GemmParams& p, char* smem, i
     }
     // all of this wave's LDS reads of stage t are consumed before the next barrier
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  if constexpr (BM == 128 && BN == 128 && NS * STAGE >= 128 * 128 * 4) {
+    if (lepi_ok<EPI>(p)) {
+      lds_epilogue<WGM, WGN, EPI, ACT>(p, acc, smem, m0, n0, wm, wn, w, lane, split);
+      if constexpr (BIASGRAD) {
+        // bias gradient: lane l < 16 holds the row sum of row wm*WM + i*16 + l
+        if (do_bg && (lane >> 4) == 0) {
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            const int m = m0 + wm * WM + i * 16 + (lane & 15);
+            if (m >= p.M) continue;
+            float* g = p.bias_grad + split * p.bg_split_stride + m;
+            if (p.sg.g_base) sgd_fused_store(p.sg, g, accb[i][0]);
+            else *g = accb[i][0];
+          }
+        }
+      }
+      return;
+    }
   }
   gemm_epilogue<BM, BN, WGM, WGN, EPI, ACT, BIASGRAD>(p, acc, accb, do_bg, m0, n0, wm, wn, lane, split,
                                                       EPI == EPI_BIAS_ACT ? bias_pre : nullptr);
