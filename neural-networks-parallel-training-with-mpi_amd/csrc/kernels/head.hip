@@ -333,10 +333,193 @@ static hipError_t head_launch_c(const HeadArgs& a, int act, int blocks, size_t s
   // fused (out == 1) heads keep several rows in flight per wave; wide heads one row (registers)
   constexpr int D = (FUSE || OM == 1) ? 1 : 16;
   if (nch <= 64) return head_launch_act<TA, 1, LOSS, FUSE, (2 / D > 0 ? 2 / D : 1), OM, 16>(a, act, blocks, smem, wslab, bslab, s);
-  if (nch <= 128) return head_launch_act<TA, 2, LOSS, FUSE, (2 / D > 0 ? 2 / D : 1), OM, 8>(a, act, blocks, smem, wslab, bslab, s);
+  // multi-output heads of <= 1024 features: 4 rows per wave-iteration too (their loads and
+  // 4 x out butterflies in flight together; one row at a time left the waves 53 % in s_waitcnt)
+  if (nch <= 128) return head_launch_act<TA, 2, LOSS, FUSE, (FUSE || OM == 1) ? 2 : 4, OM, 8>(a, act, blocks, smem, wslab, bslab, s);
   if (nch <= 256) return head_launch_act<TA, 4, LOSS, FUSE, (4 / D > 0 ? 4 / D : 1), OM, 4>(a, act, blocks, smem, wslab, bslab, s);
   if (nch <= 1024) return head_launch_act<TA, 16, LOSS, FUSE, 1, OM, 4>(a, act, blocks, smem, wslab, bslab, s);
   return hipErrorInvalidValue;
+}
+
+// ------------------------------------------------------------------------------------------
+// Multi-output head (cross-entropy / multi-target MSE, out <= 16) on the matrix cores.
+//
+// One block = 4 waves = one 16-row group at a time.  The logits are a 16 (outputs, padded) x 16
+// (rows) x in GEMM on v_mfma_f32_16x16x4_f32 (exact fp32 products and sums, like the VALU head
+// it replaces): wave w covers the w-th quarter of the features, the 4 partial tiles are summed
+// through LDS in wave order, and every wave then holds the 16 rows' logits (lane l: row l&15,
+// outputs 4(l>>4)..+3), so softmax / MSE need only two cross-lane steps.  dZ_prev = (dl . W) *
+// act'(a) is a second MFMA product (16 features x 16 rows, K = 16 outputs) per 16-feature tile
+// of the wave's quarter; dl enters as the B operand after 16 shuffles.  W sits in LDS as fp32
+// [16][in] with 16-byte chunk c of row n at c ^ (n & 15) (conflict-free for both reads).  The
+// VALU head needed ~1500 VALU instructions per row (44 us for 8192 x 1024 x 10).
+// ------------------------------------------------------------------------------------------
+constexpr int MH_WAVES = 4;
+
+__device__ __forceinline__ int mh_off(int n, int k, int in) { return n * in + (((k >> 2) ^ (n & 15)) << 2) + (k & 3); }
+
+template <int ACT, int LOSS, int Q>
+__global__ void __launch_bounds__(64 * MH_WAVES) head_mfma_kernel(HeadArgs p) {
+  extern __shared__ __attribute__((aligned(16))) float ml[];   // W image [16][in] + partials
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int in = p.in, out = p.out;   // in == 4 * Q
+  for (int i = tid; i < 16 * in; i += 64 * MH_WAVES) {
+    const int n = i / in, k = i - n * in;
+    ml[mh_off(n, k, in)] = n < out ? p.W[n * in + k] : 0.f;
+  }
+  f32x4* part = reinterpret_cast<f32x4*>(ml + 16 * in);          // [4 waves][64 lanes]
+  __syncthreads();
+  const bf16* A = reinterpret_cast<const bf16*>(p.a);
+  bf16* DZ = reinterpret_cast<bf16*>(p.dz_prev);
+  const int r = lane & 15, g = lane >> 4;
+  float bias[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) bias[j] = (4 * g + j) < out ? p.b[4 * g + j] : 0.f;
+  float block_loss = 0.f;
+  const int ngroups = (p.rows + 15) / 16;
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const int row = grp * 16 + r;
+    const bool valid = row < p.rows;
+    const int rowc = valid ? row : p.rows - 1;
+    // every global load of the group first (row chunks for the logits, the saved activation
+    // for dZ): one exposed round trip per group instead of one per loop iteration
+    bf16x8 xs[Q / 32];
+    bf16x4 avs[Q / 16];
+#pragma unroll
+    for (int c = 0; c < Q / 32; ++c)
+      xs[c] = *reinterpret_cast<const bf16x8*>(A + (long long)rowc * in + w * Q + c * 32 + g * 8);
+    if (DZ != nullptr) {
+#pragma unroll
+      for (int t = 0; t < Q / 16; ++t)
+        avs[t] = *reinterpret_cast<const bf16x4*>(A + (long long)rowc * in + w * Q + t * 16 + 4 * g);
+    }
+    // ---- logits: this wave's quarter of the features ----
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int c = 0; c < Q / 32; ++c) {
+      const int k = w * Q + c * 32 + g * 8;
+      const bf16x8 xv = xs[c];
+      const f32x4 w0 = *reinterpret_cast<const f32x4*>(ml + mh_off(r, k, in));
+      const f32x4 w1 = *reinterpret_cast<const f32x4*>(ml + mh_off(r, k + 4, in));
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w0[e], (float)xv[e], acc, 0, 0, 0);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) acc = __builtin_amdgcn_mfma_f32_16x16x4f32(w1[e], (float)xv[e + 4], acc, 0, 0, 0);
+    }
+    part[w * 64 + lane] = acc;
+    __syncthreads();
+    f32x4 z = part[lane];
+#pragma unroll
+    for (int ww = 1; ww < MH_WAVES; ++ww) z += part[ww * 64 + lane];
+    // ---- loss and dlogits (lane: row r, outputs 4g..4g+3) ----
+    float dl[4];
+    float row_loss = 0.f;
+    if constexpr (LOSS == LOSS_XENT) {
+      float mx = -INFINITY;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        z[j] += bias[j];
+        if (4 * g + j < out) mx = fmaxf(mx, z[j]);
+      }
+      mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+      mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+      float se = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) if (4 * g + j < out) se += __expf(z[j] - mx);
+      se += __shfl_xor(se, 16, 64);
+      se += __shfl_xor(se, 32, 64);
+      const float lse = mx + __logf(se);
+      const int lab = (int)p.labels[rowc];
+      float picked = 0.f;
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = 4 * g + j;
+        if (n == lab) picked = z[j];
+        dl[j] = (n < out && valid) ? (__expf(z[j] - lse) - (n == lab ? 1.f : 0.f)) * p.inv_count : 0.f;
+      }
+      picked += __shfl_xor(picked, 16, 64);
+      picked += __shfl_xor(picked, 32, 64);
+      row_loss = lse - picked;
+    } else {
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int n = 4 * g + j;
+        z[j] += bias[j];
+        const float d = n < out ? z[j] - p.y[(long long)rowc * out + n] : 0.f;
+        row_loss += d * d;
+        dl[j] = valid ? 2.f * d * p.inv_count : 0.f;
+      }
+      row_loss += __shfl_xor(row_loss, 16, 64);
+      row_loss += __shfl_xor(row_loss, 32, 64);
+    }
+    if (w == 0) {
+      if (valid && g == 0) block_loss += row_loss;
+      if (p.dlogits && valid) {
+#pragma unroll
+        for (int j = 0; j < 4; ++j)
+          if (4 * g + j < out) p.dlogits[(long long)row * out + 4 * g + j] = dl[j];
+      }
+    }
+    // ---- dZ_prev for this wave's quarter: 16-feature tiles, K = 16 outputs ----
+    if (DZ != nullptr) {
+      float bfr[4];   // B operand of step s: dl[row r][n = 4s + g], held by lane (s, r) reg g
+#pragma unroll
+      for (int st = 0; st < 4; ++st) {
+        const int src = st * 16 + r;
+        const float t0 = __shfl(dl[0], src, 64), t1 = __shfl(dl[1], src, 64);
+        const float t2 = __shfl(dl[2], src, 64), t3 = __shfl(dl[3], src, 64);
+        bfr[st] = g == 0 ? t0 : g == 1 ? t1 : g == 2 ? t2 : t3;
+      }
+#pragma unroll
+      for (int t = 0; t < Q / 16; ++t) {
+        const int k0 = w * Q + t * 16;
+        const bf16x4 av = avs[t];
+        f32x4 d = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+        for (int st = 0; st < 4; ++st)
+          d = __builtin_amdgcn_mfma_f32_16x16x4f32(ml[mh_off(4 * st + g, k0 + r, in)], bfr[st], d, 0, 0, 0);
+        if (valid) {
+          bf16x4 o;
+#pragma unroll
+          for (int j = 0; j < 4; ++j) o[j] = (bf16)(d[j] * act_bwd_t<ACT>((float)av[j]));
+          *reinterpret_cast<bf16x4*>(DZ + (long long)row * in + k0 + 4 * g) = o;
+        }
+      }
+    }
+    __syncthreads();   // the partial buffer is rewritten by the next group
+  }
+  if (w == 0) {
+    const float t = wave_sum(block_loss);
+    if (lane == 0) p.loss_part[blockIdx.x] = t;
+  }
+}
+
+// feature counts with a compiled quarter (the loads of a group are unrolled into registers)
+bool head_mfma_ok(int a_bf16, int in, int out, bool fuse) {
+  return !fuse && a_bf16 && out > 1 && out <= 16 && (in == 512 || in == 1024);
+}
+
+template <int Q>
+static hipError_t head_mfma_launch_q(const HeadArgs& h, int act, int loss, int blocks, hipStream_t s) {
+  const size_t smem = (size_t)(16 * h.in + MH_WAVES * 64 * 4) * sizeof(float);
+  using Fn = void (*)(HeadArgs);
+  static const Fn fns[2][3] = {
+      {head_mfma_kernel<ACT_NONE, LOSS_MSE, Q>, head_mfma_kernel<ACT_RELU, LOSS_MSE, Q>, head_mfma_kernel<ACT_TANH, LOSS_MSE, Q>},
+      {head_mfma_kernel<ACT_NONE, LOSS_XENT, Q>, head_mfma_kernel<ACT_RELU, LOSS_XENT, Q>, head_mfma_kernel<ACT_TANH, LOSS_XENT, Q>}};
+  static bool attr[2][3] = {};
+  const int li = loss == LOSS_XENT ? 1 : 0, ai = act == ACT_RELU ? 1 : act == ACT_TANH ? 2 : 0;
+  if (!attr[li][ai]) {
+    (void)hipFuncSetAttribute((const void*)fns[li][ai], hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
+    attr[li][ai] = true;
+  }
+  hipLaunchKernelGGL(fns[li][ai], dim3(blocks), dim3(64 * MH_WAVES), smem, s, h);
+  return hipGetLastError();
+}
+
+static hipError_t head_mfma_launch(const HeadArgs& h, int act, int loss, int blocks, hipStream_t s) {
+  return h.in == 512 ? head_mfma_launch_q<128>(h, act, loss, blocks, s)
+                     : head_mfma_launch_q<256>(h, act, loss, blocks, s);
 }
 
 static hipError_t head_fwd_impl(const void* a, int a_bf16, int rows, int in, const float* W,
@@ -349,6 +532,7 @@ static hipError_t head_fwd_impl(const void* a, int a_bf16, int rows, int in, con
   if (smem > 65536 + 32768) return hipErrorInvalidValue;
   HeadArgs h{a, rows, in, W, b, out, y, labels, inv_count, act_prev, dz_prev, dlogits, loss_part};
   const int blocks = head_fwd_parts(rows, in);
+  if (head_mfma_ok(a_bf16, in, out, fuse)) return head_mfma_launch(h, act_prev, loss, blocks, s);
 #define HL(TA, LS, FU, OM) head_launch_c<TA, LS, FU, OM>(h, act_prev, blocks, smem, wslab, bslab, s)
   if (fuse) {
     if (loss == LOSS_XENT || out != 1) return hipErrorInvalidValue;
