@@ -363,10 +363,20 @@ __global__ void __launch_bounds__(64 * MH_WAVES) head_mfma_kernel(HeadArgs p) {
   extern __shared__ __attribute__((aligned(16))) float ml[];   // W image [16][in] + partials
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int in = p.in, out = p.out;   // in == 4 * Q
-  for (int i = tid; i < 16 * in; i += 64 * MH_WAVES) {
-    const int n = i / in, k = i - n * in;
-    ml[mh_off(n, k, in)] = n < out ? p.W[n * in + k] : 0.f;
+  constexpr int in = 4 * Q;
+  const int out = p.out;
+  // W image: 16-byte loads, all issued before the first LDS store (compile-time trip count)
+  constexpr int NV = 16 * in / 4 / (64 * MH_WAVES);
+  f32x4 wv[NV];
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int i4 = j * 64 * MH_WAVES + tid, n = i4 / (in / 4), k = (i4 % (in / 4)) * 4;
+    wv[j] = n < out ? *reinterpret_cast<const f32x4*>(p.W + n * in + k) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+#pragma unroll
+  for (int j = 0; j < NV; ++j) {
+    const int i4 = j * 64 * MH_WAVES + tid, n = i4 / (in / 4), k = (i4 % (in / 4)) * 4;
+    *reinterpret_cast<f32x4*>(ml + mh_off(n, k, in)) = wv[j];
   }
   f32x4* part = reinterpret_cast<f32x4*>(ml + 16 * in);          // [4 waves][64 lanes]
   __syncthreads();

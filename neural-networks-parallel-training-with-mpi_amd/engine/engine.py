@@ -174,6 +174,9 @@ class MLPEngine:
         n = idx.numel()
         if n > self.R:
             raise ValueError(f"batch of {n} rows exceeds capacity {self.R}")
+        if n == 0:   # empty micro-batch of a short shard: zero gradient, still steps
+            self.rows = 0
+            return
         ctx = torch.cuda.stream(self.stream) if self.is_cuda else _nullctx()
         with ctx, torch.no_grad():
             self.ops.gather_rows(X, idx, self.X)
@@ -509,6 +512,58 @@ class MLPEngine:
         g.end()
         return g
 
+    # ---------------- gradient accumulation ----------------------------------------------------
+    # Not in the reference (one backward per step, SURVEY.md §2.3 "optional").  A step over more
+    # rows than fit the activation buffers is cut into micro-batches: each runs the sequential
+    # forward/backward kernels with communication and the optimizer switched off and its
+    # gradient is added into an fp32 accumulation arena; the step's gradient synchronisation
+    # and update then run ONCE on the sum.  set_scales() must carry the row count of the whole
+    # step (inv_count = 1/rows_step), so the sum is the step's mean gradient and the summed
+    # micro-batch losses are the step's mean loss.
+    def accumulate(self):
+        """Forward + backward of the loaded micro-batch; gradient and loss are added to the
+        accumulators (asynchronous on the GPU)."""
+        ar = self.arena
+        if not hasattr(self, "_acc"):
+            self._acc = torch.zeros_like(ar.grad)
+            self._acc_loss = torch.zeros(1, dtype=torch.float32, device=self.device)
+            self._n_acc = 0
+        ctx = torch.cuda.stream(self.stream) if self.is_cuda else _nullctx()
+        with ctx, torch.no_grad():
+            sync, tiny_fused = self.sync, self.tiny_fused
+            self.sync, self.tiny_fused = _SilentSync(), False
+            try:
+                self.forward_backward()
+            finally:
+                self.sync, self.tiny_fused = sync, tiny_fused
+            if self._n_acc == 0:
+                self._acc.copy_(ar.grad)
+                self._acc_loss.copy_(self.loss_out[:1])
+            else:
+                self._acc.add_(ar.grad)
+                self._acc_loss.add_(self.loss_out[:1])
+        self._n_acc += 1
+
+    def apply_accumulated(self):
+        """Gradient synchronisation + optimizer update on the accumulated gradient: one optimizer
+        step (steps_done += 1).  The accumulators restart empty."""
+        if not getattr(self, "_n_acc", 0):
+            raise RuntimeError("apply_accumulated() without a preceding accumulate()")
+        first = self.steps_done == 0
+        ar = self.arena
+        ctx = torch.cuda.stream(self.stream) if self.is_cuda else _nullctx()
+        with ctx, torch.no_grad():
+            ar.grad.copy_(self._acc)
+            self.loss_out[:1].copy_(self._acc_loss)
+            self._first = first
+            self.sync.begin()
+            for i in reversed(range(self.L)):
+                self.sync.ready(i)
+            self.sync.finish()
+            self._update(first)
+        self._n_acc = 0
+        self.steps_done += 1
+
     # ---------------- evaluation (forward only) ---------------------------------------------
     def evaluate(self, X: torch.Tensor, Y: Optional[torch.Tensor] = None,
                  labels: Optional[torch.Tensor] = None):
@@ -568,6 +623,13 @@ class MLPEngine:
     @property
     def flops_per_step(self) -> float:
         return float(self.spec.flops_per_sample()) * self.rows
+
+
+class _SilentSync:
+    """Stand-in for the gradient sync while a micro-batch's gradient is produced."""
+
+    def ready(self, layer: int):
+        pass
 
 
 class _nullctx:

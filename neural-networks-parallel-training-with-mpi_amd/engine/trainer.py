@@ -323,7 +323,11 @@ def _run(j: Job) -> TrainResult:
     ops = make_ops(j)
     bs = cfg.batch_size
     max_rows = max(train_counts)
-    cap = min(bs, max_rows) if bs else max_rows
+    K = max(1, int(cfg.grad_accum))
+    # micro-batch size (every rank uses the same one, so every rank runs the same number of
+    # micro-batches and optimizer steps; a short shard gets empty micro-batches)
+    mb = bs if bs else (max(1, math.ceil(max_rows / K)) if K > 1 else None)
+    cap = min(mb, max_rows) if mb else max_rows
     eng = MLPEngine(spec, arena, ops, sync, device=j.device, dtype=dtype,
                     rows_capacity=max(cap, 1), lr=cfg.lr, momentum=cfg.momentum,
                     dampening=cfg.dampening, weight_decay=cfg.weight_decay,
@@ -337,7 +341,11 @@ def _run(j: Job) -> TrainResult:
     seqchk = SequenceChecker(j.pg) if cfg.seqcheck else None
     wd = Watchdog(cfg.timeout_s, j.native_comm) if world > 1 else None
     res = TrainResult(rank, world, rows=rows_local)
-    steps_per_epoch = 1 if not bs else max(1, math.ceil(max_rows / bs))
+    n_micro = max(1, math.ceil(max_rows / mb)) if mb else 1
+    steps_per_epoch = math.ceil(n_micro / K) if K > 1 else (1 if not bs else n_micro)
+
+    def micro_rows(c: int, m: int) -> int:
+        return max(0, min(mb, c - m * mb))
     gen = torch.Generator(device="cpu")
     full_loaded = False
     try:
@@ -350,6 +358,22 @@ def _run(j: Job) -> TrainResult:
             else:
                 perm = None
             for s in range(steps_per_epoch):
+                if K > 1:
+                    micros = range(s * K, min((s + 1) * K, n_micro))
+                    rows_all = [sum(micro_rows(c, m) for m in micros) for c in train_counts]
+                    inv, lsc, gsc = loss_scales(cfg, rows_all[rank], rows_all, cfg.widths[-1])
+                    eng.set_scales(inv, lsc, gsc)
+                    for m in micros:
+                        lo, hi = m * mb, m * mb + micro_rows(rows_local, m)
+                        idx = (perm[lo:hi] if perm is not None
+                               else torch.arange(lo, hi, device=j.device))
+                        eng.load_batch_indexed(Xc, Y, labels, idx.contiguous())
+                        eng.accumulate()
+                    eng.apply_accumulated()
+                    step_rows = rows_all[rank]
+                    if wd:
+                        wd.kick()
+                    continue
                 if not bs:
                     if not full_loaded:  # full-shard batch: order-irrelevant, uploaded once (D10)
                         eng.load_batch(Xc, Y, labels)
@@ -363,6 +387,7 @@ def _run(j: Job) -> TrainResult:
                 inv, lsc, gsc = loss_scales(cfg, eng.rows, rows_all, cfg.widths[-1])
                 eng.set_scales(inv, lsc, gsc)
                 eng.step()
+                step_rows = eng.rows
                 if wd:
                     wd.kick()
             loss = eng.loss()
@@ -371,7 +396,7 @@ def _run(j: Job) -> TrainResult:
             res.epoch_times.append(dt)
             _print(cfg, rank, f"loss in worker {rank}: {loss}")
             if cfg.global_loss and world > 1:
-                t = torch.tensor([loss * eng.rows, float(eng.rows)], dtype=torch.float64)
+                t = torch.tensor([loss * step_rows, float(step_rows)], dtype=torch.float64)
                 j.pg.allreduce_cpu(t)
                 gl = float(t[0] / max(t[1], 1.0))
                 res.global_losses.append(gl)

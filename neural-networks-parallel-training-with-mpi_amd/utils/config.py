@@ -63,6 +63,7 @@ class TrainConfig:
     averaging: str = "unweighted"     # unweighted (reference, D5) | weighted
     shuffle: bool = True
     val_fraction: float = 0.0         # held-out tail of every shard, evaluated after each epoch
+    grad_accum: int = 1               # micro-batches per optimizer step (gradient accumulation)
     # --- runtime ---
     seed: int = 0                     # init seed (reference: torch.manual_seed(0) on rank 0)
     device: str = "cpu"               # cpu | cuda
@@ -137,6 +138,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--val_fraction", type=float, default=0.0,
                    help="hold out this fraction of every rank's rows and print the global "
                         "validation loss after each epoch (the reference's dead x_val/y_val hook)")
+    p.add_argument("--grad_accum", "--accum_steps", dest="grad_accum", type=int, default=1,
+                   help="micro-batches whose gradients are summed before one synchronisation + "
+                        "optimizer step (with the whole-shard batch the shard is cut into this "
+                        "many micro-batches)")
     p.add_argument("--seed", type=int, default=0)
     p.add_argument("--device", choices=["cpu", "cuda"], default="cpu")
     p.add_argument("--comm", choices=["auto", "torch", "native", "none"], default="auto")
@@ -225,3 +230,5 @@ def validate(cfg: TrainConfig) -> None:
         raise ValueError("n_samples must be positive")
     if not 0.0 <= cfg.val_fraction < 1.0:
         raise ValueError("val_fraction must be in [0, 1)")
+    if int(cfg.grad_accum) < 1:
+        raise ValueError("grad_accum must be >= 1")

@@ -356,3 +356,23 @@ def test_minibatch_training_gpu_matches_cpu():
     assert gpu.steps == cpu.steps == 2 * 6
     assert gpu.losses == pytest.approx(cpu.losses, rel=1e-4)
     assert torch.allclose(gpu.final_params, cpu.final_params, atol=1e-5, rtol=1e-4)
+
+
+def test_grad_accum_gpu_matches_cpu_and_single_batch():
+    """Accumulated micro-batches on the GPU (fp32 GEMMs, then the tiny kernel with its in-kernel
+    SGD switched off) == the CPU oracle, and == one batch of the same rows."""
+    kw = dict(widths=[64, 48, 32, 1], n_features=64, n_samples=512, dtype="fp32", nepochs=2,
+              print_rank="none", batch_size=64, grad_accum=3)
+    gpu = trainer.run_worker(TrainConfig(device="cuda", **kw))
+    cpu = trainer.run_worker(TrainConfig(device="cpu", **kw))
+    assert gpu.steps == cpu.steps == 2 * 3
+    assert gpu.losses == pytest.approx(cpu.losses, rel=1e-4)
+    assert torch.allclose(gpu.final_params, cpu.final_params, atol=1e-5, rtol=1e-4)
+    one = trainer.run_worker(TrainConfig(device="cuda", **dict(kw, batch_size=192, grad_accum=1)))
+    assert torch.allclose(gpu.final_params, one.final_params, atol=1e-5, rtol=1e-4)
+    t = dict(print_rank="none", nepochs=4)
+    a = trainer.run_worker(TrainConfig(device="cuda", grad_accum=2, **t))
+    b = trainer.run_worker(TrainConfig(device="cpu", grad_accum=2, **t))
+    assert a.losses == pytest.approx(b.losses, rel=1e-5)
+    c = trainer.run_worker(_cfg(device="cuda", nepochs=3, grad_accum=2))
+    assert c.losses[-1] < c.losses[0]

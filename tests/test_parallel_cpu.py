@@ -217,3 +217,33 @@ def test_validation_split_multirank_is_global():
     assert [o["rows"] for o in out] == [12, 12]
     assert out[0]["losses"] != out[1]["losses"]        # local training losses differ
     assert out[0]["val"] == out[1]["val"] and len(out[0]["val"]) == 2   # one global value
+
+
+def test_grad_accum_full_shard_equals_one_batch():
+    """Cutting the whole-shard batch into 4 accumulated micro-batches gives the same steps
+    (up to fp32 summation order) and the same per-epoch mean losses."""
+    cfg = dict(print_rank="none", nepochs=5, n_samples=64, lr=0.01)
+    a = trainer.run_worker(TrainConfig(**cfg))
+    b = trainer.run_worker(TrainConfig(grad_accum=4, **cfg))
+    assert a.steps == b.steps == 5
+    torch.testing.assert_close(b.final_params, a.final_params, rtol=1e-5, atol=1e-6)
+    assert b.losses == pytest.approx(a.losses, rel=1e-5)
+
+
+def test_grad_accum_minibatches_multirank():
+    """batch 4 x 2 accumulated micro-batches == batch 8 (same shuffled rows per step), on an
+    uneven 3-rank split (9/8/8 rows) whose short shards run an empty last micro-batch."""
+    cfg = dict(print_rank="none", nepochs=3, n_samples=25, lr=0.01)
+    a = run_ranks(TrainConfig(batch_size=8, **cfg), 3)
+    b = run_ranks(TrainConfig(batch_size=4, grad_accum=2, **cfg), 3)
+    for x, y in zip(a, b):
+        assert x["steps"] == y["steps"] == 3 * 2
+        torch.testing.assert_close(y["final"], x["final"], rtol=1e-5, atol=1e-6)
+    assert torch.equal(b[0]["final"], b[2]["final"])
+
+
+def test_grad_accum_flag():
+    from nnmpi_amd.utils.config import build_parser, config_from_args
+    assert config_from_args(build_parser().parse_args(["--accum_steps", "3"])).grad_accum == 3
+    with pytest.raises(ValueError):
+        config_from_args(build_parser().parse_args(["--grad_accum", "0"]))
