@@ -194,10 +194,27 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
   m.def("wgrad_will_split", [](int M, int N, int K) { return wgrad_splits(M, N, K) > 1; });
   m.def("head_wgrad_workspace_bytes", &head_wgrad_workspace_bytes);
   m.def("head_wgrad", [](uptr a, int a_bf16, int rows, int in, uptr dl, int out, uptr gW, uptr gb,
-                         uptr ws, uptr lp, int nlp, float lscale, uptr lout, uptr s) {
+                         uptr ws, uptr lp, int nlp, float lscale, uptr lout, uptr s, py::object sgd) {
+    SgdFuse f{};
+    const bool fu = to_sgd(sgd, f);
     check(head_wgrad(P<const void>(a), a_bf16, rows, in, P<const float>(dl), out, P<float>(gW),
-                     P<float>(gb), P<float>(ws), P<const float>(lp), nlp, lscale, P<float>(lout), S(s)),
+                     P<float>(gb), P<float>(ws), P<const float>(lp), nlp, lscale, P<float>(lout), S(s),
+                     fu ? &f : nullptr),
           "head_wgrad");
+  }, py::arg("a"), py::arg("a_bf16"), py::arg("rows"), py::arg("in"), py::arg("dl"), py::arg("out"),
+     py::arg("gW"), py::arg("gb"), py::arg("ws"), py::arg("lp"), py::arg("nlp"), py::arg("lscale"),
+     py::arg("lout"), py::arg("s"), py::arg("sgd") = py::none());
+  m.def("head_wgrad_deferred", [](uptr a, int a_bf16, int rows, int in, uptr dl, int out, uptr gW,
+                                  uptr gb, uptr ws, uptr lp, int nlp, float lscale, uptr lout, uptr s,
+                                  py::object sgd) {
+    SgdFuse f{};
+    const bool fu = to_sgd(sgd, f);
+    SlabReduce r{};
+    check(head_wgrad(P<const void>(a), a_bf16, rows, in, P<const float>(dl), out, P<float>(gW),
+                     P<float>(gb), P<float>(ws), P<const float>(lp), nlp, lscale, P<float>(lout), S(s),
+                     fu ? &f : nullptr, &r),
+          "head_wgrad_deferred");
+    return r;
   });
 
   // ---- tiny fused MLP ----
@@ -205,7 +222,7 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
   m.def("tiny_mlp_step", [](std::vector<int> widths, std::vector<int> w_off, std::vector<int> b_off,
                             int act, int loss, uptr params, uptr X, uptr y, uptr labels, int rows,
                             float inv_count, uptr grad, int numel, uptr ws, uptr lout, uptr s,
-                            py::object sgd) {
+                            py::object sgd, float loss_scale) {
     TinyMLPDesc d{};
     d.n_layers = (int)widths.size() - 1;
     if (d.n_layers < 1 || d.n_layers > 4 || (int)w_off.size() != d.n_layers || (int)b_off.size() != d.n_layers)
@@ -218,11 +235,11 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
     const bool fu = to_sgd(sgd, f);
     check(tiny_mlp_step(d, P<const float>(params), P<const float>(X), P<const float>(y),
                         P<const int64_t>(labels), rows, inv_count, P<float>(grad), numel, P<float>(ws),
-                        P<float>(lout), S(s), fu ? &f : nullptr), "tiny_mlp_step");
+                        P<float>(lout), S(s), fu ? &f : nullptr, loss_scale), "tiny_mlp_step");
   }, py::arg("widths"), py::arg("w_off"), py::arg("b_off"), py::arg("act"), py::arg("loss"),
      py::arg("params"), py::arg("X"), py::arg("y"), py::arg("labels"), py::arg("rows"),
      py::arg("inv_count"), py::arg("grad"), py::arg("numel"), py::arg("ws"), py::arg("lout"),
-     py::arg("s"), py::arg("sgd") = py::none());
+     py::arg("s"), py::arg("sgd") = py::none(), py::arg("loss_scale") = -1.f);
   m.def("tiny_mlp_can_fuse_sgd", &tiny_mlp_can_fuse_sgd);
 
   // ---- optimizer / elementwise ----

@@ -120,9 +120,12 @@ hipError_t head_fused(const void* a, int a_bf16, int rows, int in, const float* 
                       float* gb, float* ws, float* loss_part, float loss_scale, float* loss_out,
                       hipStream_t s, const SgdFuse* sgd = nullptr, SlabReduce* pending = nullptr);
 size_t head_wgrad_workspace_bytes(int rows, int in, int out);
+// sgd: apply the optimizer update in the combine; pending: return the combine unlaunched (see
+// bwd_group) instead of running it
 hipError_t head_wgrad(const void* a, int a_bf16, int rows, int in, const float* dlogits, int out,
                       float* gW, float* gb, float* ws, const float* loss_part, int n_loss_part,
-                      float loss_scale, float* loss_out, hipStream_t s);
+                      float loss_scale, float* loss_out, hipStream_t s, const SgdFuse* sgd = nullptr,
+                      SlabReduce* pending = nullptr);
 
 // ---- whole tiny MLP in one launch (tiny_mlp.hip), fp32, widths <= 16, layers <= 4 ----
 struct TinyMLPDesc {
@@ -135,11 +138,12 @@ struct TinyMLPDesc {
 };
 size_t tiny_mlp_workspace_bytes(int rows, int arena_numel);
 // sgd != nullptr (single block, i.e. rows <= 256, single rank): the kernel applies the optimizer
-// update itself instead of storing the gradient (the whole step is ONE launch).
+// update itself instead of storing the gradient (the whole step is ONE launch).  loss_scale < 0:
+// the reported loss is the mean over these rows (else sum * loss_scale, e.g. micro-batches).
 hipError_t tiny_mlp_step(const TinyMLPDesc& d, const float* params, const float* X,
                          const float* y, const int64_t* labels, int rows, float inv_count,
                          float* grad, int arena_numel, float* ws, float* loss_out, hipStream_t s,
-                         const SgdFuse* sgd = nullptr);
+                         const SgdFuse* sgd = nullptr, float loss_scale = -1.f);
 bool tiny_mlp_can_fuse_sgd(int rows);
 
 // ---- optimizer / elementwise (optim.hip) ----

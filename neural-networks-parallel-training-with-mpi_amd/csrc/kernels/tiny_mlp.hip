@@ -169,7 +169,7 @@ size_t tiny_mlp_workspace_bytes(int rows, int arena_numel) {
 hipError_t tiny_mlp_step(const TinyMLPDesc& d, const float* params, const float* X,
                          const float* y, const int64_t* labels, int rows, float inv_count,
                          float* grad, int arena_numel, float* ws, float* loss_out, hipStream_t s,
-                         const SgdFuse* sgd) {
+                         const SgdFuse* sgd, float loss_scale_in) {
   if (d.n_layers < 1 || d.n_layers > TL) return hipErrorInvalidValue;
   for (int l = 0; l <= d.n_layers; ++l)
     if (d.widths[l] < 1 || d.widths[l] > TW) return hipErrorInvalidValue;
@@ -183,7 +183,8 @@ hipError_t tiny_mlp_step(const TinyMLPDesc& d, const float* params, const float*
   float* slabs = ws + ((nb + 3) & ~3) + 4;  // keep 16-byte alignment for the vector reducer
   float* gout = nb > 1 ? slabs : grad + base;
   const long long slab = nb > 1 ? numel : 0;
-  const float loss_scale = d.loss == LOSS_XENT ? 1.f / rows : 1.f / ((float)rows * d.widths[d.n_layers]);
+  const float loss_scale = loss_scale_in >= 0.f ? loss_scale_in
+                           : d.loss == LOSS_XENT ? 1.f / rows : 1.f / ((float)rows * d.widths[d.n_layers]);
   // one block: loss written and (single rank) optimizer applied in-kernel -> ONE launch per step
   SgdFuse sg{};
   if (nb == 1 && sgd) sg = *sgd;

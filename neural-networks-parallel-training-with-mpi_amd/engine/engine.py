@@ -209,7 +209,8 @@ class MLPEngine:
                   if self.tiny_fused else None)
             ops.tiny_step(self.spec, ar, self.X[:rows], self.Y[:rows] if self.Y is not None else None,
                           self.labels[:rows] if self.labels is not None else None,
-                          self.inv_count, self.loss_out, self.ws, sgd=fz)
+                          self.inv_count, self.loss_out, self.ws, sgd=fz,
+                          loss_scale=self.loss_scale)
             for i in reversed(range(L)):
                 self.sync.ready(i)
             return
@@ -368,10 +369,12 @@ class MLPEngine:
         dz = self._dzl(last - 1, rows)
         unfused = []
         if ops.head_can_fuse_sgd(self.spec.widths[-1], self.spec.widths[-2], self.loss_kind):
-            pending = ops.head_deferred(h, ar.weight(last), ar.bias(last), self.Y[:rows],
-                                        self.inv_count, self.act, dz, ar.grad_weight(last),
-                                        ar.grad_bias(last), self.loss_out, self.loss_scale,
-                                        self.ws_pair[0], sgd=fz)
+            pending = ops.head_deferred(
+                h, ar.weight(last), ar.bias(last), self.Y[:rows] if self.Y is not None else None,
+                self.inv_count, self.act, dz, ar.grad_weight(last), ar.grad_bias(last),
+                self.loss_out, self.loss_scale, self.ws_pair[0], sgd=fz,
+                labels=self.labels[:rows] if self.labels is not None else None,
+                loss=self.loss_kind, dlogits=self.dlogits[:rows])
         else:
             self._head(h, dz)
             pending = None

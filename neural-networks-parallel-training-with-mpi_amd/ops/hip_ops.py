@@ -112,7 +112,9 @@ class HipOps:
                    int(self.lib.head_fused_workspace_bytes(rows, in_f))) + 4 * off
 
     def head_can_fuse_sgd(self, out_f, in_f, loss) -> bool:
-        return bool(self.lib.head_can_fuse(out_f, in_f, LOSS_CODES[loss]))
+        # both head forms end in a slab combine that can apply the update: the fused regression
+        # kernel's (out == 1, MSE) and the separate weight-gradient kernel's
+        return True
 
     def head(self, a, W, b, y, labels, loss: str, inv_count: float, act_prev: str, dz_out,
              gW, gb, dlogits, loss_out, loss_scale: float, ws=None, sgd=None):
@@ -130,24 +132,35 @@ class HipOps:
                                 ACT_CODES[act_prev], _p(dz_out), _p(gW), _p(gb), _p(wws), _p(lp),
                                 float(loss_scale), _p(loss_out), self.stream, sgd)
             return
-        assert sgd is None, "optimizer fusion needs the fused regression head"
         self.lib.head_fwd(_p(a), a_bf16, rows, in_f, _p(W), _p(b), out_f, _p(y), _p(labels),
                           LOSS_CODES[loss], float(inv_count), ACT_CODES[act_prev], _p(dz_out),
                           _p(dlogits), _p(lp), self.stream)
         self.lib.head_wgrad(_p(a), a_bf16, rows, in_f, _p(dlogits), out_f, _p(gW), _p(gb),
-                            _p(wws), _p(lp), parts, float(loss_scale), _p(loss_out), self.stream)
+                            _p(wws), _p(lp), parts, float(loss_scale), _p(loss_out), self.stream,
+                            sgd)
 
     # ---------------- grouped backward (bf16) ----------------
     def head_deferred(self, a, W, b, y, inv_count: float, act_prev: str, dz_out, gW, gb, loss_out,
-                      loss_scale: float, ws, sgd=None):
-        """Fused regression head whose slab combine is deferred (returned, see bwd_group)."""
+                      loss_scale: float, ws, sgd=None, labels=None, loss: str = "mse",
+                      dlogits=None):
+        """Head whose final slab combine (gW, gb, loss; optionally the optimizer update) is
+        deferred: returned as a SlabReduce for the next grouped backward launch (bwd_group)."""
         rows, in_f = a.shape
+        out_f = W.shape[0]
         parts, off = self._head_split(rows, in_f)
-        self._check_ws(ws, self.head_workspace_bytes(rows, in_f, 1), "head")
+        self._check_ws(ws, self.head_workspace_bytes(rows, in_f, out_f), "head")
         a_bf16 = 1 if a.dtype == torch.bfloat16 else 0
-        return self.lib.head_fused_deferred(_p(a), a_bf16, rows, in_f, _p(W), _p(b), _p(y),
-                                            float(inv_count), ACT_CODES[act_prev], _p(dz_out),
-                                            _p(gW), _p(gb), _p(ws[off:]), _p(ws[:parts]),
+        if self.lib.head_can_fuse(out_f, in_f, LOSS_CODES[loss]):
+            return self.lib.head_fused_deferred(_p(a), a_bf16, rows, in_f, _p(W), _p(b), _p(y),
+                                                float(inv_count), ACT_CODES[act_prev], _p(dz_out),
+                                                _p(gW), _p(gb), _p(ws[off:]), _p(ws[:parts]),
+                                                float(loss_scale), _p(loss_out), self.stream, sgd)
+        _check(dlogits is not None, "multi-output head needs a dlogits buffer")
+        self.lib.head_fwd(_p(a), a_bf16, rows, in_f, _p(W), _p(b), out_f, _p(y), _p(labels),
+                          LOSS_CODES[loss], float(inv_count), ACT_CODES[act_prev], _p(dz_out),
+                          _p(dlogits), _p(ws[:parts]), self.stream)
+        return self.lib.head_wgrad_deferred(_p(a), a_bf16, rows, in_f, _p(dlogits), out_f, _p(gW),
+                                            _p(gb), _p(ws[off:]), _p(ws[:parts]), parts,
                                             float(loss_scale), _p(loss_out), self.stream, sgd)
 
     def bwd_group_supported(self, rows, out_f, in_f) -> bool:
@@ -185,14 +198,16 @@ class HipOps:
     def tiny_can_fuse_sgd(self, rows: int) -> bool:
         return bool(self.lib.tiny_mlp_can_fuse_sgd(rows))
 
-    def tiny_step(self, spec, arena, X, y, labels, inv_count, loss_out, ws, sgd=None):
+    def tiny_step(self, spec, arena, X, y, labels, inv_count, loss_out, ws, sgd=None,
+                  loss_scale=None):
         L = spec.n_layers
         w_off = [arena.by_name[f"layers.{2 * i}.weight"].offset for i in range(L)]
         b_off = [arena.by_name[f"layers.{2 * i}.bias"].offset for i in range(L)]
         self.lib.tiny_mlp_step(list(spec.widths), w_off, b_off, ACT_CODES[spec.activation],
                                LOSS_CODES[spec.loss], _p(arena.master), _p(X), _p(y), _p(labels),
                                X.shape[0], float(inv_count), _p(arena.grad), arena.numel,
-                               _p(ws), _p(loss_out), self.stream, sgd)
+                               _p(ws), _p(loss_out), self.stream, sgd,
+                               -1.0 if loss_scale is None else float(loss_scale))
 
     # ---------------- data ----------------
     def gather_rows(self, src, idx, dst):

@@ -376,3 +376,30 @@ def test_grad_accum_gpu_matches_cpu_and_single_batch():
     assert a.losses == pytest.approx(b.losses, rel=1e-5)
     c = trainer.run_worker(_cfg(device="cuda", nepochs=3, grad_accum=2))
     assert c.losses[-1] < c.losses[0]
+
+
+@pytest.mark.parametrize("grouped", [True, False])
+def test_xent_head_optimizer_fusion_is_bitwise_equal(grouped):
+    """Multi-output head: SGD applied in the head weight-gradient combine (deferred into the
+    grouped backward launch, or run right after the head) == a separate SGD pass."""
+    import nnmpi_amd.engine.engine as eng_mod
+    cfg = TrainConfig(device="cuda", widths=[784, 1024, 1024, 10], n_features=784, loss="xent",
+                      n_samples=2048, dtype="bf16", nepochs=4, lr=0.05, print_rank="none",
+                      data_gen="device", data_dist="local")
+    orig = eng_mod.MLPEngine.__init__
+
+    def patched(fuse):
+        def init(self, *args, **kw):
+            kw["fuse_sgd"] = fuse
+            kw["grouped"] = grouped
+            orig(self, *args, **kw)
+        return init
+    try:
+        eng_mod.MLPEngine.__init__ = patched(True)
+        a = trainer.run_worker(cfg)
+        eng_mod.MLPEngine.__init__ = patched(False)
+        b = trainer.run_worker(cfg)
+    finally:
+        eng_mod.MLPEngine.__init__ = orig
+    assert a.losses == b.losses
+    assert torch.equal(a.final_params, b.final_params)
