@@ -119,7 +119,7 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
   });
 
   // ---- head ----
-  m.def("head_fwd_parts", &head_fwd_parts);
+  m.def("head_fwd_parts", &head_fwd_parts, py::arg("rows"), py::arg("in"), py::arg("out") = 1);
   m.def("head_fwd", [](uptr a, int a_bf16, int rows, int in, uptr W, uptr b, int out, uptr y,
                        uptr labels, int loss, float inv_count, int act_prev, uptr dz, uptr dl,
                        uptr lp, uptr s) {

@@ -1139,6 +1139,12 @@ static hipError_t launch_t(GemmParams p, int splits, hipStream_t s, int variant 
         case 6: return launch_dma<128, 64, 2, 2, 3, LA, LB, EPI, ACT, BG>(p, splits, s);
         case 7: return launch_dma<64, 128, 2, 4, 3, LA, LB, EPI, ACT, BG>(p, splits, s);
         case 8: return launch_dma<128, 128, 2, 2, 4, LA, LB, EPI, ACT, BG>(p, splits, s);
+        // rectangular tiles (0.75x the L2->LDS bytes per FLOP of 128x128) for shapes with
+        // >= 256 of them
+        case 10: return launch_dma<256, 128, 4, 2, 2, LA, LB, EPI, ACT, BG>(p, splits, s);
+        case 11: return launch_dma<128, 256, 2, 4, 2, LA, LB, EPI, ACT, BG>(p, splits, s);
+        case 12: return launch_dma<256, 128, 4, 2, 3, LA, LB, EPI, ACT, BG>(p, splits, s);
+        case 13: return launch_dma<128, 256, 2, 4, 3, LA, LB, EPI, ACT, BG>(p, splits, s);
         default: return launch_dma<128, 128, 2, 4, 2, LA, LB, EPI, ACT, BG>(p, splits, s);  // = variant 4
       }
     } else {

@@ -304,7 +304,12 @@ static int head_rpw(int in) {
 }
 
 // one wave-iteration per wave where possible: blocks = rows / (waves * RPW), capped at 256
-int head_fwd_parts(int rows, int in) {
+// MFMA multi-output head (head_mfma_kernel): one block per CU (measured on the 8192 x 1024 x 10
+// head: 512 blocks, one row group each and 2 per CU, 16.0 us; 256 blocks 15.3 us)
+constexpr int MH_MAX_BLOCKS = 256;
+
+int head_fwd_parts(int rows, int in, int out) {
+  if (out > 1 && (in == 512 || in == 1024)) return std::max(1, std::min((rows + 15) / 16, MH_MAX_BLOCKS));
   const int per_block = head_waves(in) * head_rpw(in);
   return std::max(1, std::min((rows + per_block - 1) / per_block, 256));
 }
@@ -358,6 +363,30 @@ constexpr int MH_WAVES = 4;
 
 __device__ __forceinline__ int mh_off(int n, int k, int in) { return n * in + (((k >> 2) ^ (n & 15)) << 2) + (k & 3); }
 
+// Global inputs of one 16-row group for one lane (row r = lane & 15, column group g = lane >> 4)
+template <int Q>
+struct MhLoads {
+  bf16x8 xs[Q / 32];   // this wave's quarter, 8 features per 32-chunk (logits operand, and the
+                       // saved activation the dZ of the same features needs)
+  float yv[4];         // MSE targets of outputs 4g .. 4g+3
+  int lab;             // cross-entropy label
+};
+
+template <int Q, int LOSS>
+__device__ __forceinline__ void mh_load(MhLoads<Q>& L, const HeadArgs& p, const bf16* A, int rowc,
+                                        int w, int g) {
+  constexpr int in = 4 * Q;
+  const bf16* ar = A + (long long)rowc * in + w * Q;
+#pragma unroll
+  for (int c = 0; c < Q / 32; ++c) L.xs[c] = *reinterpret_cast<const bf16x8*>(ar + c * 32 + g * 8);
+  if constexpr (LOSS == LOSS_XENT) {
+    L.lab = (int)p.labels[rowc];
+  } else {
+#pragma unroll
+    for (int j = 0; j < 4; ++j) L.yv[j] = p.y[(long long)rowc * p.out + min(4 * g + j, p.out - 1)];
+  }
+}
+
 template <int ACT, int LOSS, int Q>
 __global__ void __launch_bounds__(64 * MH_WAVES) head_mfma_kernel(HeadArgs p) {
   extern __shared__ __attribute__((aligned(16))) float ml[];   // W image [16][in] + partials
@@ -365,6 +394,14 @@ __global__ void __launch_bounds__(64 * MH_WAVES) head_mfma_kernel(HeadArgs p) {
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   constexpr int in = 4 * Q;
   const int out = p.out;
+  const bf16* A = reinterpret_cast<const bf16*>(p.a);
+  bf16* DZ = reinterpret_cast<bf16*>(p.dz_prev);
+  const int r = lane & 15, g = lane >> 4;
+  const int ngroups = (p.rows + 15) / 16;
+  // software pipeline: the global loads of a block's next row group are issued before the
+  // current one is computed (first group: before the W image is built)
+  MhLoads<Q> cur, nxt;
+  mh_load<Q, LOSS>(cur, p, A, min((int)blockIdx.x * 16 + r, p.rows - 1), w, g);
   // W image: 16-byte loads, all issued before the first LDS store (compile-time trip count)
   constexpr int NV = 16 * in / 4 / (64 * MH_WAVES);
   f32x4 wv[NV];
@@ -380,30 +417,17 @@ __global__ void __launch_bounds__(64 * MH_WAVES) head_mfma_kernel(HeadArgs p) {
   }
   f32x4* part = reinterpret_cast<f32x4*>(ml + 16 * in);          // [4 waves][64 lanes]
   __syncthreads();
-  const bf16* A = reinterpret_cast<const bf16*>(p.a);
-  bf16* DZ = reinterpret_cast<bf16*>(p.dz_prev);
-  const int r = lane & 15, g = lane >> 4;
   float bias[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) bias[j] = (4 * g + j) < out ? p.b[4 * g + j] : 0.f;
   float block_loss = 0.f;
-  const int ngroups = (p.rows + 15) / 16;
   for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
     const int row = grp * 16 + r;
     const bool valid = row < p.rows;
-    const int rowc = valid ? row : p.rows - 1;
-    // every global load of the group first (row chunks for the logits, the saved activation
-    // for dZ): one exposed round trip per group instead of one per loop iteration
-    bf16x8 xs[Q / 32];
-    bf16x4 avs[Q / 16];
-#pragma unroll
-    for (int c = 0; c < Q / 32; ++c)
-      xs[c] = *reinterpret_cast<const bf16x8*>(A + (long long)rowc * in + w * Q + c * 32 + g * 8);
-    if (DZ != nullptr) {
-#pragma unroll
-      for (int t = 0; t < Q / 16; ++t)
-        avs[t] = *reinterpret_cast<const bf16x4*>(A + (long long)rowc * in + w * Q + t * 16 + 4 * g);
-    }
+    // next group's loads (past the end: the last row again, never read back)
+    mh_load<Q, LOSS>(nxt, p, A, min((grp + (int)gridDim.x) * 16 + r, p.rows - 1), w, g);
+    __builtin_amdgcn_sched_barrier(0);
+    const bf16x8* xs = cur.xs;
     // ---- logits: this wave's quarter of the features ----
     f32x4 acc = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
@@ -440,7 +464,7 @@ __global__ void __launch_bounds__(64 * MH_WAVES) head_mfma_kernel(HeadArgs p) {
       se += __shfl_xor(se, 16, 64);
       se += __shfl_xor(se, 32, 64);
       const float lse = mx + __logf(se);
-      const int lab = (int)p.labels[rowc];
+      const int lab = cur.lab;
       float picked = 0.f;
 #pragma unroll
       for (int j = 0; j < 4; ++j) {
@@ -456,7 +480,7 @@ __global__ void __launch_bounds__(64 * MH_WAVES) head_mfma_kernel(HeadArgs p) {
       for (int j = 0; j < 4; ++j) {
         const int n = 4 * g + j;
         z[j] += bias[j];
-        const float d = n < out ? z[j] - p.y[(long long)rowc * out + n] : 0.f;
+        const float d = n < out ? z[j] - cur.yv[j] : 0.f;
         row_loss += d * d;
         dl[j] = valid ? 2.f * d * p.inv_count : 0.f;
       }
@@ -481,23 +505,34 @@ __global__ void __launch_bounds__(64 * MH_WAVES) head_mfma_kernel(HeadArgs p) {
         const float t2 = __shfl(dl[2], src, 64), t3 = __shfl(dl[3], src, 64);
         bfr[st] = g == 0 ? t0 : g == 1 ? t1 : g == 2 ? t2 : t3;
       }
+      // 32 features per pair of 16x16 tiles; A-operand row i of tile half h is feature
+      // f0 + 8(i>>2) + 4h + (i&3), so a lane's two accumulators are features f0 + 8g .. +7 of
+      // its row: ONE 16-byte store per pair, and the activation it needs is the logits
+      // operand xs[tp] already in registers
 #pragma unroll
-      for (int t = 0; t < Q / 16; ++t) {
-        const int k0 = w * Q + t * 16;
-        const bf16x4 av = avs[t];
-        f32x4 d = {0.f, 0.f, 0.f, 0.f};
+      for (int tp = 0; tp < Q / 32; ++tp) {
+        const int f0 = w * Q + tp * 32;
+        const int kf = f0 + 8 * (r >> 2) + (r & 3);
+        const bf16x8 av = xs[tp];
+        f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
-        for (int st = 0; st < 4; ++st)
-          d = __builtin_amdgcn_mfma_f32_16x16x4f32(ml[mh_off(4 * st + g, k0 + r, in)], bfr[st], d, 0, 0, 0);
+        for (int st = 0; st < 4; ++st) {
+          d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ml[mh_off(4 * st + g, kf, in)], bfr[st], d0, 0, 0, 0);
+          d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ml[mh_off(4 * st + g, kf + 4, in)], bfr[st], d1, 0, 0, 0);
+        }
         if (valid) {
-          bf16x4 o;
+          bf16x8 o;
 #pragma unroll
-          for (int j = 0; j < 4; ++j) o[j] = (bf16)(d[j] * act_bwd_t<ACT>((float)av[j]));
-          *reinterpret_cast<bf16x4*>(DZ + (long long)row * in + k0 + 4 * g) = o;
+          for (int j = 0; j < 4; ++j) {
+            o[j] = (bf16)(d0[j] * act_bwd_t<ACT>((float)av[j]));
+            o[j + 4] = (bf16)(d1[j] * act_bwd_t<ACT>((float)av[j + 4]));
+          }
+          *reinterpret_cast<bf16x8*>(DZ + (long long)row * in + f0 + 8 * g) = o;
         }
       }
     }
     __syncthreads();   // the partial buffer is rewritten by the next group
+    cur = nxt;
   }
   if (w == 0) {
     const float t = wave_sum(block_loss);
@@ -541,7 +576,7 @@ static hipError_t head_fwd_impl(const void* a, int a_bf16, int rows, int in, con
   const size_t smem = (size_t)(out * in + (fuse ? head_waves(in) * in : 0)) * sizeof(float);
   if (smem > 65536 + 32768) return hipErrorInvalidValue;
   HeadArgs h{a, rows, in, W, b, out, y, labels, inv_count, act_prev, dz_prev, dlogits, loss_part};
-  const int blocks = head_fwd_parts(rows, in);
+  const int blocks = head_fwd_parts(rows, in, out);
   if (head_mfma_ok(a_bf16, in, out, fuse)) return head_mfma_launch(h, act_prev, loss, blocks, s);
 #define HL(TA, LS, FU, OM) head_launch_c<TA, LS, FU, OM>(h, act_prev, blocks, smem, wslab, bslab, s)
   if (fuse) {

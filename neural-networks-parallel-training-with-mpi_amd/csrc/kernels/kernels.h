@@ -109,7 +109,7 @@ hipError_t linear_wgrad_f32(const float* dZ, int lddz, const float* X, int ldx, 
 // a: [rows][in] activations (bf16 if a_bf16 else fp32); W: [out][in] fp32; y: [rows][out] fp32
 // (MSE) or labels int64 (XENT).  Writes dlogits [rows][out] fp32, dz_prev [rows][in] (same dtype
 // as a; may be null), loss partials [n_part].
-int head_fwd_parts(int rows, int in);
+int head_fwd_parts(int rows, int in, int out = 1);   // loss partials (= blocks) of head_fwd
 hipError_t head_fwd(const void* a, int a_bf16, int rows, int in, const float* W, const float* b,
                     int out, const float* y, const int64_t* labels, int loss, float inv_count,
                     int act_prev, void* dz_prev, float* dlogits, float* loss_part, hipStream_t s);

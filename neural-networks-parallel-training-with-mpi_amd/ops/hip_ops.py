@@ -99,15 +99,15 @@ class HipOps:
                                       M, N, rows, _p(ws), self.stream)
 
     # ---------------- head ----------------
-    def head_parts(self, rows: int, in_f: int) -> int:
-        return int(self.lib.head_fwd_parts(rows, in_f))
+    def head_parts(self, rows: int, in_f: int, out_f: int = 1) -> int:
+        return int(self.lib.head_fwd_parts(rows, in_f, out_f))
 
-    def _head_split(self, rows, in_f):
-        parts = self.head_parts(rows, in_f)
+    def _head_split(self, rows, in_f, out_f=1):
+        parts = self.head_parts(rows, in_f, out_f)
         return parts, (parts + 3) // 4 * 4 + 4   # keep the slab region 16-byte aligned
 
     def head_workspace_bytes(self, rows, in_f, out_f, loss="mse") -> int:
-        _, off = self._head_split(rows, in_f)
+        _, off = self._head_split(rows, in_f, out_f)
         return max(int(self.lib.head_wgrad_workspace_bytes(rows, in_f, out_f)),
                    int(self.lib.head_fused_workspace_bytes(rows, in_f))) + 4 * off
 
@@ -121,7 +121,7 @@ class HipOps:
         rows, in_f = a.shape
         out_f = W.shape[0]
         _check(in_f % 8 == 0, f"head needs in%8==0 (in={in_f})")
-        parts, off = self._head_split(rows, in_f)
+        parts, off = self._head_split(rows, in_f, out_f)
         self._check_ws(ws, self.head_workspace_bytes(rows, in_f, out_f), "head")
         lp = ws[:parts]
         wws = ws[off:]
@@ -147,7 +147,7 @@ class HipOps:
         deferred: returned as a SlabReduce for the next grouped backward launch (bwd_group)."""
         rows, in_f = a.shape
         out_f = W.shape[0]
-        parts, off = self._head_split(rows, in_f)
+        parts, off = self._head_split(rows, in_f, out_f)
         self._check_ws(ws, self.head_workspace_bytes(rows, in_f, out_f), "head")
         a_bf16 = 1 if a.dtype == torch.bfloat16 else 0
         if self.lib.head_can_fuse(out_f, in_f, LOSS_CODES[loss]):

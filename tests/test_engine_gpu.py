@@ -232,7 +232,7 @@ def test_grouped_backward_async_lds_reads_bitwise_equal(mode):
     assert torch.equal(a.final_params, b.final_params)
 
 
-@pytest.mark.parametrize("variant", [1, 2, 5, 6, 8])
+@pytest.mark.parametrize("variant", [1, 2, 5, 6, 8, 10, 11, 12, 13])
 def test_forward_variants_bitwise_equal(variant):
     """Every forward main-loop variant accumulates each output in the same k order."""
     from nnmpi_amd import native
