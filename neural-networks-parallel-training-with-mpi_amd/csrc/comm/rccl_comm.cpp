@@ -143,9 +143,9 @@ GradSync::GradSync(RcclComm* comm, int n_buckets, int priority) : comm_(comm) {
 }
 
 GradSync::~GradSync() {
-  for (auto& e : ready_) hipEventDestroy(e);
-  if (done_) hipEventDestroy(done_);
-  if (comm_stream_) hipStreamDestroy(comm_stream_);
+  for (auto& e : ready_) (void)hipEventDestroy(e);
+  if (done_) (void)hipEventDestroy(done_);
+  if (comm_stream_) (void)hipStreamDestroy(comm_stream_);
 }
 
 void GradSync::bucket_ready(int b, void* ptr, size_t count, int dtype, hipStream_t compute) {
@@ -162,13 +162,13 @@ void GradSync::join(hipStream_t compute) {
 
 // ---------------------------------------------------------------------------------------------
 GraphRunner::~GraphRunner() {
-  if (exec_) hipGraphExecDestroy(exec_);
-  if (graph_) hipGraphDestroy(graph_);
+  if (exec_) (void)hipGraphExecDestroy(exec_);
+  if (graph_) (void)hipGraphDestroy(graph_);
 }
 
 void GraphRunner::begin(hipStream_t s) {
-  if (exec_) { hipGraphExecDestroy(exec_); exec_ = nullptr; }
-  if (graph_) { hipGraphDestroy(graph_); graph_ = nullptr; }
+  if (exec_) { (void)hipGraphExecDestroy(exec_); exec_ = nullptr; }
+  if (graph_) { (void)hipGraphDestroy(graph_); graph_ = nullptr; }
   cap_ = s;
   HIP_THROW(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
 }
@@ -186,7 +186,7 @@ void GraphRunner::launch(hipStream_t s) {
 size_t GraphRunner::num_nodes() const {
   if (!graph_) return 0;
   size_t n = 0;
-  hipGraphGetNodes(graph_, nullptr, &n);
+  (void)hipGraphGetNodes(graph_, nullptr, &n);
   return n;
 }
 

@@ -198,3 +198,21 @@ def test_forced_tile_fwd_dgrad_wgrad(tile, M, N, K):
     tops.linear_wgrad(dz, x, rgW, rgb)
     torch.testing.assert_close(gW, rgW, rtol=1e-3, atol=2e-2)
     torch.testing.assert_close(gb, rgb, rtol=1e-3, atol=2e-2)
+
+
+def test_native_runtime_under_host_asan():
+    """The C++ runtime (RCCL communicator, GradSync, GraphRunner, launchers) driven from a native
+    binary built with host AddressSanitizer + UBSan (scripts/build_runtime_check.sh; device code
+    is not instrumented).  Any ASan/UBSan report aborts the binary with a non-zero status."""
+    import os
+    import subprocess
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    exe = os.path.join(root, "neural-networks-parallel-training-with-mpi_amd", "native_tests",
+                       "runtime_check_asan")
+    if not os.path.exists(exe):
+        pytest.skip("runtime_check_asan not built (scripts/build_runtime_check.sh)")
+    env = dict(os.environ, ASAN_OPTIONS="detect_leaks=0:abort_on_error=1",
+               UBSAN_OPTIONS="halt_on_error=1:print_stacktrace=1")
+    r = subprocess.run([exe], capture_output=True, text=True, timeout=100, env=env)
+    assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
+    assert "ALL OK" in r.stdout
