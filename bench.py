@@ -10,6 +10,13 @@ short rank only leaves a partial last tile; a LONG rank (8192 + 1 rows) would ad
 row of GEMM tiles on that rank and, since the step time is the max over ranks, slow every rank
 down.  Gradients are all-reduced over RCCL (xGMI) every step.
 
+Gradient-sync schedule (``--comm_mode``, default auto): for latency-bound gradient volumes the
+fastest schedule depends on the node's collective latency, so the three candidates (one inline
+all-reduce; ZeRO-1 reduce-scatter + sharded SGD + bf16 all-gather; per-bucket all-reduce on a
+comm stream overlapped with backward) are each timed for ``--tune_steps`` steps BEFORE the timed
+region and the fastest (max over ranks, so every rank agrees) is kept; its time per candidate
+is reported in ``config.comm_tune_ms_per_step``.  Large gradients always overlap.
+
     python bench.py [--gpus N] [--steps K] [--warmup W]
     python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
 
@@ -65,9 +72,15 @@ def parse():
     p.add_argument("--graph_chunk", type=int, default=16,
                    help="steps per replayed hipGraph (1 = one graph launch per step)")
     p.add_argument("--lr", type=float, default=1e-5)
-    p.add_argument("--comm_mode", choices=["auto", "overlap", "inline"], default="auto",
-                   help="overlap: comm stream + per-bucket SGD; inline: all-reduce on the compute "
-                        "stream (auto: inline when the gradient volume is small)")
+    p.add_argument("--comm_mode", choices=["auto", "tune", "overlap", "inline", "zero1"],
+                   default="auto",
+                   help="overlap: per-bucket all-reduce on a comm stream + per-bucket SGD; "
+                        "inline: one all-reduce on the compute stream; zero1: reduce-scatter + "
+                        "sharded SGD + bf16 all-gather; tune: time all three before the timed "
+                        "region and keep the fastest (auto: tune for small gradient volumes, "
+                        "overlap for large)")
+    p.add_argument("--tune_steps", type=int, default=32,
+                   help="steps per candidate timing in --comm_mode tune (untimed region)")
     p.add_argument("--force_comm", action="store_true",
                    help="use the RCCL gradient path even with one rank (smoke-tests comm overlap)")
     p.add_argument("--fwd_variant", type=int, default=-1, help="forward GEMM variant (experiments)")
@@ -89,7 +102,7 @@ def main():
     from nnmpi_amd.models.mlp import MLPSpec, reference_init
     from nnmpi_amd.ops.hip_ops import HipOps
     from nnmpi_amd.parallel import dist as pdist
-    from nnmpi_amd.parallel.sync import NativeRcclSync, NoSync, TorchDistSync
+    from nnmpi_amd.parallel.sync import NativeRcclSync, NoSync, ShardedSync, TorchDistSync
     from nnmpi_amd.utils.config import TrainConfig
     from nnmpi_amd import native
 
@@ -124,49 +137,101 @@ def main():
         labels = None
     # model: same seed everywhere + broadcast from rank 0 (reference ref.py:87)
     big = spec.n_params > 20_000_000
-    model = reference_init(widths, "relu", seed=0, device=dev if big else None)
-    arena = Arena([spec.layer_shape(i) for i in range(spec.n_layers)], dev,
-                  shadow_dtype=torch.bfloat16 if dtype == torch.bfloat16 else None,
-                  bucket_bytes=a.bucket_mb * 2 ** 20)
-    arena.bind_model(model)
-    del model
+    use_comm = (world > 1 or a.force_comm)
+    cfg = TrainConfig(widths=list(widths), loss=c["loss"], n_features=widths[0])
+    inv, lsc, gsc = loss_scales(cfg, rows, list(part.counts), widths[-1])
     native_comm = None
-    if (world > 1 or a.force_comm) and a.comm == "native":
+    if use_comm and a.comm == "native":
         lib = native.lib()
         uid = pg.broadcast_object(lib.rccl_unique_id() if rank == 0 else None, 0)
         native_comm = native.make_comm(uid, world, rank, dev.index)
-        s = torch.cuda.current_stream()
-        native_comm.broadcast(arena.master.data_ptr(), arena.numel, 0, 0, int(s.cuda_stream))
-        s.synchronize()
-        arena.sync_shadow()
-        inline = (a.comm_mode == "inline" or
-                  (a.comm_mode == "auto" and arena.numel * 4 <= INLINE_MAX_GRAD_BYTES))
-        sync = NativeRcclSync(arena, native_comm, world, inline=inline)
-    elif world > 1:
-        dist.broadcast(arena.master, src=0, group=pg.nccl)
-        arena.sync_shadow()
-        sync = TorchDistSync(arena, pg.nccl, world)
-    else:
-        sync = NoSync(arena)
-    ops = HipOps(dev)
-    eng = MLPEngine(spec, arena, ops, sync, device=dev, dtype=dtype, rows_capacity=rows,
-                    lr=a.lr, momentum=0.9, use_graph=not a.no_graph,
-                    overlap=not a.no_overlap, grouped=not a.no_group)
-    eng.load_batch(X.to(dtype), Y, labels)
-    del X
-    cfg = TrainConfig(widths=list(widths), loss=c["loss"], n_features=widths[0])
-    inv, lsc, gsc = loss_scales(cfg, rows, list(part.counts), widths[-1])
-    eng.set_scales(inv, lsc, gsc)
+
+    def build(mode):
+        """One arena + gradient-sync strategy + engine.  mode: inline | overlap | zero1."""
+        model = reference_init(widths, "relu", seed=0, device=dev if big else None)
+        arena = Arena([spec.layer_shape(i) for i in range(spec.n_layers)], dev,
+                      shadow_dtype=torch.bfloat16 if dtype == torch.bfloat16 else None,
+                      bucket_bytes=a.bucket_mb * 2 ** 20,
+                      pad_to=64 * world if mode == "zero1" else 64)
+        arena.bind_model(model)
+        del model
+        if native_comm is not None:
+            s = torch.cuda.current_stream()
+            native_comm.broadcast(arena.master.data_ptr(), arena.numel, 0, 0, int(s.cuda_stream))
+            s.synchronize()
+            arena.sync_shadow()
+            if mode == "zero1":
+                sync = ShardedSync(arena, world, rank, native_comm=native_comm)
+            else:
+                sync = NativeRcclSync(arena, native_comm, world, inline=(mode == "inline"))
+        elif world > 1:
+            dist.broadcast(arena.master, src=0, group=pg.nccl)
+            arena.sync_shadow()
+            sync = TorchDistSync(arena, pg.nccl, world)
+        else:
+            sync = NoSync(arena)
+        eng = MLPEngine(spec, arena, HipOps(dev), sync, device=dev, dtype=dtype,
+                        rows_capacity=rows, lr=a.lr, momentum=0.9, use_graph=not a.no_graph,
+                        overlap=not a.no_overlap, grouped=not a.no_group)
+        eng.load_batch(Xc, Y, labels)
+        eng.set_scales(inv, lsc, gsc)
+        return eng
 
     def barrier():
         torch.cuda.synchronize()
         pg.barrier()
         torch.cuda.synchronize()
 
+    def timed(eng, n, chunk):
+        """Wall time of n steps, max over ranks (graphs captured beforehand)."""
+        eng.prepare_steps(n, chunk)
+        barrier()
+        t0 = time.perf_counter()
+        eng.run_steps(n, chunk)
+        eng.synchronize()
+        torch.cuda.synchronize()
+        el = time.perf_counter() - t0
+        pg.barrier()
+        if world > 1:
+            t = torch.tensor([el], dtype=torch.float64)
+            pg.allreduce_cpu(t, op=dist.ReduceOp.MAX)
+            el = float(t.item())
+        return el
+
+    Xc = X.to(dtype)
+    del X
+    chunk = max(1, a.graph_chunk)
+    grad_bytes = spec.n_params * 4
+    mode = a.comm_mode
+    if mode == "auto":
+        # small (latency-bound) gradients: the best collective schedule depends on the link
+        # latency of the node, so it is measured (untimed, before the timed region) rather than
+        # assumed; large gradients always overlap per-bucket all-reduces with the backward.
+        mode = "tune" if grad_bytes <= INLINE_MAX_GRAD_BYTES else "overlap"
+    if native_comm is None:
+        mode = "inline" if use_comm else "none"
+    tune = None
+    if mode == "tune":
+        tune = {}
+        eng = None
+        for m in ("inline", "zero1", "overlap"):
+            e = build(m)
+            e.run_steps(a.warmup, chunk)
+            tm = min(timed(e, a.tune_steps, chunk) for _ in range(2))
+            tune[m] = round(tm / a.tune_steps * 1e3, 5)
+            # every rank sees the same max-over-ranks times, so every rank keeps the same mode
+            if eng is None or tm < best_t:
+                eng, best_t, mode = e, tm, m
+            del e
+        torch.cuda.empty_cache()
+    else:
+        eng = build(mode)
+        eng.run_steps(a.warmup, chunk)
+    sync = eng.sync
+    del Xc
+
     # graph mode: steps replayed as hipGraphs of `chunk` complete consecutive steps (one
     # replay's fixed cost per chunk); every graph is captured before the timed region
-    chunk = max(1, a.graph_chunk)
-    eng.run_steps(a.warmup, chunk)
     eng.prepare_steps(a.steps, chunk)
     loss0 = eng.loss()
     barrier()
@@ -207,8 +272,8 @@ def main():
                        "comm": a.comm if (world > 1 or a.force_comm) else "none",
                        "graph": not a.no_graph, "graph_chunk": a.graph_chunk, "overlap": not a.no_overlap,
                        "grouped": not a.no_group,
-                       "comm_mode": (("inline" if sync.inline else "overlap")
-                                     if hasattr(sync, "inline") else None),
+                       "comm_mode": mode if use_comm else None,
+                       "comm_tune_ms_per_step": tune,
                        "bucket_mb": a.bucket_mb},
             "model_tflops_per_s": round(tflops, 2),
             "loss_after_warmup": loss0,
