@@ -66,6 +66,23 @@ __device__ __forceinline__ int xcd_remap(int bid, int nwg) {
   return (xcd < r ? xcd * (q + 1) : r * (q + 1) + (xcd - r) * q) + bid / 8;
 }
 
+// Grouped tile order: consecutive block ids walk a GM-row band column by column, so the
+// blocks one XCD runs at the same time (consecutive ids after xcd_remap) cover a GM x (n/GM)
+// patch of output tiles and share GM A panels + n/GM B panels in that XCD's L2, instead of one
+// A panel + n distinct B panels (row-major order).  Bijective for any gx, gy (the last band may
+// be shorter).
+__device__ __forceinline__ void grouped_tile(int bid, int gx, int gy, int gm, int& tx, int& ty) {
+  if (gm <= 1) {
+    tx = bid % gx;
+    ty = bid / gx;
+    return;
+  }
+  const int per = gm * gx, first = (bid / per) * gm;
+  const int gsz = min(gy - first, gm), r = bid % per;
+  ty = first + r % gsz;
+  tx = r / gsz;
+}
+
 // torch.optim.SGD update of one element (sgd.py semantics; dampening/nesterov/weight decay).
 // Contraction is pinned (explicit fmaf, no compiler contraction) so every kernel that applies
 // the update -- the standalone optimizer pass or a fused reducer epilogue -- rounds identically.

@@ -744,7 +744,14 @@ constexpr int PP_BUF = 4 * PP_HALF;        // one K-tile: A0 A1 B0 B1
 constexpr int PP_SMEM = 2 * PP_BUF;        // 128 KiB
 constexpr int PP_THREADS = 512;
 
-template <int LA, int LB, int EPI, int ACT, bool BIASGRAD>
+// LATE_LGKM: the phase's LDS reads are retired AFTER the pre-MFMA barrier (their latency
+// overlaps the barrier wait; cdna_hip_programming.md 8-phase template order).  WAR margin: a
+// half is re-staged >= 2 phases after its read, and with the one-barrier stagger the earliest
+// overwriting DMA issue is 3 barriers after the read's phase barrier, so retiring the reads one
+// barrier later stays inside it.
+// GM: grouped tile order (grouped_tile) -- 32 blocks resident per XCD read 4 A + 8 B panels per
+// K-tile instead of 1 A + 32 B at the 8192-wide shape.
+template <int LA, int LB, int EPI, int ACT, bool BIASGRAD, bool LATE_LGKM = true, int GM = 4>
 __global__ void __launch_bounds__(PP_THREADS) gemm_bf16_pp256_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   constexpr int BK = GEMM_BK;
@@ -753,7 +760,8 @@ __global__ void __launch_bounds__(PP_THREADS) gemm_bf16_pp256_kernel(GemmParams 
   const int wm = w >> 2, wn = w & 3;
   const int gx = gridDim.x, gy = gridDim.y;
   const int bid = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy);
-  const int tx = bid % gx, ty = bid / gx;
+  int tx, ty;
+  grouped_tile(bid, gx, gy, GM, tx, ty);
   const int split = blockIdx.z;
   const int m0 = ty * 256, n0 = tx * 256;
   const int kbeg = split * p.k_per_split;
@@ -849,9 +857,16 @@ __global__ void __launch_bounds__(PP_THREADS) gemm_bf16_pp256_kernel(GemmParams 
       } else {
         pb1.issue(rsB, B1(b), w, kof(t + 2), kend);
       }
-      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
-      __builtin_amdgcn_sched_barrier(0);
-      __builtin_amdgcn_s_barrier();
+      if constexpr (LATE_LGKM) {
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+      } else {
+        asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+        __builtin_amdgcn_sched_barrier(0);
+        __builtin_amdgcn_s_barrier();
+      }
       // ---- MFMA section: quadrant (hA, hB) ----
       const int hA = ph >> 1;                        // P1,P2 -> A0; P3,P4 -> A1
       const int hB = (ph == 1 || ph == 2) ? 1 : 0;   // P1,P4 -> B0; P2,P3 -> B1
@@ -1119,10 +1134,21 @@ static hipError_t launch_t(GemmParams p, int splits, hipStream_t s, int variant 
     if (variant == 9) return launch_dma<256, 256, 2, 4, 2, LA, LB, EPI, ACT, BG>(p, splits, s);
     dim3 grid((p.N + 255) / 256, (p.M + 255) / 256, splits);
     set_extents<LA, LB>(p);
-    auto kfn = gemm_bf16_pp256_kernel<LA, LB, EPI, ACT, BG>;
+    // default: reads retired after the barrier + grouped tile order (GM 4); A/B variants:
+    // 16 = both off (previous default), 17 = late reads + row-major order, 18 = GM 8
+    using K = void (*)(GemmParams);
+    static const K kfns[4] = {gemm_bf16_pp256_kernel<LA, LB, EPI, ACT, BG, true, 4>,
+                              gemm_bf16_pp256_kernel<LA, LB, EPI, ACT, BG, false, 1>,
+                              gemm_bf16_pp256_kernel<LA, LB, EPI, ACT, BG, true, 1>,
+                              gemm_bf16_pp256_kernel<LA, LB, EPI, ACT, BG, true, 8>};
+    // (the weight gradient -- XMAJ x XMAJ, 4 waves of tiles at 8192 wide -- measured 2-3 %
+    // faster in row-major order: profiles/gemm_wide8192_pp256_variants.json)
+    const int dflt = EPI == EPI_F32 ? 2 : 0;
+    const K kfn = kfns[(variant >= 16 && variant <= 18) ? variant - 15 : dflt];
     static bool attr = false;
     if (!attr) {
-      (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, PP_SMEM);
+      for (K f : kfns)
+        (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, PP_SMEM);
       attr = true;
     }
     hipLaunchKernelGGL(kfn, grid, dim3(PP_THREADS), PP_SMEM, s, p);

@@ -56,6 +56,7 @@ def main():
     impls = [(int(i), int(t), int(v)) for i in a.impls.split(",") for t in a.tiles.split(",")
              for v in (a.variants.split(",") if i == "2" else ["0"])]
     res = {(j, i): [] for j in jobs for i in impls}
+    first_out, same = {}, {}
     for r in range(a.rounds):
         for name in jobs:
             for impl in impls:
@@ -71,6 +72,12 @@ def main():
                 if ws.numel() < need:
                     ws = torch.empty(need, device=dev)
                 fn()
+                if r == 0 and impl[0] != 0:
+                    # bitwise check of every own-kernel variant against the first one (same
+                    # MFMA order per output element -> identical results expected)
+                    out = {"fwd": y, "dgrad": dx, "wgrad": gW}[name].clone()
+                    ref = first_out.setdefault(name, out)
+                    same[(name, impl)] = bool(torch.equal(ref, out))
                 s, e = torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)
                 s.record()
                 for _ in range(a.iters):
@@ -83,7 +90,8 @@ def main():
         med = statistics.median(v)
         print(json.dumps({"kernel": name, "impl": impl[0], "tile": impl[1], "variant": impl[2], "rows": R, "in": K, "out": N,
                           "median_us": round(med, 2), "min_us": round(min(v), 2),
-                          "tflops": round(flops / (med * 1e-6) / 1e12, 1)}))
+                          "tflops": round(flops / (med * 1e-6) / 1e12, 1),
+                          "bitwise_equal_first_variant": same.get((name, impl))}))
     lib.set_gemm_impl(2)
     lib.set_gemm_tile(0)
     lib.set_gemm_variant(0)
