@@ -104,6 +104,7 @@ def main():
     from nnmpi_amd.parallel import dist as pdist
     from nnmpi_amd.parallel.sync import NativeRcclSync, NoSync, ShardedSync, TorchDistSync
     from nnmpi_amd.utils.config import TrainConfig
+    from nnmpi_amd.utils.metrics import comm_volume
     from nnmpi_amd import native
 
     job = pdist.detect_job()
@@ -274,6 +275,9 @@ def main():
                        "grouped": not a.no_group,
                        "comm_mode": mode if use_comm else None,
                        "comm_tune_ms_per_step": tune,
+                       "grad_wire_bytes_per_rank": comm_volume(
+                           eng.arena.numel, world, sharded=(mode == "zero1"),
+                           shadow=eng.arena.shadow is not None)["wire_bytes_per_rank"],
                        "bucket_mb": a.bucket_mb},
             "model_tflops_per_s": round(tflops, 2),
             "loss_after_warmup": loss0,

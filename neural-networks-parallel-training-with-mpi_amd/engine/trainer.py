@@ -33,7 +33,7 @@ from ..parallel import dist as pdist
 from ..parallel.sync import NativeRcclSync, NoSync, ShardedSync, TorchDistSync
 from ..utils import checkpoint as ckpt
 from ..utils.config import TrainConfig, config_from_args
-from ..utils.metrics import MetricsWriter
+from ..utils.metrics import MetricsWriter, comm_bus_gbps, comm_volume, parallel_efficiency
 from ..utils.seqcheck import SequenceChecker
 from ..utils.watchdog import Watchdog
 from .arena import Arena
@@ -338,6 +338,8 @@ def _run(j: Job) -> TrainResult:
         eng.timer = EventTimer(j.device.type)
     Xc = X.to(dtype)
     metrics = MetricsWriter(cfg.metrics_json if rank == 0 else None)
+    cvol = comm_volume(arena.numel, world, cfg.grad_dtype, sharded=getattr(sync, "sharded", False),
+                       shadow=arena.shadow is not None)
     seqchk = SequenceChecker(j.pg) if cfg.seqcheck else None
     wd = Watchdog(cfg.timeout_s, j.native_comm) if world > 1 else None
     res = TrainResult(rank, world, rows=rows_local)
@@ -413,9 +415,12 @@ def _run(j: Job) -> TrainResult:
                 _print(cfg, rank, f"validation loss: {vl}") if rank == 0 else None
             if seqchk:
                 seqchk.check(epoch, sync.seq)
+            sps = sum(train_counts) / dt if dt > 0 else None
             metrics.write(epoch=epoch, loss=loss, epoch_s=dt, steps=steps_per_epoch,
-                          samples_per_s=sum(train_counts) / dt if dt > 0 else None, world=world,
-                          val_loss=res.val_losses[-1] if res.val_losses else None)
+                          samples_per_s=sps, world=world,
+                          parallel_efficiency=parallel_efficiency(sps, world,
+                                                                  cfg.ref_samples_per_s),
+                          **cvol, val_loss=res.val_losses[-1] if res.val_losses else None)
             if cfg.checkpoint and cfg.checkpoint_every and (epoch + 1) % cfg.checkpoint_every == 0:
                 _gather_state(eng, sync)
                 if rank == 0:
@@ -427,7 +432,9 @@ def _run(j: Job) -> TrainResult:
             res.phase_ms = eng.timer.summary_ms()
             _print(cfg, rank, "[profile] mean ms per step: " +
                    ", ".join(f"{k} {v:.4f}" for k, v in res.phase_ms.items()))
-            metrics.write(profile_ms_per_step=res.phase_ms, rank=rank)
+            comm_ms = res.phase_ms.get("bwd->comm")
+            metrics.write(profile_ms_per_step=res.phase_ms, rank=rank,
+                          comm_bus_GBps=comm_bus_gbps(cvol["wire_bytes_per_rank"], comm_ms))
         _gather_state(eng, sync)
         if cfg.checkpoint and rank == 0:
             ckpt.save(cfg.checkpoint, arena, cfg.nepochs, eng.steps_done, cfg)

@@ -86,6 +86,7 @@ class TrainConfig:
     timeout_s: float = 300.0
     seqcheck: bool = False
     profile_steps: bool = False
+    ref_samples_per_s: Optional[float] = None   # 1-GPU samples/s -> parallel efficiency metric
     nprocs: int = 0                   # >0: self-spawn this many ranks when not under a launcher
 
     def __post_init__(self):
@@ -164,6 +165,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--timeout_s", type=float, default=300.0)
     p.add_argument("--seqcheck", action="store_true")
     p.add_argument("--profile_steps", action="store_true")
+    p.add_argument("--ref_samples_per_s", type=float, default=None,
+                   help="single-GPU samples/s of the same per-rank work: the JSON metrics then "
+                        "carry parallel_efficiency = samples_per_s / (world * this)")
     p.add_argument("--nprocs", type=int, default=0,
                    help="self-spawn N ranks (when not launched by mpiexec/torchrun)")
     return p

@@ -72,3 +72,35 @@ class EventTimer:
     def summary_ms(self):
         n = max(self.steps, 1)
         return {k: v / n for k, v in self.intervals_ms().items()}
+
+
+def comm_volume(grad_numel: int, world: int, grad_dtype: str = "fp32", sharded: bool = False,
+                shadow: bool = False) -> dict:
+    """Bytes one rank moves per step for the gradient synchronisation (ring algorithms:
+    all-reduce 2(P-1)/P * S, reduce-scatter and all-gather (P-1)/P * S each).  ZeRO-1 = fp32
+    reduce-scatter + all-gather of the bf16 shadow (fp32 master without one)."""
+    if world <= 1:
+        return {"grad_bytes": 0, "wire_bytes_per_rank": 0}
+    f = (world - 1) / world
+    if sharded:
+        wire = f * grad_numel * 4 + f * grad_numel * (2 if shadow else 4)
+        gb = grad_numel * 4
+    else:
+        gb = grad_numel * (2 if grad_dtype == "bf16" else 4)
+        wire = 2 * f * gb
+    return {"grad_bytes": int(gb), "wire_bytes_per_rank": int(wire)}
+
+
+def comm_bus_gbps(wire_bytes_per_rank: int, comm_ms: Optional[float]) -> Optional[float]:
+    """Achieved bus bandwidth (GB/s per rank) of a step's synchronisation phase."""
+    if not comm_ms or comm_ms <= 0 or not wire_bytes_per_rank:
+        return None
+    return wire_bytes_per_rank / (comm_ms * 1e-3) / 1e9
+
+
+def parallel_efficiency(samples_per_s: Optional[float], world: int,
+                        ref_samples_per_s: Optional[float]) -> Optional[float]:
+    """S(P) / (P * S(1)) -- the BASELINE metric's efficiency term."""
+    if not samples_per_s or not ref_samples_per_s:
+        return None
+    return samples_per_s / (world * ref_samples_per_s)

@@ -96,6 +96,27 @@ def test_metrics_json(tmp_path):
     assert len(lines) == 3 and all("samples_per_s" in l for l in lines)
 
 
+def test_metrics_comm_volume_and_efficiency(tmp_path):
+    """per-rank wire bytes of the gradient sync and S(P)/(P*S(1))."""
+    import json
+    from nnmpi_amd.utils.metrics import comm_bus_gbps, comm_volume, parallel_efficiency
+    v = comm_volume(1000, 4)
+    assert v == {"grad_bytes": 4000, "wire_bytes_per_rank": 6000}       # 2*(3/4)*4000
+    z = comm_volume(1000, 4, sharded=True, shadow=True)
+    assert z["wire_bytes_per_rank"] == 3000 + 1500                         # RS fp32 + AG bf16
+    assert comm_volume(1000, 1)["wire_bytes_per_rank"] == 0
+    assert abs(comm_bus_gbps(6000, 0.001) - 6.0) < 1e-9
+    assert parallel_efficiency(300.0, 4, 100.0) == 0.75
+    assert parallel_efficiency(300.0, 4, None) is None
+    mj = str(tmp_path / "m.jsonl")
+    run_ranks(TrainConfig(print_rank="none", metrics_json=mj, ref_samples_per_s=1000.0), 2)
+    lines = [json.loads(l) for l in open(mj)]
+    assert lines and all(l["world"] == 2 for l in lines)
+    # 13 parameters padded into the 64-aligned arena, fp32 ring all-reduce over 2 ranks
+    assert all(l["wire_bytes_per_rank"] == l["grad_bytes"] for l in lines)
+    assert all(abs(l["parallel_efficiency"] - l["samples_per_s"] / 2000.0) < 1e-9 for l in lines)
+
+
 def test_cli_single_process_prints_reference_lines():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "dataParallelTraining_NN_MPI.py")],
                        capture_output=True, text=True, timeout=300)
