@@ -10,34 +10,55 @@ short rank only leaves a partial last tile; a LONG rank (8192 + 1 rows) would ad
 row of GEMM tiles on that rank and, since the step time is the max over ranks, slow every rank
 down.  Gradients are all-reduced over RCCL (xGMI) every step.
 
+Launch (the reference: ``mpiexec -n N python ...``, README.md:12, ref.py:61-63):
+
+    python bench.py --gpus N [--steps K] [--warmup W]     # spawns N ranks itself
+    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+
+Without a launcher, ``--gpus N > 1`` starts N fresh rank processes (before anything touches
+the GPU in this one) and exits with the worst of their exit codes.  Under a launcher the
+launched world must equal ``--gpus``, and a GPU run needs one visible device per local rank:
+anything else exits non-zero instead of measuring a different job.
+
 Gradient-sync schedule (``--comm_mode``, default auto): for latency-bound gradient volumes the
-fastest schedule depends on the node's collective latency, so the three candidates (one inline
+fastest schedule depends on the node's collective latency, so the candidates (one inline
 all-reduce; ZeRO-1 reduce-scatter + sharded SGD + bf16 all-gather; per-bucket all-reduce on a
 comm stream overlapped with backward) are each timed for ``--tune_steps`` steps BEFORE the timed
 region and the fastest (max over ranks, so every rank agrees) is kept; its time per candidate
-is reported in ``config.comm_tune_ms_per_step``.  Large gradients always overlap.
-
-    python bench.py [--gpus N] [--steps K] [--warmup W]
-    python -m torch.distributed.run --nproc-per-node N bench.py --gpus N ...
+is reported in ``config.comm_tune_ms_per_step``.  Large gradients always overlap, with a bf16
+payload (``--grad_dtype auto``).
 
 Rank 0 prints ONE JSON line.  The timed region is exactly K full training steps (forward,
 loss, backward, gradient all-reduce, optimizer update), bracketed by barrier + device sync on
-both sides; the reported time is the max over ranks.
+both sides; the reported time is the max over ranks.  AFTER the timed region (``--no_extras``
+skips it) the same ranks measure, each for min(K, 50) steps: the step with the gradient sync
+switched off (= the single-GPU step of the same shard: parallel efficiency, exposed comm), the
+step's collectives alone (bus GB/s, overlap %), and the step at a fixed global batch equal to
+the 1-GPU dataset (8192 rows for the proxy: strong scaling, the reference's own scaling mode,
+BASELINE.md:36-39).
+
+``--device cpu`` runs the same job on the CPU/gloo path (BASELINE config 1 plumbing): the
+multi-rank logic of this script is tested that way without a GPU.
 """
 from __future__ import annotations
 
 import argparse
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
-sys.path.insert(0, os.path.dirname(os.path.abspath(__file__)))
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, ROOT)
 
-# Reference numbers (BASELINE.md, reference algorithm on the 512-wide proxy, CPU, samples/s)
+# Reference numbers (BASELINE.md, reference algorithm on the 512-wide proxy, CPU, samples/s;
+# strong scaling of a fixed 8192-row dataset)
 BASELINE_SAMPLES_PER_S = {1: 32190.0, 2: 61546.0, 4: 88657.0, 8: 105377.0}
 # below this gradient volume the all-reduce is latency-bound: issue it inline (see parallel/sync.py)
 INLINE_MAX_GRAD_BYTES = 64 << 20
+EXTRA_STEPS = 50
 
 CONFIGS = {
     "proxy512": dict(widths=[512, 512, 512, 512, 1], loss="mse", rows=8192,
@@ -53,16 +74,21 @@ CONFIGS = {
 }
 
 
-def parse():
+def parse(argv=None):
     p = argparse.ArgumentParser()
-    p.add_argument("--gpus", type=int, default=1)
+    p.add_argument("--gpus", type=int, default=1,
+                   help="ranks (one per GPU); > 1 without a launcher: spawn them")
     p.add_argument("--steps", type=int, default=200)
     p.add_argument("--warmup", type=int, default=20)
     p.add_argument("--config", default="proxy512", choices=sorted(CONFIGS))
+    p.add_argument("--device", choices=["auto", "cuda", "cpu"], default="auto",
+                   help="cpu: the CPU/gloo plumbing path (no GPU)")
     p.add_argument("--rows", type=int, default=None, help="rows per GPU (weak scaling)")
     p.add_argument("--scaling", choices=["weak", "strong"], default="weak")
     p.add_argument("--dtype", choices=["bf16", "fp32"], default="bf16")
     p.add_argument("--comm", choices=["native", "torch"], default="native")
+    p.add_argument("--grad_dtype", choices=["auto", "fp32", "bf16"], default="auto",
+                   help="all-reduce payload (auto: bf16 above 64 MB of fp32 gradients)")
     p.add_argument("--bucket_mb", type=float, default=1.0)
     p.add_argument("--no_graph", action="store_true")
     p.add_argument("--no_overlap", action="store_true")
@@ -83,105 +109,205 @@ def parse():
                    help="steps per candidate timing in --comm_mode tune (untimed region)")
     p.add_argument("--force_comm", action="store_true",
                    help="use the RCCL gradient path even with one rank (smoke-tests comm overlap)")
+    p.add_argument("--no_extras", action="store_true",
+                   help="skip the post-timed-region efficiency / overlap / strong-scaling runs")
     p.add_argument("--fwd_variant", type=int, default=-1, help="forward GEMM variant (experiments)")
     p.add_argument("--group_async", type=int, default=-1,
                    help="grouped-backward LDS read mode (experiments)")
-    return p.parse_args()
+    return p.parse_args(argv)
 
 
-def main():
-    a = parse()
+def _free_port() -> int:
+    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+        s.bind(("127.0.0.1", 0))
+        return s.getsockname()[1]
+
+
+def _fail(msg: str, code: int = 2):
+    print(f"[bench] error: {msg}", file=sys.stderr, flush=True)
+    sys.exit(code)
+
+
+def launch_ranks(a, argv) -> int:
+    """Start ``--gpus`` rank processes of this script (nothing in this process has touched the
+    GPU: ``device_count()`` does not initialise HIP) and return the worst exit code."""
+    n = a.gpus
+    if a.device != "cpu":
+        import torch
+        have = torch.cuda.device_count()
+        if have < n and not (a.device == "auto" and have == 0):
+            _fail(f"--gpus {n} needs {n} visible GPUs, this node shows {have}")
+        if a.device == "auto" and have == 0:
+            a.device = "cpu"
+    port = _free_port()
+    procs = []
+    for r in range(n):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(n), LOCAL_RANK=str(r),
+                   LOCAL_WORLD_SIZE=str(n), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   NNMPI_LAUNCHER="bench")
+        if a.device == "cpu":
+            env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // n)))
+        procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
+                                      env=env))
+    first_bad = 0
+    try:
+        pending = list(procs)
+        while pending:
+            for p in list(pending):
+                rc = p.poll()
+                if rc is None:
+                    continue
+                pending.remove(p)
+                if rc != 0 and not first_bad:
+                    first_bad = rc if rc > 0 else 1
+                    for q in pending:      # one rank failed: its peers cannot finish
+                        q.terminate()
+            time.sleep(0.05)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    return first_bad
+
+
+def main(argv=None):
+    argv = sys.argv[1:] if argv is None else argv
+    a = parse(argv)
+    import torch  # noqa: F401  (import only: does not initialise HIP)
+    import nnmpi_amd  # noqa: F401
+    from nnmpi_amd.parallel import dist as pdist
+
+    job = pdist.detect_job()
+    if job.launcher == "single" and a.gpus > 1:
+        sys.exit(launch_ranks(a, argv))
+    if job.world != a.gpus:
+        _fail(f"launched with {job.world} rank(s) but --gpus {a.gpus}: refusing to report a "
+              "different job")
+    if a.device == "auto":
+        a.device = "cuda" if torch.cuda.device_count() > 0 else "cpu"
+    if a.device == "cuda":
+        have = torch.cuda.device_count()
+        if have < job.local_world:
+            _fail(f"{job.local_world} local ranks need as many GPUs; {have} visible "
+                  "(one rank per GPU: RCCL refuses two ranks on one device)")
+    run(a, job)
+
+
+def run(a, job):
     import torch
     import torch.distributed as dist
-    import nnmpi_amd  # noqa: F401
     from nnmpi_amd.data import synth
     from nnmpi_amd.data.partition import partition_rows
     from nnmpi_amd.engine.arena import Arena
     from nnmpi_amd.engine.engine import MLPEngine
     from nnmpi_amd.engine.trainer import loss_scales
     from nnmpi_amd.models.mlp import MLPSpec, reference_init
-    from nnmpi_amd.ops.hip_ops import HipOps
     from nnmpi_amd.parallel import dist as pdist
     from nnmpi_amd.parallel.sync import NativeRcclSync, NoSync, ShardedSync, TorchDistSync
     from nnmpi_amd.utils.config import TrainConfig
-    from nnmpi_amd.utils.metrics import comm_volume
-    from nnmpi_amd import native
+    from nnmpi_amd.utils.metrics import comm_volume, scaling_report
 
-    job = pdist.detect_job()
     rank, world = job.rank, job.world
-    native.lib().set_fwd_variant(a.fwd_variant)
-    native.lib().set_group_async(a.group_async)
-    torch.cuda.set_device(job.local_rank % torch.cuda.device_count())
-    dev = torch.device("cuda", torch.cuda.current_device())
-    pg = pdist.ProcessGroupContext(job, 600.0, want_nccl=(a.comm == "torch" and world > 1))
+    gpu = a.device == "cuda"
+    if gpu:
+        from nnmpi_amd import native
+        native.lib().set_fwd_variant(a.fwd_variant)
+        native.lib().set_group_async(a.group_async)
+        torch.cuda.set_device(job.local_rank % torch.cuda.device_count())
+        dev = torch.device("cuda", torch.cuda.current_device())
+        from nnmpi_amd.ops.hip_ops import HipOps
+        make_ops = lambda: HipOps(dev)  # noqa: E731
+    else:
+        dev = torch.device("cpu")
+        from nnmpi_amd.ops.torch_ops import TorchOps
+        make_ops = lambda: TorchOps(dev)  # noqa: E731
+        a.comm = "torch"
+    pg = pdist.ProcessGroupContext(job, 600.0, want_nccl=(gpu and a.comm == "torch" and world > 1))
     c = CONFIGS[a.config]
     widths = c["widths"]
     spec = MLPSpec(tuple(widths), "relu", c["loss"])
-    rows_pg = a.rows or c["rows"]
-    if a.scaling == "weak":
-        n_global = rows_pg * world - (0 if (a.even or world == 1) else 1)
-    else:
-        n_global = rows_pg
-    part = partition_rows(n_global, world)
-    rows = part.rows(rank)
     if "dtype" in c:
         a.dtype = c["dtype"]
+    if not gpu:
+        a.dtype = "fp32"
     dtype = torch.bfloat16 if a.dtype == "bf16" else torch.float32
-
-    # data (device-generated, partition-independent rows)
-    if c["loss"] == "xent":
-        X, labels = synth.chunked_classification(part.start(rank), rows, widths[0], widths[-1],
-                                                 device=dev)
-        Y = None
-    else:
-        X, Y = synth.chunked_regression(part.start(rank), rows, widths[0], device=dev)
-        labels = None
-    # model: same seed everywhere + broadcast from rank 0 (reference ref.py:87)
+    rows_pg = a.rows or c["rows"]
+    grad_bytes = spec.n_params * 4
+    grad_dtype = a.grad_dtype
+    if grad_dtype == "auto":
+        grad_dtype = "bf16" if (gpu and grad_bytes > INLINE_MAX_GRAD_BYTES) else "fp32"
     big = spec.n_params > 20_000_000
-    use_comm = (world > 1 or a.force_comm)
-    cfg = TrainConfig(widths=list(widths), loss=c["loss"], n_features=widths[0])
-    inv, lsc, gsc = loss_scales(cfg, rows, list(part.counts), widths[-1])
+    use_comm = (world > 1 or (a.force_comm and gpu))
     native_comm = None
-    if use_comm and a.comm == "native":
+    if use_comm and gpu and a.comm == "native":
         lib = native.lib()
         uid = pg.broadcast_object(lib.rccl_unique_id() if rank == 0 else None, 0)
         native_comm = native.make_comm(uid, world, rank, dev.index)
+    comm_group = pg.nccl if (gpu and pg.nccl is not None) else pg.gloo
 
-    def build(mode):
-        """One arena + gradient-sync strategy + engine.  mode: inline | overlap | zero1."""
-        model = reference_init(widths, "relu", seed=0, device=dev if big else None)
+    def shard(n_global):
+        part = partition_rows(n_global, world)
+        rows = part.rows(rank)
+        if c["loss"] == "xent":
+            X, labels = synth.chunked_classification(part.start(rank), rows, widths[0], widths[-1],
+                                                     device=dev)
+            Y = None
+        else:
+            X, Y = synth.chunked_regression(part.start(rank), rows, widths[0], device=dev)
+            labels = None
+        return part, X.to(dtype), Y, labels
+
+    def build(mode, data, comm=True):
+        """One arena + gradient-sync strategy + engine over ``data`` (a shard()).
+        mode: inline | overlap | zero1 | none (no gradient synchronisation at all)."""
+        part, X, Y, labels = data
+        rows = part.rows(rank)
+        model = reference_init(widths, "relu", seed=0, device=dev if (big and gpu) else None)
+        zero1 = mode == "zero1" and comm
         arena = Arena([spec.layer_shape(i) for i in range(spec.n_layers)], dev,
                       shadow_dtype=torch.bfloat16 if dtype == torch.bfloat16 else None,
-                      bucket_bytes=a.bucket_mb * 2 ** 20,
-                      pad_to=64 * world if mode == "zero1" else 64)
+                      bucket_bytes=a.bucket_mb * 2 ** 20, pad_to=64 * world if zero1 else 64)
         arena.bind_model(model)
         del model
-        if native_comm is not None:
+        if not comm or not use_comm:
+            sync = NoSync(arena)
+        elif native_comm is not None:
             s = torch.cuda.current_stream()
             native_comm.broadcast(arena.master.data_ptr(), arena.numel, 0, 0, int(s.cuda_stream))
             s.synchronize()
             arena.sync_shadow()
-            if mode == "zero1":
+            if zero1:
                 sync = ShardedSync(arena, world, rank, native_comm=native_comm)
             else:
-                sync = NativeRcclSync(arena, native_comm, world, inline=(mode == "inline"))
-        elif world > 1:
-            dist.broadcast(arena.master, src=0, group=pg.nccl)
-            arena.sync_shadow()
-            sync = TorchDistSync(arena, pg.nccl, world)
+                sync = NativeRcclSync(arena, native_comm, world, inline=(mode == "inline"),
+                                      grad_dtype=grad_dtype)
         else:
-            sync = NoSync(arena)
-        eng = MLPEngine(spec, arena, HipOps(dev), sync, device=dev, dtype=dtype,
-                        rows_capacity=rows, lr=a.lr, momentum=0.9, use_graph=not a.no_graph,
-                        overlap=not a.no_overlap, grouped=not a.no_group)
-        eng.load_batch(Xc, Y, labels)
-        eng.set_scales(inv, lsc, gsc)
+            dist.broadcast(arena.master, src=0, group=comm_group)
+            arena.sync_shadow()
+            sync = (ShardedSync(arena, world, rank, group=comm_group) if zero1 else
+                    TorchDistSync(arena, comm_group, world, grad_dtype=grad_dtype))
+        eng = MLPEngine(spec, arena, make_ops(), sync, device=dev, dtype=dtype,
+                        rows_capacity=max(rows, 1), lr=a.lr, momentum=0.9,
+                        use_graph=not a.no_graph, overlap=not a.no_overlap,
+                        grouped=not a.no_group)
+        eng.load_batch(X, Y, labels)
+        cfg = TrainConfig(widths=list(widths), loss=c["loss"], n_features=widths[0], device="cpu")
+        eng.set_scales(*loss_scales(cfg, rows, list(part.counts), widths[-1]))
         return eng
 
     def barrier():
-        torch.cuda.synchronize()
+        if gpu:
+            torch.cuda.synchronize()
         pg.barrier()
-        torch.cuda.synchronize()
+        if gpu:
+            torch.cuda.synchronize()
+
+    def max_over_ranks(x: float) -> float:
+        if world > 1:
+            t = torch.tensor([x], dtype=torch.float64)
+            pg.allreduce_cpu(t, op=dist.ReduceOp.MAX)
+            x = float(t.item())
+        return x
 
     def timed(eng, n, chunk):
         """Wall time of n steps, max over ranks (graphs captured beforehand)."""
@@ -190,33 +316,34 @@ def main():
         t0 = time.perf_counter()
         eng.run_steps(n, chunk)
         eng.synchronize()
-        torch.cuda.synchronize()
+        if gpu:
+            torch.cuda.synchronize()
         el = time.perf_counter() - t0
         pg.barrier()
-        if world > 1:
-            t = torch.tensor([el], dtype=torch.float64)
-            pg.allreduce_cpu(t, op=dist.ReduceOp.MAX)
-            el = float(t.item())
-        return el
+        return max_over_ranks(el)
 
-    Xc = X.to(dtype)
-    del X
     chunk = max(1, a.graph_chunk)
-    grad_bytes = spec.n_params * 4
+    if a.scaling == "weak":
+        n_global = rows_pg * world - (0 if (a.even or world == 1) else 1)
+    else:
+        n_global = rows_pg
+    data = shard(n_global)
     mode = a.comm_mode
     if mode == "auto":
         # small (latency-bound) gradients: the best collective schedule depends on the link
         # latency of the node, so it is measured (untimed, before the timed region) rather than
         # assumed; large gradients always overlap per-bucket all-reduces with the backward.
         mode = "tune" if grad_bytes <= INLINE_MAX_GRAD_BYTES else "overlap"
-    if native_comm is None:
-        mode = "inline" if use_comm else "none"
+    if not use_comm:
+        mode = "none"
+    elif native_comm is None and mode == "tune":
+        mode = "inline"
     tune = None
     if mode == "tune":
         tune = {}
         eng = None
         for m in ("inline", "zero1", "overlap"):
-            e = build(m)
+            e = build(m, data)
             e.run_steps(a.warmup, chunk)
             tm = min(timed(e, a.tune_steps, chunk) for _ in range(2))
             tune[m] = round(tm / a.tune_steps * 1e3, 5)
@@ -224,13 +351,13 @@ def main():
             if eng is None or tm < best_t:
                 eng, best_t, mode = e, tm, m
             del e
-        torch.cuda.empty_cache()
+        if gpu:
+            torch.cuda.empty_cache()
     else:
-        eng = build(mode)
+        eng = build(mode, data)
         eng.run_steps(a.warmup, chunk)
-    sync = eng.sync
-    del Xc
 
+    # ---------------- the timed region: exactly K steps -------------------------------------
     # graph mode: steps replayed as hipGraphs of `chunk` complete consecutive steps (one
     # replay's fixed cost per chunk); every graph is captured before the timed region
     eng.prepare_steps(a.steps, chunk)
@@ -239,20 +366,73 @@ def main():
     t0 = time.perf_counter()
     eng.run_steps(a.steps, chunk)
     eng.synchronize()
-    torch.cuda.synchronize()
+    if gpu:
+        torch.cuda.synchronize()
     t1 = time.perf_counter()
     pg.barrier()
-    elapsed = t1 - t0
-    if world > 1:
-        el = torch.tensor([elapsed], dtype=torch.float64)
-        pg.allreduce_cpu(el, op=dist.ReduceOp.MAX)
-        elapsed = float(el.item())
+    elapsed = max_over_ranks(t1 - t0)
     loss = eng.loss()
     ms = elapsed / a.steps * 1e3
-    samples = n_global
-    value = samples * a.steps / elapsed
+    value = n_global * a.steps / elapsed
+    sharded = mode == "zero1"
+    wire = comm_volume(eng.arena.numel, world, grad_dtype, sharded=sharded,
+                       shadow=eng.arena.shadow is not None)["wire_bytes_per_rank"]
+
+    # ---------------- after the timed region: what the BASELINE metric derives from it ----------
+    extras = {}
+    strong = None
+    if not a.no_extras:
+        n_ex = max(1, min(a.steps, EXTRA_STEPS))
+        comm_ms = None
+        if use_comm:
+            # the step's collectives alone (same buckets / dtype / order), replayed like the step
+            sync = eng.sync
+            with torch.no_grad():
+                eng.arena.grad.zero_()
+            if gpu:
+                torch.cuda.synchronize()
+            comm_ms = _time_comm_only(sync, n_ex, chunk, gpu and not a.no_graph, barrier,
+                                      max_over_ranks) * 1e3
+            with torch.no_grad():
+                eng.arena.grad.zero_()
+        rows_local = data[0].rows(rank)
+        del eng
+        if gpu:
+            torch.cuda.empty_cache()
+        if use_comm:
+            # the same per-rank work with the gradient sync off: every rank alone (1-GPU step)
+            e = build("none", data, comm=False)
+            e.run_steps(min(a.warmup, 10) + 1, chunk)
+            comp_ms = timed(e, n_ex, chunk) / n_ex * 1e3
+            del e
+        else:
+            comp_ms = ms
+        extras = scaling_report(world, max(data[0].counts), n_global, ms, comp_ms, comm_ms, wire)
+        extras["single_gpu_ms_per_step"] = comp_ms
+        del data
+        if world > 1 and a.scaling == "weak":
+            # strong scaling: the reference's fixed dataset (the 1-GPU shard, 8192 rows for the
+            # proxy) split over the N ranks
+            sdata = shard(rows_pg)
+            e = build(mode if mode != "none" else "inline", sdata)
+            e.run_steps(min(a.warmup, 10) + 1, chunk)
+            s_ms = timed(e, n_ex, chunk) / n_ex * 1e3
+            del e, sdata
+            # S(1): the single-GPU step of the whole dataset = the compute-only step above
+            # (weak scaling gives every rank rows_pg rows, the last one rows_pg - 1)
+            strong = {"global_batch": rows_pg, "ms_per_step": round(s_ms, 5),
+                      "samples_per_s": round(rows_pg / (s_ms * 1e-3), 1),
+                      "parallel_efficiency": round(comp_ms / (world * s_ms), 4)}
+            base = BASELINE_SAMPLES_PER_S.get(world) if a.config == "proxy512" else None
+            strong["vs_baseline"] = round(strong["samples_per_s"] / base, 2) if base else None
+        if gpu:
+            torch.cuda.empty_cache()
+
     base = BASELINE_SAMPLES_PER_S.get(world) if a.config == "proxy512" else None
-    tflops = spec.flops_per_sample() * samples / (ms * 1e-3) / 1e12
+    tflops = spec.flops_per_sample() * n_global / (ms * 1e-3) / 1e12
+
+    def rnd(x, k=4):
+        return None if x is None else round(float(x), k)
     if rank == 0:
         out = {
             "metric": "samples_per_sec_whole_node",
@@ -267,25 +447,79 @@ def main():
             "vs_baseline": (round(value / base, 2) if base else None),
             "dtype": a.dtype,
             "data": "synthetic (device-generated make_regression-style rows), random init",
-            "config": {"model": c["model"], "global_batch": samples, "seq_len": None,
+            "config": {"model": c["model"], "global_batch": n_global, "seq_len": None,
                        "parallelism": f"dp{world}", "rows_per_gpu": rows_pg,
-                       "uneven_split": (not a.even and world > 1),
-                       "comm": a.comm if (world > 1 or a.force_comm) else "none",
-                       "graph": not a.no_graph, "graph_chunk": a.graph_chunk, "overlap": not a.no_overlap,
-                       "grouped": not a.no_group,
+                       "uneven_split": (not a.even and world > 1 and a.scaling == "weak"),
+                       "device": a.device,
+                       "comm": (("rccl" if native_comm is not None else
+                                 ("nccl" if pg.nccl is not None else "gloo"))
+                                if use_comm else "none"),
+                       "graph": gpu and not a.no_graph, "graph_chunk": a.graph_chunk,
+                       "overlap": not a.no_overlap, "grouped": not a.no_group,
                        "comm_mode": mode if use_comm else None,
                        "comm_tune_ms_per_step": tune,
-                       "grad_wire_bytes_per_rank": comm_volume(
-                           eng.arena.numel, world, sharded=(mode == "zero1"),
-                           shadow=eng.arena.shadow is not None)["wire_bytes_per_rank"],
+                       "grad_dtype": grad_dtype if use_comm else None,
+                       "grad_wire_bytes_per_rank": wire,
                        "bucket_mb": a.bucket_mb},
+            "rccl_ranks": (native_comm.size if native_comm is not None else None),
             "model_tflops_per_s": round(tflops, 2),
+            "parallel_efficiency": rnd(extras.get("parallel_efficiency")),
+            "single_gpu_samples_per_s": rnd(extras.get("single_gpu_samples_per_s"), 1),
+            "single_gpu_ms_per_step": rnd(extras.get("single_gpu_ms_per_step"), 5),
+            "exposed_comm_ms": rnd(extras.get("exposed_comm_ms"), 5),
+            "comm_only_ms": rnd(extras.get("comm_only_ms"), 5),
+            "overlap_pct": rnd(extras.get("overlap_pct"), 1),
+            "comm_bus_gbps": rnd(extras.get("comm_bus_gbps"), 2),
+            "strong_scaling": strong,
             "loss_after_warmup": loss0,
             "final_loss": loss,
         }
         print(json.dumps(out), flush=True)
     native_comm = None
     pg.destroy()
+
+
+def _time_comm_only(sync, n, chunk, use_graph, barrier, max_over_ranks) -> float:
+    """Seconds per repetition of the step's collectives alone (max over ranks)."""
+    import torch
+    if use_graph:
+        from nnmpi_amd import native
+        s = torch.cuda.Stream()
+        graphs = []
+        reps = min(chunk, n)
+        with torch.cuda.stream(s):
+            sync.comm_only()           # warm (RCCL lazily sets up its channels on first use)
+            s.synchronize()
+            g = native.lib().GraphRunner()
+            g.begin(int(s.cuda_stream))
+            try:
+                for _ in range(reps):
+                    sync.comm_only()
+            except Exception:
+                g.cancel()
+                raise
+            g.end()
+            graphs.append(g)
+        n_launch = max(1, n // reps)
+        barrier()
+        t0 = time.perf_counter()
+        with torch.cuda.stream(s):
+            for _ in range(n_launch):
+                g.launch(int(s.cuda_stream))
+        s.synchronize()
+        el = time.perf_counter() - t0
+        return max_over_ranks(el) / (n_launch * reps)
+    sync.comm_only()
+    if torch.cuda.is_available() and getattr(sync.arena.grad, "is_cuda", False):
+        torch.cuda.synchronize()
+    barrier()
+    t0 = time.perf_counter()
+    for _ in range(n):
+        sync.comm_only()
+    if getattr(sync.arena.grad, "is_cuda", False):
+        torch.cuda.synchronize()
+    el = time.perf_counter() - t0
+    return max_over_ranks(el) / n
 
 
 if __name__ == "__main__":

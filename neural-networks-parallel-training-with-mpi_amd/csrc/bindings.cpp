@@ -297,6 +297,11 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
                           std::vector<long long> displs, uptr rb, int dt, int root, uptr s) {
         c.scatterv(P<const void>(sb), counts, displs, P<void>(rb), dt, root, S(s));
       })
+      .def("broadcast_pieces", [](RcclComm& c, uptr base, std::vector<long long> offsets,
+                                  std::vector<long long> counts, std::vector<int> roots, int dt,
+                                  uptr s) {
+        c.broadcast_pieces(P<void>(base), offsets, counts, roots, dt, S(s));
+      })
       .def("poll_error", &RcclComm::poll_error, py::arg("abort_on_error") = true)
       .def("abort", &RcclComm::abort);
   py::class_<GradSync>(m, "GradSync")
@@ -311,6 +316,7 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
       .def(py::init<>())
       .def("begin", [](GraphRunner& g, uptr s) { g.begin(S(s)); })
       .def("end", &GraphRunner::end)
+      .def("cancel", &GraphRunner::cancel)
       .def("launch", [](GraphRunner& g, uptr s) { g.launch(S(s)); })
       .def_property_readonly("ready", &GraphRunner::ready)
       .def_property_readonly("num_nodes", &GraphRunner::num_nodes);

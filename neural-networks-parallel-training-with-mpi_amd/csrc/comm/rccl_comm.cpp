@@ -122,9 +122,30 @@ void RcclComm::scatterv(const void* sendbuf, const std::vector<long long>& count
 int RcclComm::poll_error(bool abort_on_error) {
   if (aborted_) return (int)ncclInvalidUsage;
   ncclResult_t r = ncclSuccess;
-  ncclCommGetAsyncError(comm_, &r);
+  // the query itself can fail (e.g. a communicator torn down underneath us): that is an error
+  // of the communicator too, never "healthy"
+  const ncclResult_t q = ncclCommGetAsyncError(comm_, &r);
+  if (q != ncclSuccess) r = q;
   if (r != ncclSuccess && r != ncclInProgress && abort_on_error) abort();
   return r == ncclInProgress ? 0 : (int)r;
+}
+
+void RcclComm::broadcast_pieces(void* base, const std::vector<long long>& offsets,
+                                const std::vector<long long>& counts,
+                                const std::vector<int>& roots, int dtype, hipStream_t s) {
+  if (offsets.size() != counts.size() || offsets.size() != roots.size())
+    throw std::runtime_error("broadcast_pieces: offsets/counts/roots differ in length");
+  if (offsets.empty()) return;
+  const size_t es = dtype_size(dtype);
+  const ncclDataType_t dt = to_nccl(dtype);
+  NCCL_THROW(ncclGroupStart());
+  for (size_t i = 0; i < offsets.size(); ++i) {
+    if (counts[i] <= 0) continue;
+    if (roots[i] < 0 || roots[i] >= nranks_) throw std::runtime_error("broadcast_pieces: bad root");
+    char* p = static_cast<char*>(base) + offsets[i] * es;
+    NCCL_THROW(ncclBroadcast(p, p, counts[i], dt, roots[i], comm_, s));
+  }
+  NCCL_THROW(ncclGroupEnd());
 }
 
 void RcclComm::abort() {
@@ -174,8 +195,33 @@ void GraphRunner::begin(hipStream_t s) {
 }
 
 void GraphRunner::end() {
-  HIP_THROW(hipStreamEndCapture(cap_, &graph_));
+  const hipError_t e = hipStreamEndCapture(cap_, &graph_);
+  cap_ = nullptr;
+  if (e != hipSuccess) {
+    if (graph_) { (void)hipGraphDestroy(graph_); graph_ = nullptr; }
+    (void)hipGetLastError();
+    throw std::runtime_error(std::string("HIP error: ") + hipGetErrorString(e) +
+                             " at hipStreamEndCapture");
+  }
   HIP_THROW(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
+}
+
+void GraphRunner::cancel() {
+  // A throw while the stream was capturing (a collective refused, a shape check): end the
+  // capture and drop the partial graph, so the stream is usable again and no half-captured
+  // work is ever replayed.
+  if (cap_) {
+    hipStreamCaptureStatus st = hipStreamCaptureStatusNone;
+    if (hipStreamIsCapturing(cap_, &st) == hipSuccess && st != hipStreamCaptureStatusNone) {
+      hipGraph_t g = nullptr;
+      (void)hipStreamEndCapture(cap_, &g);
+      if (g) (void)hipGraphDestroy(g);
+    }
+    cap_ = nullptr;
+  }
+  if (exec_) { (void)hipGraphExecDestroy(exec_); exec_ = nullptr; }
+  if (graph_) { (void)hipGraphDestroy(graph_); graph_ = nullptr; }
+  (void)hipGetLastError();
 }
 
 void GraphRunner::launch(hipStream_t s) {

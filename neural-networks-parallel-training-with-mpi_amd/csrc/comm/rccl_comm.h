@@ -44,6 +44,11 @@ class RcclComm {
   // (in place when recvbuf == sendbuf + r*recvcount)
   void reduce_scatter(const void* sendbuf, void* recvbuf, size_t recvcount, int dtype, int op,
                       hipStream_t s);
+  // grouped in-place ncclBroadcast of pieces [base + offsets[i], + counts[i]) from roots[i]
+  // (the sharded optimizer's fp32 refresh of the regions the kernels read from the master)
+  void broadcast_pieces(void* base, const std::vector<long long>& offsets,
+                        const std::vector<long long>& counts, const std::vector<int>& roots,
+                        int dtype, hipStream_t s);
   // Returns the RCCL async error code (0 = ok); aborts the communicator on error if asked.
   int poll_error(bool abort_on_error);
   void abort();
@@ -80,6 +85,8 @@ class GraphRunner {
   void begin(hipStream_t s);
   void end();
   void launch(hipStream_t s);
+  // abandon an in-progress capture (after a throw) and drop any partial graph
+  void cancel();
   bool ready() const { return exec_ != nullptr; }
   size_t num_nodes() const;
 

@@ -138,7 +138,10 @@ class MLPEngine:
 
     # ------------------------------------------------------------------------------------
     def set_hparams(self, lr=None, momentum=None, grad_scale=None):
-        with torch.no_grad():
+        # written on the engine's stream: the kernels that read hp (SGD, fused combines) run
+        # there, so the write is ordered before the next step and after the previous one
+        ctx = torch.cuda.stream(self.stream) if self.is_cuda else _nullctx()
+        with ctx, torch.no_grad():
             if lr is not None:
                 self.hp[0] = lr
             if momentum is not None:
@@ -252,15 +255,19 @@ class MLPEngine:
 
     def _step_body(self, first: bool):
         self._mark("start")
-        if self.overlap:
+        if self.overlap and self.rows > 0:
             self._step_body_overlap(first)
         else:
+            # sequential schedule; also every empty batch (a short shard's empty mini-batch, a
+            # rank without rows): forward_backward zeroes the gradient and still issues every
+            # bucket's collective in backward order, so this rank joins the same collective
+            # sequence as its peers, whatever schedule they run
             self._first = first
             self.sync.begin()
             self.forward_backward()
             self.sync.finish()
             self._mark("comm")
-            if not self.tiny_fused:
+            if not self.tiny_fused or self.rows == 0:
                 self._update(first)
         self._mark("update")
 
@@ -507,10 +514,7 @@ class MLPEngine:
             for _ in range(nsteps):
                 self._step_body(False)
         except Exception:
-            try:
-                g.end()
-            except Exception:
-                pass
+            g.cancel()    # leave the stream out of capture mode, drop the partial graph
             raise
         g.end()
         return g

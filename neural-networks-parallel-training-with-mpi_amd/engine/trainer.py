@@ -32,7 +32,7 @@ from ..models.mlp import MLP, MLPSpec, reference_init
 from ..parallel import dist as pdist
 from ..parallel.sync import NativeRcclSync, NoSync, ShardedSync, TorchDistSync
 from ..utils import checkpoint as ckpt
-from ..utils.config import TrainConfig, config_from_args
+from ..utils.config import TrainConfig, config_from_args, resolve_device
 from ..utils.metrics import MetricsWriter, comm_bus_gbps, comm_volume, parallel_efficiency
 from ..utils.seqcheck import SequenceChecker
 from ..utils.watchdog import Watchdog
@@ -82,7 +82,7 @@ class Job:
         self.job = pdist.detect_job()
         self.rank, self.world = self.job.rank, self.job.world
         self.device = torch.device("cpu")
-        if cfg.device == "cuda":
+        if resolve_device(cfg.device) == "cuda":
             if not torch.cuda.is_available():
                 raise RuntimeError("--device cuda requested but no GPU is visible")
             ndev = torch.cuda.device_count()
@@ -246,7 +246,8 @@ def make_sync(j: Job, arena: Arena):
                   (cfg.comm_mode == "auto" and arena.numel * 4 <= INLINE_MAX_GRAD_BYTES))
         return NativeRcclSync(arena, j.native_comm, j.world, inline=inline,
                               grad_dtype=cfg.grad_dtype, mode=cfg.sync)
-    group = j.pg.nccl if (j.device.type == "cuda" and j.pg.nccl is not None) else j.pg.gloo
+    group = (j.pg.nccl if (j.device.type == "cuda" and j.pg.nccl is not None
+                           and j.comm_kind != "gloo") else j.pg.gloo)
     return TorchDistSync(arena, group, j.world, mode=cfg.sync, overlap=cfg.overlap,
                          grad_dtype=cfg.grad_dtype)
 
@@ -275,6 +276,17 @@ def _gather_state(eng, sync):
     if getattr(sync, "sharded", False):
         eng.synchronize()
         sync.gather_state()
+
+
+def _fault_injection(rank: int) -> Optional[int]:
+    """``NNMPI_FAULT_INJECT=<rank>:<epoch>``: that rank raises at the start of that epoch while
+    its peers are blocked in the step's collectives -- the reference's deadlock scenario
+    (ref.py:185,203), used by the failure-detection test."""
+    spec = os.environ.get("NNMPI_FAULT_INJECT")
+    if not spec:
+        return None
+    r, e = spec.split(":")
+    return int(e) if int(r) == rank else None
 
 
 def _print(cfg: TrainConfig, rank: int, msg: str):
@@ -350,8 +362,11 @@ def _run(j: Job) -> TrainResult:
         return max(0, min(mb, c - m * mb))
     gen = torch.Generator(device="cpu")
     full_loaded = False
+    fault = _fault_injection(rank)
     try:
         for epoch in range(start_epoch, cfg.nepochs):
+            if fault is not None and epoch == fault:
+                raise RuntimeError(f"injected fault on rank {rank} at epoch {epoch}")
             _print(cfg, rank, "[ = = = = = Epoch {} = = = = = ]".format(epoch))
             t0 = time.perf_counter()
             if bs and cfg.shuffle:

@@ -60,6 +60,24 @@ def _free_port() -> int:
         return s.getsockname()[1]
 
 
+class _stdout_to_stderr:
+    """fd-level redirect of stdout to stderr: gloo's C++ rendezvous prints "[Gloo] Rank r is
+    connected to ..." on stdout, which would interleave with the reference's log lines and break
+    one-JSON-line stdout contracts (bench.py)."""
+
+    def __enter__(self):
+        sys.stdout.flush()
+        self._saved = os.dup(1)
+        os.dup2(2, 1)
+        return self
+
+    def __exit__(self, *exc):
+        sys.stdout.flush()
+        os.dup2(self._saved, 1)
+        os.close(self._saved)
+        return False
+
+
 class ProcessGroupContext:
     """Owns the gloo control-plane group (and optionally a torch nccl group)."""
 
@@ -80,12 +98,15 @@ class ProcessGroupContext:
             else:
                 key = env.get("NNMPI_RDZV_KEY", str(os.getppid()))
                 init = f"file:///tmp/nnmpi_rdzv_{key}"
-            dist.init_process_group("gloo", init_method=init, rank=job.rank,
-                                    world_size=job.world, timeout=timeout)
+            with _stdout_to_stderr():
+                dist.init_process_group("gloo", init_method=init, rank=job.rank,
+                                        world_size=job.world, timeout=timeout)
             self.owned = True
-        self.gloo = dist.group.WORLD if dist.get_backend() == "gloo" else dist.new_group(backend="gloo")
-        if want_nccl:
-            self.nccl = dist.new_group(backend="nccl", timeout=timeout)
+        with _stdout_to_stderr():
+            self.gloo = (dist.group.WORLD if dist.get_backend() == "gloo"
+                         else dist.new_group(backend="gloo"))
+            if want_nccl:
+                self.nccl = dist.new_group(backend="nccl", timeout=timeout)
 
     def barrier(self):
         if self.gloo is not None:

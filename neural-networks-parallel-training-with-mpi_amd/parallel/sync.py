@@ -62,6 +62,11 @@ class GradSync:
     def finish(self):
         pass
 
+    def comm_only(self):
+        """Issue exactly the collectives of one step's gradient synchronisation on the current
+        stream, with no compute around them (the bench's comm-only timing: achieved bus
+        bandwidth and how much of the communication the overlapped step hides)."""
+
 
 class NoSync(GradSync):
     world = 1
@@ -99,6 +104,15 @@ class TorchDistSync(GradSync):
         w = dist.all_reduce(view, group=self.group, async_op=self.overlap)
         if w is not None:
             self._works.append(w)
+
+    def comm_only(self):
+        for b in self.arena.buckets:
+            view = self.arena.grad[b.offset:b.offset + b.numel]
+            if self.mode == "root":
+                dist.reduce(view, dst=0, group=self.group)
+                dist.broadcast(view, src=0, group=self.group)
+            else:
+                dist.all_reduce(view, group=self.group)
 
     def finish(self):
         for w in self._works:
@@ -167,6 +181,23 @@ class NativeRcclSync(GradSync):
         self._launch(bucket, stream)
         return None if self.inline else self._comm_stream
 
+    def comm_only(self):
+        h = self.native.stream_handle()
+        lib = self.native.lib()
+        for b in self.arena.buckets:
+            view = self.arena.grad[b.offset:b.offset + b.numel]
+            ptr, dt = view.data_ptr(), 0
+            if self.bf16:
+                ptr, dt = self.gbuf[b.offset:].data_ptr(), 1
+                lib.cast_f32_bf16(view.data_ptr(), ptr, b.numel, h)
+            if self.mode == "root":
+                self.comm.reduce(ptr, b.numel, dt, 0, 0, h)
+                self.comm.broadcast(ptr, b.numel, dt, 0, h)
+            else:
+                self.comm.allreduce(ptr, b.numel, dt, 0, h)
+            if self.bf16:
+                lib.cast_bf16_f32(ptr, view.data_ptr(), b.numel, h)
+
     def finish(self):
         if self._launched:
             self.gs.join(self.native.stream_handle())
@@ -186,11 +217,15 @@ class ShardedSync(GradSync):
     2. only the owner applies SGD-momentum to its slice (1/P folded in, as usual), so the
        momentum of the other slices is never read or written;
     3. the updated parameters are all-gathered: the bf16 compute shadow when there is one (half
-       the bytes of fp32; the fp32 master of foreign slices then goes stale until
-       :meth:`gather_state`), else the fp32 master.
+       the bytes of fp32), else the fp32 master.  With a shadow, the fp32 master is still read
+       by the kernels in a few places -- every bias (forward epilogue) and the whole output
+       layer (head) -- so those regions are refreshed in fp32 as well: one grouped in-place
+       ncclBroadcast of each region's pieces from their owners (:meth:`_master_pieces`; a few
+       KB).  The rest of the master of foreign slices is never read until
+       :meth:`gather_state`.
 
-    Bytes on the wire per step: reduce-scatter fp32 + all-gather bf16 = 3/4 of an fp32
-    all-reduce.  :meth:`gather_state` re-assembles the full fp32 master and momentum (collective:
+    Bytes on the wire per step: reduce-scatter fp32 + all-gather bf16 (+ the fp32 bias/head
+    pieces) ~= 3/4 of an fp32 all-reduce.  :meth:`gather_state` re-assembles the full fp32 master and momentum (collective:
     every rank calls it) before checkpoints and the final state_dict.
     """
     sharded = True
@@ -208,6 +243,28 @@ class ShardedSync(GradSync):
         if native_comm is not None:
             from .. import native
             self.native = native
+        self.pieces = self._master_pieces()
+
+    def _master_pieces(self):
+        """(offsets, counts, roots) of the fp32-master regions the kernels read besides the
+        bf16 shadow -- the output layer's weight + bias and every hidden bias -- cut at the
+        shard boundaries, each piece owned (and broadcast) by the rank whose slice holds it."""
+        ar = self.arena
+        last = ar.n_layers - 1
+        regions = [ar.layer_range[last]]
+        for li in range(last):
+            sl = ar.by_name[f"layers.{2 * li}.bias"]
+            regions.append((sl.offset, sl.offset + sl.numel))
+        offs, cnts, roots = [], [], []
+        for s, e in regions:
+            while s < e:
+                r = s // self.shard
+                cut = min(e, (r + 1) * self.shard)
+                offs.append(s)
+                cnts.append(cut - s)
+                roots.append(r)
+                s = cut
+        return offs, cnts, roots
 
     def ready(self, layer: int):
         pass   # nothing moves until the whole gradient exists
@@ -233,6 +290,8 @@ class ShardedSync(GradSync):
             if ar.shadow is not None:
                 s = ar.shadow.data_ptr()
                 self.comm.allgather(s + 2 * self.off, s, self.shard, 1, h)
+                offs, cnts, roots = self.pieces
+                self.comm.broadcast_pieces(ar.master.data_ptr(), offs, cnts, roots, 0, h)
             else:
                 m = ar.master.data_ptr()
                 self.comm.allgather(m + 4 * self.off, m, self.shard, 0, h)
@@ -241,6 +300,25 @@ class ShardedSync(GradSync):
                             ar.master[self.off:self.off + self.shard].clone(), group=self.group)
             if ar.shadow is not None:
                 ar.shadow.copy_(ar.master)
+
+    def comm_only(self):
+        ar = self.arena
+        if self.comm is None:
+            dist.all_reduce(ar.grad, group=self.group)
+            dist.all_gather(self._views(ar.master),
+                            ar.master[self.off:self.off + self.shard].clone(), group=self.group)
+            return
+        h = self.native.stream_handle()
+        g = ar.grad.data_ptr()
+        self.comm.reduce_scatter(g, g + 4 * self.off, self.shard, 0, 0, h)
+        if ar.shadow is not None:
+            s = ar.shadow.data_ptr()
+            self.comm.allgather(s + 2 * self.off, s, self.shard, 1, h)
+            offs, cnts, roots = self.pieces
+            self.comm.broadcast_pieces(ar.master.data_ptr(), offs, cnts, roots, 0, h)
+        else:
+            m = ar.master.data_ptr()
+            self.comm.allgather(m + 4 * self.off, m, self.shard, 0, h)
 
     def gather_state(self):
         """Full fp32 master + momentum on every rank (checkpoint / final parameters)."""

@@ -66,8 +66,9 @@ class TrainConfig:
     grad_accum: int = 1               # micro-batches per optimizer step (gradient accumulation)
     # --- runtime ---
     seed: int = 0                     # init seed (reference: torch.manual_seed(0) on rank 0)
-    device: str = "cpu"               # cpu | cuda
-    comm: str = "auto"                # auto | torch | native | none
+    device: str = "auto"              # auto (cuda when a GPU is visible) | cpu | cuda
+    comm: str = "auto"                # auto | native (RCCL) | torch (torch.distributed) |
+                                      # gloo (gloo even for device tensors) | none
     sync: str = "allreduce"           # allreduce | root (reference-style reduce+bcast)
     comm_mode: str = "auto"           # auto | overlap (comm stream) | inline (compute stream)
     bucket_mb: float = 1.0
@@ -144,8 +145,13 @@ def build_parser() -> argparse.ArgumentParser:
                         "optimizer step (with the whole-shard batch the shard is cut into this "
                         "many micro-batches)")
     p.add_argument("--seed", type=int, default=0)
-    p.add_argument("--device", choices=["cpu", "cuda"], default="cpu")
-    p.add_argument("--comm", choices=["auto", "torch", "native", "none"], default="auto")
+    p.add_argument("--device", choices=["auto", "cpu", "cuda"], default="auto",
+                   help="auto: the MI355X (HIP kernels + RCCL) when a GPU is visible, else the "
+                        "CPU/gloo path")
+    p.add_argument("--comm", choices=["auto", "torch", "native", "gloo", "none"], default="auto",
+                   help="gradient transport: native = the C++ RCCL runtime (GPU default), torch = "
+                        "torch.distributed (nccl on GPU, gloo on CPU), gloo = gloo also for "
+                        "device tensors (several ranks sharing one GPU)")
     p.add_argument("--sync", choices=["allreduce", "root"], default="allreduce")
     p.add_argument("--comm_mode", choices=["auto", "overlap", "inline"], default="auto")
     p.add_argument("--bucket_mb", type=float, default=1.0)
@@ -210,8 +216,19 @@ def config_from_args(args) -> TrainConfig:
     return cfg
 
 
+def resolve_device(device: str) -> str:
+    """``auto`` -> ``cuda`` when a GPU is visible.  ``device_count()`` does not initialise the
+    HIP runtime, so a launcher process may call this before it spawns its ranks."""
+    if device != "auto":
+        return device
+    import torch
+    return "cuda" if torch.cuda.device_count() > 0 else "cpu"
+
+
 def validate(cfg: TrainConfig) -> None:
     """Fail fast before any collective."""
+    if cfg.device not in ("auto", "cpu", "cuda"):
+        raise ValueError(f"device must be auto, cpu or cuda, got {cfg.device!r}")
     if len(cfg.widths) < 2:
         raise ValueError(f"widths needs >= 2 entries, got {cfg.widths}")
     if cfg.n_features != cfg.widths[0]:

@@ -104,3 +104,34 @@ def parallel_efficiency(samples_per_s: Optional[float], world: int,
     if not samples_per_s or not ref_samples_per_s:
         return None
     return samples_per_s / (world * ref_samples_per_s)
+
+
+def scaling_report(world: int, rows_per_rank: int, global_rows: int, step_ms: float,
+                   compute_ms: Optional[float], comm_ms: Optional[float],
+                   wire_bytes_per_rank: int) -> dict:
+    """The BASELINE metric's derived terms for one measured configuration (BASELINE.md:66-70).
+
+    * ``step_ms``    -- the full data-parallel step (max over ranks);
+    * ``compute_ms`` -- the same per-rank work with the gradient synchronisation switched off
+      (every rank alone = the single-GPU step of this shard size);
+    * ``comm_ms``    -- the step's collectives alone (same buckets, dtype and order), no compute.
+
+    Returns samples/s, ``parallel_efficiency`` = S(P) / (P * S(1)) with S(1) the single-GPU
+    throughput of the same per-rank work (weak scaling: = compute_ms / step_ms),
+    ``exposed_comm_ms`` = step - compute (communication time not hidden behind compute),
+    ``overlap_pct`` = the share of the collectives' own time that the step hides, and the
+    achieved all-reduce bus bandwidth ``comm_bus_gbps`` = wire bytes per rank / comm_ms.
+    """
+    out = {"samples_per_s": global_rows / (step_ms * 1e-3) if step_ms > 0 else None}
+    if compute_ms:
+        s1 = rows_per_rank / (compute_ms * 1e-3)
+        out["single_gpu_samples_per_s"] = s1
+        out["parallel_efficiency"] = out["samples_per_s"] / (world * s1)
+        out["exposed_comm_ms"] = max(0.0, step_ms - compute_ms)
+    if comm_ms and compute_ms:
+        out["comm_only_ms"] = comm_ms
+        hidden = comm_ms - out["exposed_comm_ms"]
+        out["overlap_pct"] = 100.0 * min(1.0, max(0.0, hidden / comm_ms))
+    if comm_ms:
+        out["comm_bus_gbps"] = comm_bus_gbps(wire_bytes_per_rank, comm_ms)
+    return out

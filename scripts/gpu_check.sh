@@ -23,6 +23,10 @@ for s in $STEPS; do
     tests)
       timeout -k 10 900 python -u -m pytest tests -m gpu -x -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
       ok_or_stop $? tests ;;
+    multirank)
+      # P >= 2 on the one GPU: gloo-shared and RCCL (per-rank NCCL_HOSTID) rank processes
+      timeout -k 10 1000 python -u -m pytest tests/test_multirank_gpu.py tests/test_bench.py -m gpu -v --timeout 400 --timeout-method thread > gpurun_out/pytest_multirank.log 2>&1
+      ok_or_stop $? multirank ;;
     testsall)
       timeout -k 10 900 python -u -m pytest tests -m gpu -v --timeout 120 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1
       ok_or_stop $? testsall ;;

@@ -1,0 +1,91 @@
+"""bench.py contract: N ranks launched by the script itself, refusal to misreport, and the
+BASELINE metric's derived fields (efficiency, exposed comm, overlap %, bus GB/s, strong scaling)."""
+import json
+import os
+import subprocess
+import sys
+
+import pytest
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+BENCH = os.path.join(ROOT, "bench.py")
+
+
+def _run(args, env=None, timeout=300):
+    e = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "LOCAL_WORLD_SIZE", "MASTER_ADDR",
+              "MASTER_PORT", "PMI_RANK", "PMI_SIZE", "OMPI_COMM_WORLD_RANK"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, BENCH] + args, capture_output=True, text=True,
+                          timeout=timeout, env=e)
+
+
+def _line(r):
+    assert r.returncode == 0, r.stderr[-3000:]
+    lines = [l for l in r.stdout.splitlines() if l.strip()]
+    assert len(lines) == 1, r.stdout            # ONE JSON line on stdout, nothing else
+    return json.loads(lines[0])
+
+
+def test_bench_self_launches_two_ranks_cpu():
+    d = _line(_run(["--gpus", "2", "--device", "cpu", "--config", "ref", "--steps", "10",
+                    "--warmup", "2"]))
+    assert d["n_gpus"] == 2 and d["config"]["parallelism"] == "dp2"
+    assert d["steps"] == 10 and d["warmup"] == 2
+    assert d["config"]["comm"] == "gloo" and d["config"]["uneven_split"]
+    assert d["config"]["global_batch"] == 31          # 16 * 2 - 1: the uneven split
+    for k in ("parallel_efficiency", "exposed_comm_ms", "overlap_pct", "comm_bus_gbps",
+              "comm_only_ms", "single_gpu_samples_per_s"):
+        assert d[k] is not None, k
+    assert 0.0 <= d["overlap_pct"] <= 100.0
+    assert 0.0 < d["parallel_efficiency"]
+    s = d["strong_scaling"]
+    assert s["global_batch"] == 16 and s["samples_per_s"] > 0 and s["parallel_efficiency"] > 0
+
+
+def test_bench_single_rank_cpu_unchanged_shape():
+    d = _line(_run(["--device", "cpu", "--config", "ref", "--steps", "10", "--warmup", "2"]))
+    assert d["n_gpus"] == 1 and d["config"]["parallelism"] == "dp1"
+    assert d["config"]["comm"] == "none" and d["parallel_efficiency"] == 1.0
+    assert d["strong_scaling"] is None
+
+
+def test_bench_refuses_world_mismatch_under_launcher():
+    r = _run(["--gpus", "3", "--device", "cpu", "--config", "ref", "--steps", "2"],
+             env={"RANK": "0", "WORLD_SIZE": "2", "LOCAL_RANK": "0", "MASTER_ADDR": "127.0.0.1",
+                  "MASTER_PORT": "1"})
+    assert r.returncode != 0 and "refusing" in r.stderr
+
+
+def test_bench_rank_failure_fails_the_job():
+    """A rank that dies makes the self-launched job exit non-zero (never a partial result)."""
+    r = _run(["--gpus", "2", "--device", "cpu", "--config", "nonexistent"])
+    assert r.returncode != 0
+
+
+def test_scaling_report_arithmetic():
+    from nnmpi_amd.utils.metrics import scaling_report
+    # 4 ranks x 1000 rows; step 2.0 ms, compute-only 1.5 ms, collectives alone 1.0 ms
+    r = scaling_report(4, 1000, 4000, 2.0, 1.5, 1.0, 3_000_000)
+    assert r["samples_per_s"] == pytest.approx(4000 / 2e-3)
+    assert r["single_gpu_samples_per_s"] == pytest.approx(1000 / 1.5e-3)
+    assert r["parallel_efficiency"] == pytest.approx(0.75)        # = compute / step
+    assert r["exposed_comm_ms"] == pytest.approx(0.5)
+    assert r["overlap_pct"] == pytest.approx(50.0)                # 0.5 of 1.0 ms hidden
+    assert r["comm_bus_gbps"] == pytest.approx(3.0)               # 3 MB / 1 ms
+    # fully hidden / not hidden at all; clamped
+    assert scaling_report(2, 10, 20, 1.0, 1.0, 0.4, 1)["overlap_pct"] == 100.0
+    assert scaling_report(2, 10, 20, 3.0, 1.0, 0.4, 1)["overlap_pct"] == 0.0
+    assert "overlap_pct" not in scaling_report(1, 10, 10, 1.0, 1.0, None, 0)
+
+
+@pytest.mark.gpu
+def test_bench_more_gpus_than_visible_fails():
+    """On a box with fewer GPUs than --gpus the bench must exit non-zero, not run one rank."""
+    import torch
+    n = torch.cuda.device_count() + 1
+    r = _run(["--gpus", str(n), "--steps", "2", "--warmup", "1"], timeout=120)
+    assert r.returncode != 0
+    assert "visible" in r.stderr
+    assert r.stdout.strip() == ""

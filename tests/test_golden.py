@@ -46,14 +46,14 @@ def test_reference_init_matches_golden():
 
 
 def test_golden_p1_single_process():
-    res = nnmpi_amd.engine.trainer.run_worker(TrainConfig())
+    res = nnmpi_amd.engine.trainer.run_worker(TrainConfig(device="cpu"))
     assert res.losses == pytest.approx(GOLDEN_LOSSES[1][0], rel=1e-5)
     assert torch.allclose(res.final_params, torch.tensor(GOLDEN_PARAMS[1]), atol=2e-6)
 
 
 @pytest.mark.parametrize("world", [2, 4, 8])
 def test_golden_multirank(world):
-    out = run_ranks(TrainConfig(print_rank="none"), world)
+    out = run_ranks(TrainConfig(device="cpu", print_rank="none"), world)
     for r in range(world):
         assert out[r]["losses"] == pytest.approx(GOLDEN_LOSSES[world][r], rel=1e-5), r
     for r in range(world):

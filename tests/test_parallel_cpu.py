@@ -8,7 +8,7 @@ import sys
 import pytest
 import torch
 
-from _mp import run_ranks
+from _mp import _free_port, run_ranks
 
 import nnmpi_amd  # noqa: F401
 from nnmpi_amd.engine import trainer
@@ -20,7 +20,7 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 @pytest.mark.parametrize("world", [3, 5, 6, 7])
 def test_uneven_world_sizes_train(world):
     """The reference crashes for P in {3,5,6,7} (int8 counts as MPI.INT, D2); here they train."""
-    out = run_ranks(TrainConfig(print_rank="none"), world)
+    out = run_ranks(TrainConfig(device="cpu", print_rank="none"), world)
     rows = [o["rows"] for o in out]
     assert sum(rows) == 16 and max(rows) - min(rows) <= 1
     for o in out:
@@ -29,7 +29,7 @@ def test_uneven_world_sizes_train(world):
 
 
 def test_more_ranks_than_rows_allows_empty_shards():
-    cfg = TrainConfig(print_rank="none", n_samples=3, averaging="weighted", scaling="global")
+    cfg = TrainConfig(device="cpu", print_rank="none", n_samples=3, averaging="weighted", scaling="global")
     out = run_ranks(cfg, 4)
     assert [o["rows"] for o in out] == [1, 1, 1, 0]
     for o in out:
@@ -39,7 +39,7 @@ def test_more_ranks_than_rows_allows_empty_shards():
 @pytest.mark.parametrize("world", [2, 3, 4])
 def test_dp_equals_single_process_with_global_scaling(world):
     """With global feature scaling and sample-weighted averaging, P-rank DP == 1 rank."""
-    cfg = TrainConfig(print_rank="none", scaling="global", averaging="weighted", nepochs=6,
+    cfg = TrainConfig(device="cpu", print_rank="none", scaling="global", averaging="weighted", nepochs=6,
                       n_samples=48, lr=0.01)
     single = trainer.run_worker(cfg)
     out = run_ranks(cfg, world)
@@ -48,14 +48,14 @@ def test_dp_equals_single_process_with_global_scaling(world):
 
 
 def test_root_sync_mode_matches_allreduce():
-    a = run_ranks(TrainConfig(print_rank="none", sync="root"), 4)
-    b = run_ranks(TrainConfig(print_rank="none", sync="allreduce"), 4)
+    a = run_ranks(TrainConfig(device="cpu", print_rank="none", sync="root"), 4)
+    b = run_ranks(TrainConfig(device="cpu", print_rank="none", sync="allreduce"), 4)
     for x, y in zip(a, b):
         torch.testing.assert_close(x["final"], y["final"], rtol=1e-5, atol=2e-6)
 
 
 def test_minibatches_uneven_ranks_do_not_deadlock():
-    cfg = TrainConfig(print_rank="none", batch_size=2, n_samples=17, nepochs=2)
+    cfg = TrainConfig(device="cpu", print_rank="none", batch_size=2, n_samples=17, nepochs=2)
     out = run_ranks(cfg, 3)
     for o in out:
         assert o["steps"] == 2 * 3          # ceil(6 rows / 2) steps per epoch on every rank
@@ -63,12 +63,12 @@ def test_minibatches_uneven_ranks_do_not_deadlock():
 
 
 def test_sequence_checker_passes():
-    out = run_ranks(TrainConfig(print_rank="none", seqcheck=True), 2)
+    out = run_ranks(TrainConfig(device="cpu", print_rank="none", seqcheck=True), 2)
     assert len(out) == 2
 
 
 def test_bf16_cpu_path_trains():
-    cfg = TrainConfig(print_rank="none", widths=[64, 64, 64, 1], n_features=64, n_samples=512,
+    cfg = TrainConfig(device="cpu", print_rank="none", widths=[64, 64, 64, 1], n_features=64, n_samples=512,
                       dtype="bf16", nepochs=4, lr=1e-4)
     out = run_ranks(cfg, 2)
     assert out[0]["losses"][-1] < out[0]["losses"][0]
@@ -77,9 +77,9 @@ def test_bf16_cpu_path_trains():
 
 def test_checkpoint_resume_is_exact(tmp_path):
     ck = str(tmp_path / "model.pt")
-    full = trainer.run_worker(TrainConfig(print_rank="none", nepochs=5))
-    trainer.run_worker(TrainConfig(print_rank="none", nepochs=3, checkpoint=ck))
-    res = trainer.run_worker(TrainConfig(print_rank="none", nepochs=5, resume=ck))
+    full = trainer.run_worker(TrainConfig(device="cpu", print_rank="none", nepochs=5))
+    trainer.run_worker(TrainConfig(device="cpu", print_rank="none", nepochs=3, checkpoint=ck))
+    res = trainer.run_worker(TrainConfig(device="cpu", print_rank="none", nepochs=5, resume=ck))
     assert torch.equal(res.final_params, full.final_params)
     sd = torch.load(ck, weights_only=True)
     assert list(sd) == ["layers.0.weight", "layers.0.bias", "layers.2.weight", "layers.2.bias"]
@@ -90,7 +90,7 @@ def test_checkpoint_resume_is_exact(tmp_path):
 
 def test_metrics_json(tmp_path):
     mj = str(tmp_path / "m.jsonl")
-    trainer.run_worker(TrainConfig(print_rank="none", metrics_json=mj))
+    trainer.run_worker(TrainConfig(device="cpu", print_rank="none", metrics_json=mj))
     import json
     lines = [json.loads(l) for l in open(mj)]
     assert len(lines) == 3 and all("samples_per_s" in l for l in lines)
@@ -109,7 +109,7 @@ def test_metrics_comm_volume_and_efficiency(tmp_path):
     assert parallel_efficiency(300.0, 4, 100.0) == 0.75
     assert parallel_efficiency(300.0, 4, None) is None
     mj = str(tmp_path / "m.jsonl")
-    run_ranks(TrainConfig(print_rank="none", metrics_json=mj, ref_samples_per_s=1000.0), 2)
+    run_ranks(TrainConfig(device="cpu", print_rank="none", metrics_json=mj, ref_samples_per_s=1000.0), 2)
     lines = [json.loads(l) for l in open(mj)]
     assert lines and all(l["world"] == 2 for l in lines)
     # 13 parameters padded into the 64-aligned arena, fp32 ring all-reduce over 2 ranks
@@ -167,8 +167,8 @@ def test_bf16_gradient_payload_trains_close_to_fp32():
     """--grad_dtype bf16: the all-reduce payload is rounded to bf16 (half the xGMI bytes);
     replicas stay identical and the run tracks the fp32-payload run closely."""
     cfg = dict(print_rank="none", n_samples=64, nepochs=5, lr=0.01)
-    a = run_ranks(TrainConfig(grad_dtype="bf16", **cfg), 2)
-    b = run_ranks(TrainConfig(grad_dtype="fp32", **cfg), 2)
+    a = run_ranks(TrainConfig(device="cpu", grad_dtype="bf16", **cfg), 2)
+    b = run_ranks(TrainConfig(device="cpu", grad_dtype="fp32", **cfg), 2)
     assert torch.equal(a[0]["final"], a[1]["final"])
     torch.testing.assert_close(a[0]["final"], b[0]["final"], rtol=2e-2, atol=2e-3)
     assert not torch.equal(a[0]["final"], b[0]["final"])   # the rounding really happened
@@ -179,8 +179,8 @@ def test_sharded_optimizer_matches_allreduce_bitwise(world):
     """ZeRO-1 (reduce-scatter -> SGD on the own 1/P slice -> all-gather) computes exactly the
     all-reduce path's update; world 3 leaves an uneven data split and a padded arena."""
     cfg = dict(print_rank="none", nepochs=4, n_samples=17)
-    a = run_ranks(TrainConfig(shard_optimizer=True, **cfg), world)
-    b = run_ranks(TrainConfig(**cfg), world)
+    a = run_ranks(TrainConfig(device="cpu", shard_optimizer=True, **cfg), world)
+    b = run_ranks(TrainConfig(device="cpu", **cfg), world)
     for x, y in zip(a, b):
         assert x["losses"] == y["losses"]
         assert torch.equal(x["final"], y["final"])
@@ -189,8 +189,8 @@ def test_sharded_optimizer_matches_allreduce_bitwise(world):
 def test_sharded_optimizer_bf16_mlp():
     cfg = dict(print_rank="none", widths=[64, 64, 64, 1], n_features=64, n_samples=256,
                dtype="bf16", nepochs=3, lr=1e-4)
-    a = run_ranks(TrainConfig(shard_optimizer=True, **cfg), 2)
-    b = run_ranks(TrainConfig(**cfg), 2)
+    a = run_ranks(TrainConfig(device="cpu", shard_optimizer=True, **cfg), 2)
+    b = run_ranks(TrainConfig(device="cpu", **cfg), 2)
     assert torch.equal(a[0]["final"], a[1]["final"])
     assert torch.equal(a[0]["final"], b[0]["final"])
 
@@ -205,9 +205,9 @@ def test_sharded_optimizer_checkpoint_resume_is_exact(tmp_path):
     """The checkpoint of a sharded run holds the re-assembled master AND momentum."""
     ck = str(tmp_path / "z.pt")
     cfg = dict(print_rank="none", shard_optimizer=True, n_samples=32)
-    full = run_ranks(TrainConfig(nepochs=5, **cfg), 2)
-    run_ranks(TrainConfig(nepochs=3, checkpoint=ck, **cfg), 2)
-    res = run_ranks(TrainConfig(nepochs=5, resume=ck, **cfg), 2)
+    full = run_ranks(TrainConfig(device="cpu", nepochs=5, **cfg), 2)
+    run_ranks(TrainConfig(device="cpu", nepochs=3, checkpoint=ck, **cfg), 2)
+    res = run_ranks(TrainConfig(device="cpu", nepochs=5, resume=ck, **cfg), 2)
     assert torch.equal(res[0]["final"], full[0]["final"])
 
 
@@ -228,13 +228,13 @@ def _reference_val_loss(res, n_val):
 
 
 def test_validation_split_loss_matches_independent_eval():
-    res = trainer.run_worker(TrainConfig(print_rank="none", val_fraction=0.25, nepochs=4))
+    res = trainer.run_worker(TrainConfig(device="cpu", print_rank="none", val_fraction=0.25, nepochs=4))
     assert len(res.val_losses) == 4 and res.rows == 12
     assert res.val_losses[-1] == pytest.approx(_reference_val_loss(res, 4), rel=1e-5)
 
 
 def test_validation_split_multirank_is_global():
-    out = run_ranks(TrainConfig(print_rank="none", val_fraction=0.25, n_samples=32, nepochs=2), 2)
+    out = run_ranks(TrainConfig(device="cpu", print_rank="none", val_fraction=0.25, n_samples=32, nepochs=2), 2)
     assert [o["rows"] for o in out] == [12, 12]
     assert out[0]["losses"] != out[1]["losses"]        # local training losses differ
     assert out[0]["val"] == out[1]["val"] and len(out[0]["val"]) == 2   # one global value
@@ -244,8 +244,8 @@ def test_grad_accum_full_shard_equals_one_batch():
     """Cutting the whole-shard batch into 4 accumulated micro-batches gives the same steps
     (up to fp32 summation order) and the same per-epoch mean losses."""
     cfg = dict(print_rank="none", nepochs=5, n_samples=64, lr=0.01)
-    a = trainer.run_worker(TrainConfig(**cfg))
-    b = trainer.run_worker(TrainConfig(grad_accum=4, **cfg))
+    a = trainer.run_worker(TrainConfig(device="cpu", **cfg))
+    b = trainer.run_worker(TrainConfig(device="cpu", grad_accum=4, **cfg))
     assert a.steps == b.steps == 5
     torch.testing.assert_close(b.final_params, a.final_params, rtol=1e-5, atol=1e-6)
     assert b.losses == pytest.approx(a.losses, rel=1e-5)
@@ -255,8 +255,8 @@ def test_grad_accum_minibatches_multirank():
     """batch 4 x 2 accumulated micro-batches == batch 8 (same shuffled rows per step), on an
     uneven 3-rank split (9/8/8 rows) whose short shards run an empty last micro-batch."""
     cfg = dict(print_rank="none", nepochs=3, n_samples=25, lr=0.01)
-    a = run_ranks(TrainConfig(batch_size=8, **cfg), 3)
-    b = run_ranks(TrainConfig(batch_size=4, grad_accum=2, **cfg), 3)
+    a = run_ranks(TrainConfig(device="cpu", batch_size=8, **cfg), 3)
+    b = run_ranks(TrainConfig(device="cpu", batch_size=4, grad_accum=2, **cfg), 3)
     for x, y in zip(a, b):
         assert x["steps"] == y["steps"] == 3 * 2
         torch.testing.assert_close(y["final"], x["final"], rtol=1e-5, atol=1e-6)
@@ -268,3 +268,40 @@ def test_grad_accum_flag():
     assert config_from_args(build_parser().parse_args(["--accum_steps", "3"])).grad_accum == 3
     with pytest.raises(ValueError):
         config_from_args(build_parser().parse_args(["--grad_accum", "0"]))
+
+
+@pytest.mark.parametrize("fail_rank", [0, 1])
+def test_one_rank_failure_ends_every_rank(fail_rank):
+    """the reference hangs when one rank raises while the others block in
+    gather/recv (ref.py:185,203).  Here 3 independently launched ranks (as mpiexec/torchrun
+    would start them), one raising at epoch 1: every process must exit non-zero, well within
+    timeout_s + 10 s (the collectives error out, or the watchdog aborts)."""
+    import time
+    timeout_s = 20
+    port = _free_port()
+    procs = []
+    t0 = time.monotonic()
+    for r in range(3):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE="3", LOCAL_RANK=str(r),
+                   LOCAL_WORLD_SIZE="3", MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   NNMPI_FAULT_INJECT=f"{fail_rank}:1", OMP_NUM_THREADS="1")
+        procs.append(subprocess.Popen(
+            [sys.executable, os.path.join(ROOT, "dataParallelTraining_NN_MPI.py"),
+             "--device", "cpu", "--nepochs", "50", "--timeout_s", str(timeout_s),
+             "--print_rank", "none"],
+            env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True))
+    codes = []
+    try:
+        for p in procs:
+            left = max(1.0, timeout_s + 10 - (time.monotonic() - t0) + 30)  # +30: python start
+            p.wait(timeout=left)
+            codes.append(p.returncode)
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+    elapsed = time.monotonic() - t0
+    assert all(c != 0 for c in codes), codes
+    assert elapsed < timeout_s + 10 + 30, elapsed
+    err = procs[fail_rank].stderr.read()
+    assert "injected fault" in err

@@ -151,7 +151,7 @@ def test_chunked_generator_is_partition_independent():
 
 def test_engine_cpu_mse_mnist_shapes_run():
     from nnmpi_amd.engine import trainer
-    cfg = TrainConfig(print_rank="none", widths=[20, 16, 4], n_features=20, loss="xent",
+    cfg = TrainConfig(device="cpu", print_rank="none", widths=[20, 16, 4], n_features=20, loss="xent",
                       n_samples=64, nepochs=3, lr=0.1)
     res = trainer.run_worker(cfg)
     assert res.losses[-1] < res.losses[0]
@@ -191,7 +191,7 @@ def test_sequence_checker_detects_mismatch():
 
 def test_profile_steps_phase_breakdown(capsys):
     from nnmpi_amd.engine import trainer
-    cfg = TrainConfig(print_rank="all", widths=[20, 16, 1], n_features=20, n_samples=64,
+    cfg = TrainConfig(device="cpu", print_rank="all", widths=[20, 16, 1], n_features=20, n_samples=64,
                       nepochs=3, profile_steps=True)
     res = trainer.run_worker(cfg)
     assert set(res.phase_ms) == {"start->fwd", "fwd->head", "head->bwd", "bwd->comm",
