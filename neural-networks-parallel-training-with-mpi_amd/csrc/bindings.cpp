@@ -314,7 +314,8 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
       .def_property_readonly("comm_stream", [](GradSync& g) { return (uptr)g.comm_stream(); });
   py::class_<GraphRunner>(m, "GraphRunner")
       .def(py::init<>())
-      .def("begin", [](GraphRunner& g, uptr s) { g.begin(S(s)); })
+      .def("begin", [](GraphRunner& g, uptr s, int mode) { g.begin(S(s), mode); },
+           py::arg("s"), py::arg("mode") = 1)
       .def("end", &GraphRunner::end)
       .def("cancel", &GraphRunner::cancel)
       .def("launch", [](GraphRunner& g, uptr s) { g.launch(S(s)); })

@@ -187,11 +187,14 @@ GraphRunner::~GraphRunner() {
   if (graph_) (void)hipGraphDestroy(graph_);
 }
 
-void GraphRunner::begin(hipStream_t s) {
+void GraphRunner::begin(hipStream_t s, int mode) {
   if (exec_) { (void)hipGraphExecDestroy(exec_); exec_ = nullptr; }
   if (graph_) { (void)hipGraphDestroy(graph_); graph_ = nullptr; }
   cap_ = s;
-  HIP_THROW(hipStreamBeginCapture(s, hipStreamCaptureModeThreadLocal));
+  const hipStreamCaptureMode m = mode == 0 ? hipStreamCaptureModeGlobal
+                               : mode == 2 ? hipStreamCaptureModeRelaxed
+                                           : hipStreamCaptureModeThreadLocal;
+  HIP_THROW(hipStreamBeginCapture(s, m));
 }
 
 void GraphRunner::end() {

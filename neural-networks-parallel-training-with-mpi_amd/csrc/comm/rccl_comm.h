@@ -82,7 +82,8 @@ class GraphRunner {
  public:
   GraphRunner() = default;
   ~GraphRunner();
-  void begin(hipStream_t s);
+  // mode: 0 global, 1 thread-local (default), 2 relaxed (hipStreamCaptureMode*)
+  void begin(hipStream_t s, int mode = 1);
   void end();
   void launch(hipStream_t s);
   // abandon an in-progress capture (after a throw) and drop any partial graph

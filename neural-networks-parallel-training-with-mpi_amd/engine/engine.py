@@ -508,11 +508,19 @@ class MLPEngine:
     def _capture(self, nsteps: int = 1):
         from .. import native
         g = native.lib().GraphRunner()
-        s = int(self.stream.cuda_stream)
-        g.begin(s)
+        origin = self.sync.capture_origin()
+        if origin is None:
+            origin = self.stream
+        g.begin(int(origin.cuda_stream))
         try:
+            if origin is not self.stream:
+                # collectives live on the comm stream: it is the capture origin, the compute
+                # stream forks from it here and joins back below (see GradSync.capture_origin)
+                self.stream.wait_stream(origin)
             for _ in range(nsteps):
                 self._step_body(False)
+            if origin is not self.stream:
+                origin.wait_stream(self.stream)
         except Exception:
             g.cancel()    # leave the stream out of capture mode, drop the partial graph
             raise

@@ -62,6 +62,15 @@ class GradSync:
     def finish(self):
         pass
 
+    def capture_origin(self):
+        """The stream a hipGraph capture of a step must START on (None: the compute stream).
+        RCCL (ROCm 7, RCCL 2.26) crashes in hipStreamEndCapture when the first collective of a
+        capture is issued on a stream forked from the origin (scripts/rccl_capture_probe.py,
+        variant "side": SIGSEGV at P=2; "comm_origin": fine), so a schedule that issues its
+        collectives on a comm stream captures with that stream as the origin and forks the
+        compute stream from it."""
+        return None
+
     def comm_only(self):
         """Issue exactly the collectives of one step's gradient synchronisation on the current
         stream, with no compute around them (the bench's comm-only timing: achieved bus
@@ -179,6 +188,9 @@ class NativeRcclSync(GradSync):
 
     def launch_bucket(self, bucket, stream):
         self._launch(bucket, stream)
+        return None if self.inline else self._comm_stream
+
+    def capture_origin(self):
         return None if self.inline else self._comm_stream
 
     def comm_only(self):

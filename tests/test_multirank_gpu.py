@@ -24,7 +24,7 @@ pytestmark = pytest.mark.gpu
 
 def rccl_env(rank):
     return {"NCCL_HOSTID": f"nnmpi-test-host-{rank}", "NCCL_SOCKET_IFNAME": "lo",
-            "NCCL_IB_DISABLE": "1"}
+            "NCCL_IB_DISABLE": "1", "PYTHONFAULTHANDLER": "1", "NCCL_DEBUG": "WARN"}
 
 
 def _cfg(**kw):
@@ -104,6 +104,13 @@ def test_rccl_two_ranks_bitwise_equal_gloo():
     _replicas_equal(a)
     assert a[0]["losses"] == b[0]["losses"] and a[1]["losses"] == b[1]["losses"]
     assert torch.equal(a[0]["final"], b[0]["final"])
+
+
+@pytest.mark.parametrize("graph", [False, True])
+def test_rccl_overlap_two_ranks_runs(graph):
+    out = run_ranks_proc(_cfg(comm="native", comm_mode="overlap", graph=graph, nepochs=2), 2,
+                         env_per_rank=rccl_env)
+    _replicas_equal(out)
 
 
 @pytest.mark.parametrize("mode", ["overlap", "inline"])
