@@ -111,6 +111,10 @@ def parse(argv=None):
                    help="use the RCCL gradient path even with one rank (smoke-tests comm overlap)")
     p.add_argument("--no_extras", action="store_true",
                    help="skip the post-timed-region efficiency / overlap / strong-scaling runs")
+    p.add_argument("--shared_gpu_rehearsal", action="store_true",
+                   help="TESTING ONLY: let the N ranks share the visible GPU(s) (each rank its own "
+                        "NCCL_HOSTID, RCCL over loopback) to rehearse the multi-rank code path on "
+                        "a 1-GPU box; the JSON line says so and its numbers are not a measurement")
     p.add_argument("--fwd_variant", type=int, default=-1, help="forward GEMM variant (experiments)")
     p.add_argument("--group_async", type=int, default=-1,
                    help="grouped-backward LDS read mode (experiments)")
@@ -135,7 +139,7 @@ def launch_ranks(a, argv) -> int:
     if a.device != "cpu":
         import torch
         have = torch.cuda.device_count()
-        if have < n and not (a.device == "auto" and have == 0):
+        if have < n and not (a.device == "auto" and have == 0) and not a.shared_gpu_rehearsal:
             _fail(f"--gpus {n} needs {n} visible GPUs, this node shows {have}")
         if a.device == "auto" and have == 0:
             a.device = "cpu"
@@ -147,6 +151,10 @@ def launch_ranks(a, argv) -> int:
                    NNMPI_LAUNCHER="bench")
         if a.device == "cpu":
             env.setdefault("OMP_NUM_THREADS", str(max(1, (os.cpu_count() or 1) // n)))
+        if a.shared_gpu_rehearsal:
+            # RCCL refuses two ranks on one device unless they look like different hosts
+            env.update(NCCL_HOSTID=f"nnmpi-rehearsal-{r}", NCCL_SOCKET_IFNAME="lo",
+                       NCCL_IB_DISABLE="1")
         procs.append(subprocess.Popen([sys.executable, os.path.abspath(__file__)] + list(argv),
                                       env=env))
     first_bad = 0
@@ -187,7 +195,7 @@ def main(argv=None):
         a.device = "cuda" if torch.cuda.device_count() > 0 else "cpu"
     if a.device == "cuda":
         have = torch.cuda.device_count()
-        if have < job.local_world:
+        if have < job.local_world and not a.shared_gpu_rehearsal:
             _fail(f"{job.local_world} local ranks need as many GPUs; {have} visible "
                   "(one rank per GPU: RCCL refuses two ranks on one device)")
     run(a, job)
@@ -462,6 +470,7 @@ def run(a, job):
                        "grad_wire_bytes_per_rank": wire,
                        "bucket_mb": a.bucket_mb},
             "rccl_ranks": (native_comm.size if native_comm is not None else None),
+            "shared_gpu_rehearsal": bool(a.shared_gpu_rehearsal),
             "model_tflops_per_s": round(tflops, 2),
             "parallel_efficiency": rnd(extras.get("parallel_efficiency")),
             "single_gpu_samples_per_s": rnd(extras.get("single_gpu_samples_per_s"), 1),

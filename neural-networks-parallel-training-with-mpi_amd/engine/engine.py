@@ -57,7 +57,11 @@ class MLPEngine:
             use_tiny = (self.is_cuda and dtype == torch.float32 and L <= TINY_MAX_LAYERS
                         and max(w) <= TINY_MAX_WIDTH)
         self.use_tiny = bool(use_tiny)
-        self.use_graph = bool(use_graph) and self.is_cuda
+        # host-driven torch.distributed transports (gloo copies device tensors through the host;
+        # torch's nccl runs on its own side stream) cannot live inside a replayed hipGraph
+        from ..parallel.sync import TorchDistSync
+        self.use_graph = (bool(use_graph) and self.is_cuda
+                          and not (isinstance(sync, TorchDistSync) and sync.world > 1))
         self._validate()
         dev, R = self.device, self.R
         self.stream = torch.cuda.Stream(device=dev) if self.is_cuda else None

@@ -89,3 +89,20 @@ def test_bench_more_gpus_than_visible_fails():
     assert r.returncode != 0
     assert "visible" in r.stderr
     assert r.stdout.strip() == ""
+
+
+@pytest.mark.gpu
+def test_bench_two_rank_rehearsal_on_one_gpu():
+    """The whole multi-rank bench path -- tune of inline / ZeRO-1 / overlap schedules with the
+    RCCL collectives captured in hipGraphs, timed region, efficiency / comm-only / strong-scaling
+    extras -- with 2 RCCL ranks sharing the one GPU (NCCL_HOSTID rehearsal mode)."""
+    r = _run(["--gpus", "2", "--shared_gpu_rehearsal", "--steps", "8", "--warmup", "2",
+              "--tune_steps", "4"], timeout=300)
+    d = _line(r)
+    assert d["n_gpus"] == 2 and d["rccl_ranks"] == 2 and d["shared_gpu_rehearsal"]
+    assert d["config"]["comm"] == "rccl" and d["config"]["comm_mode"] in ("inline", "zero1",
+                                                                         "overlap")
+    assert set(d["config"]["comm_tune_ms_per_step"]) == {"inline", "zero1", "overlap"}
+    assert d["parallel_efficiency"] is not None and d["comm_bus_gbps"] is not None
+    assert d["strong_scaling"]["global_batch"] == 8192
+    assert d["final_loss"] == d["final_loss"]
