@@ -13,6 +13,7 @@ all-reduce and checkpointing all operate on flat ranges.
 """
 from __future__ import annotations
 
+import os
 from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
@@ -47,13 +48,37 @@ class Bucket:
     layers: Tuple[int, ...]   # layer ids in backward order (descending)
     offset: int
     numel: int
+    rows: Optional[Tuple[int, int]] = None   # sub-layer bucket: output rows [r0, r1) of layers[0]
+
+
+# A layer whose gradient is larger than one bucket is cut into output-row chunks, each its own
+# bucket, so its all-reduce can start while the rest of that layer's weight gradient is still
+# being computed (the last layer of backward is otherwise one fully exposed collective).  The
+# chunk count keeps every chunk's weight-gradient GEMM a full wave of 256x256 tiles on the
+# 256 CUs (rows per chunk a multiple of 256, >= 256 tiles per chunk).
+CHUNK_TILE = 256
+CHUNK_MIN_TILES = 256
+
+
+def row_chunks(out_f: int, in_f: int, grad_bytes: int, bucket_bytes: float) -> int:
+    if grad_bytes <= bucket_bytes or out_f % CHUNK_TILE or in_f % CHUNK_TILE:
+        return 1
+    # (NNMPI_CHUNK_MIN_TILES: tests exercise the chunked schedule on small layers)
+    min_tiles = int(os.environ.get("NNMPI_CHUNK_MIN_TILES", CHUNK_MIN_TILES))
+    c = 1
+    while (out_f % (2 * c * CHUNK_TILE) == 0 and
+           (out_f // (2 * c * CHUNK_TILE)) * (in_f // CHUNK_TILE) >= min_tiles):
+        c *= 2
+    return c
 
 
 class Arena:
     def __init__(self, layer_shapes: List[Tuple[int, int]], device, shadow_dtype=None,
-                 bucket_bytes: float = 25 * 2 ** 20, grad_elem_bytes: int = 4, pad_to: int = ALIGN):
+                 bucket_bytes: float = 25 * 2 ** 20, grad_elem_bytes: int = 4, pad_to: int = ALIGN,
+                 chunk_layers: bool = True):
         """``pad_to``: the total length is rounded up to this multiple (a multiple of ALIGN) --
-        the sharded optimizer uses ``world * ALIGN`` so every rank owns an equal, aligned shard."""
+        the sharded optimizer uses ``world * ALIGN`` so every rank owns an equal, aligned shard.
+        ``chunk_layers``: cut layers larger than a bucket into output-row chunk buckets."""
         self.layer_shapes = list(layer_shapes)
         self.n_layers = len(layer_shapes)
         self.device = torch.device(device)
@@ -76,6 +101,12 @@ class Arena:
         self.grad = z(torch.float32)
         self.momentum = z(torch.float32)
         self.shadow: Optional[torch.Tensor] = z(shadow_dtype) if shadow_dtype is not None else None
+        self.layer_chunks: Dict[int, int] = {}
+        if chunk_layers:
+            for li, (out_f, in_f) in enumerate(layer_shapes):
+                c = row_chunks(out_f, in_f, out_f * in_f * grad_elem_bytes, bucket_bytes)
+                if c > 1:
+                    self.layer_chunks[li] = c
         self.buckets = self._plan_buckets(bucket_bytes, grad_elem_bytes)
 
     # ---- views -------------------------------------------------------------------------
@@ -146,28 +177,65 @@ class Arena:
         return torch.cat(parts)
 
     # ---- buckets ----------------------------------------------------------------------
-    def _plan_buckets(self, bucket_bytes: float, elem_bytes: int) -> List[Bucket]:
-        """Greedy grouping of consecutive layers (backward order) into contiguous buckets."""
+    def _plan_buckets(self, bucket_bytes: float, elem_bytes: int,
+                      min_bytes: float = 64 * 2 ** 10, chunked: bool = True) -> List[Bucket]:
+        """Greedy grouping of consecutive layers (backward order) into contiguous buckets.  A
+        bucket below ``min_bytes`` (the output layer: a few KB) is never closed on its own --
+        it rides with the next layer instead of paying a collective's latency by itself.
+        Layers in ``layer_chunks`` become one bucket per output-row chunk (the last chunk also
+        holds the bias)."""
         cap = max(1, int(bucket_bytes // elem_bytes))
+        minc = int(min_bytes // elem_bytes)
         buckets: List[Bucket] = []
         cur: List[int] = []
         cur_start = 0
+
+        def close():
+            end = self.layer_range[cur[-1]][1]
+            buckets.append(Bucket(len(buckets), tuple(cur), cur_start, end - cur_start))
+
         for li in reversed(range(self.n_layers)):
             s, e = self.layer_range[li]
-            if cur and (e - cur_start) > cap:
-                buckets.append(Bucket(len(buckets), tuple(cur), cur_start,
-                                      self.layer_range[cur[-1]][1] - cur_start))
+            nch = self.layer_chunks.get(li, 1) if chunked else 1
+            if nch > 1:
+                if cur:
+                    close()
+                    cur = []
+                out_f, in_f = self.layer_shapes[li]
+                per = out_f // nch
+                for c in range(nch):
+                    r0, r1 = c * per, (c + 1) * per
+                    o0 = s + r0 * in_f
+                    o1 = e if c == nch - 1 else s + r1 * in_f
+                    buckets.append(Bucket(len(buckets), (li,), o0, o1 - o0, rows=(r0, r1)))
+                continue
+            if cur and (e - cur_start) > cap and (s - cur_start) >= minc:
+                close()
                 cur = []
             if not cur:
                 cur_start = s
             cur.append(li)
         if cur:
-            buckets.append(Bucket(len(buckets), tuple(cur), cur_start,
-                                  self.layer_range[cur[-1]][1] - cur_start))
+            close()
         return buckets
 
+    def replan_single_bucket(self):
+        """One bucket over the whole arena (a serial all-reduce amortises the latency)."""
+        self.buckets = [Bucket(0, tuple(reversed(range(self.n_layers))), 0, self.numel)]
+
     def bucket_of_layer(self, li: int) -> Bucket:
+        """The bucket that holds the END of layer ``li`` (its bias): the one that completes
+        when the layer's gradient is final."""
+        s, e = self.layer_range[li]
         for b in self.buckets:
-            if li in b.layers:
+            if li in b.layers and b.offset < e <= b.offset + b.numel:
                 return b
         raise KeyError(li)
+
+    def buckets_completed_by(self, li: int) -> List[Bucket]:
+        """Buckets whose every gradient is final once layer ``li``'s is (backward order: the
+        layer with the smallest index in the bucket is produced last)."""
+        return [b for b in self.buckets if li in b.layers and li == min(b.layers)]
+
+    def chunk_buckets(self, li: int) -> List[Bucket]:
+        return [b for b in self.buckets if b.rows is not None and b.layers == (li,)]

@@ -95,9 +95,12 @@ class MLPEngine:
         self.sharded = bool(getattr(sync, "sharded", False))
         inline_sync = (isinstance(sync, NoSync) or self.sharded or
                        (isinstance(sync, NativeRcclSync) and sync.inline))
+        # per-bucket collectives on the native comm stream, each bucket's SGD on an update stream
+        self.comm_overlap = isinstance(sync, NativeRcclSync) and not sync.inline
         # (shapes the grouped kernel does not cover -- e.g. the 256x256-tile 8192-wide layers --
         # take the sequential fused schedule, whose un-split wgrads apply SGD in their epilogue)
-        self.grouped = (bool(grouped) and self.overlap and dtype == torch.bfloat16 and inline_sync
+        self.grouped = (bool(grouped) and self.overlap and dtype == torch.bfloat16
+                        and (inline_sync or self.comm_overlap)
                         and hasattr(ops, "bwd_group") and L > 1 and
                         all(ops.bwd_group_supported(self.R, *spec.layer_shape(i))
                             for i in range(L - 1)))
@@ -231,13 +234,31 @@ class MLPEngine:
         self.sync.ready(last)
         for i in range(L - 2, -1, -1):
             x_in = self.acts[i - 1][:rows] if i > 0 else x
-            ops.linear_wgrad(dz, x_in, ar.grad_weight(i), ar.grad_bias(i), ws=self.ws)
+            for _ in self._wgrad_chunks(i, dz, x_in):
+                pass
             self.sync.ready(i)
             if i > 0:
                 dz_next = self._dzl(i - 1, rows)
                 ops.linear_dgrad(dz, ar.compute_weight(i), self.acts[i - 1][:rows], self.act, dz_next)
                 dz = dz_next
         self._mark("bwd")
+
+    def _wgrad_chunks(self, i: int, dz, x_in):
+        """Weight gradient of layer i; a layer cut into output-row chunk buckets (Arena
+        .layer_chunks) is computed chunk by chunk, yielding each chunk's bucket as soon as its
+        launch is queued (so its all-reduce can start while the next chunk computes).  Every
+        output tile is the same GEMM tile over the same K either way: the result is bitwise
+        independent of the chunking."""
+        ar = self.arena
+        gW, gb = ar.grad_weight(i), ar.grad_bias(i)
+        chunks = ar.chunk_buckets(i)
+        if not chunks:
+            self.ops.linear_wgrad(dz, x_in, gW, gb, ws=self.ws)
+            return
+        for b in chunks:
+            r0, r1 = b.rows
+            self.ops.linear_wgrad(dz[:, r0:r1], x_in, gW[r0:r1], gb[r0:r1], ws=self.ws)
+            yield b
 
     def _forward(self, x):
         h = x
@@ -298,6 +319,8 @@ class MLPEngine:
         main = self.stream
         self.sync.begin()
         self._sgd_done = set()
+        self._reduced = {}
+        self._pending_sgd = []
         self._first = first
         x = self.X[:rows]
         h = self._forward(x)
@@ -310,7 +333,8 @@ class MLPEngine:
         self._layer_done(last, main)
         for i in range(L - 2, -1, -1):
             x_in = self.acts[i - 1][:rows] if i > 0 else x
-            ops.linear_wgrad(dz, x_in, ar.grad_weight(i), ar.grad_bias(i), ws=self.ws)
+            for b in self._wgrad_chunks(i, dz, x_in):
+                self._bucket_reduce(b, main)      # chunk's all-reduce starts right away
             if i > 0:
                 dz_next = self._dzl(i - 1, rows)
                 ops.linear_dgrad(dz, ar.compute_weight(i), self.acts[i - 1][:rows], self.act, dz_next)
@@ -318,7 +342,7 @@ class MLPEngine:
             main.record_event(self.ev_wfree[i])
             self._layer_done(i, main)
         self._mark("bwd")
-        self.sync.finish()   # joins the comm stream into main
+        self._join_comm()
         self._mark("comm")
         rest = [b for b in ar.buckets if b.index not in self._sgd_done]
         if len(rest) == len(ar.buckets):
@@ -373,12 +397,24 @@ class MLPEngine:
     def _step_body_grouped(self, first: bool):
         rows, ops, ar, L = self.rows, self.ops, self.arena, self.L
         fz = ops.sgd_fusion(ar, self.hp, self.nesterov, first) if self.fuse_sgd else None
+        comm = self.comm_overlap
+        main = self.stream
+        if comm:
+            # several ranks, per-bucket collectives: each combine's finished layer gradient goes
+            # straight to its bucket's all-reduce on the comm stream (its SGD follows on the
+            # update stream) while the next grouped launch computes
+            self.sync.begin()
+            self._sgd_done = set()
+            self._reduced = {}
+            self._pending_sgd = []
+            self._first = first
         x = self.X[:rows]
         h = self._forward(x)
         self._mark("fwd")
         last = L - 1
         dz = self._dzl(last - 1, rows)
         unfused = []
+        pending_layer = last
         if ops.head_can_fuse_sgd(self.spec.widths[-1], self.spec.widths[-2], self.loss_kind):
             pending = ops.head_deferred(
                 h, ar.weight(last), ar.bias(last), self.Y[:rows] if self.Y is not None else None,
@@ -390,6 +426,9 @@ class MLPEngine:
             self._head(h, dz)
             pending = None
             unfused.append(last)
+            if comm:
+                main.record_event(self.ev_wfree[last])
+                self._layer_done(last, main)
         self._mark("head")
         for i in range(L - 2, -1, -1):
             x_in = self.acts[i - 1][:rows] if i > 0 else x
@@ -405,8 +444,23 @@ class MLPEngine:
             pending = ops.bwd_group(dgrad, (dz_i, x_in, ar.grad_weight(i), ar.grad_bias(i),
                                             self.ws_pair[(last - i) % 2]),
                                     fz if fuse else None, pending)
+            if comm and pending_layer == i + 1:
+                # this launch held combine_{i+1}: layer i+1's gradient is final, and its
+                # weights' last reader (dgrad_{i+1} / the head) ran in an earlier launch
+                main.record_event(self.ev_wfree[i + 1])
+                self._layer_done(i + 1, main)
+            pending_layer = i
         ops.slab_reduce(pending)
         self._mark("bwd")
+        if comm:
+            main.record_event(self.ev_wfree[0])
+            self._layer_done(0, main)
+            self._join_comm()
+            self._mark("comm")
+            for b in ar.buckets:
+                if b.index not in self._sgd_done:
+                    ops.sgd(ar, self.hp, self.nesterov, first, offset=b.offset, numel=b.numel)
+            return
         if fz is not None:
             for i in unfused:
                 s, e = ar.layer_range[i]
@@ -422,19 +476,43 @@ class MLPEngine:
         self._mark("comm")
         ops.sgd(ar, self.hp, self.nesterov, first)
 
+    def _bucket_reduce(self, b, stream):
+        """Launch bucket b's collective (once); returns the stream it completes on.  One queued
+        bucket update is issued behind every new collective, so the comm stream alternates
+        collectives and updates instead of parking a later collective behind an update that
+        waits for its weights' last reader."""
+        if b.index not in self._reduced:
+            self._reduced[b.index] = self.sync.launch_bucket(b, stream)
+            self._flush_sgd(1)
+        return self._reduced[b.index]
+
     def _layer_done(self, layer: int, stream):
-        b = self.arena.bucket_of_layer(layer)
-        if layer != min(b.layers):
-            return
-        rs = self.sync.launch_bucket(b, stream)
-        if rs is None or rs is stream:
-            return   # reduced on this stream already (single rank): update once at the end
-        with torch.cuda.stream(rs):
-            for l in b.layers:
-                rs.wait_event(self.ev_wfree[l])
-            self.ops.sgd(self.arena, self.hp, self.nesterov, self._first, offset=b.offset,
-                         numel=b.numel)
-        self._sgd_done.add(b.index)
+        """Layer ``layer``'s gradient is final and ev_wfree[layer] is recorded: reduce every
+        bucket it completes and queue each bucket's SGD (on the stream its collective completes
+        on, behind the last reader of its weights).  Updates stay on the comm stream itself: a
+        third stream in a step graph whose capture origin is the comm stream crashes hipGraph
+        instantiation on ROCm 7 (measured at 1 and 2 ranks: docs/PERF.md §3)."""
+        for b in self.arena.buckets_completed_by(layer):
+            rs = self._bucket_reduce(b, stream)
+            if rs is None or rs is stream:
+                continue   # reduced on this stream already (single rank): update once at the end
+            self._pending_sgd.append((b, rs))
+            self._sgd_done.add(b.index)
+
+    def _flush_sgd(self, n: Optional[int] = None):
+        while self._pending_sgd and (n is None or n > 0):
+            b, rs = self._pending_sgd.pop(0)
+            with torch.cuda.stream(rs):
+                for l in b.layers:
+                    rs.wait_event(self.ev_wfree[l])
+                self.ops.sgd(self.arena, self.hp, self.nesterov, self._first, offset=b.offset,
+                             numel=b.numel)
+            if n is not None:
+                n -= 1
+
+    def _join_comm(self):
+        self._flush_sgd()
+        self.sync.finish()   # joins the comm stream into the compute stream
 
     def step(self):
         """One optimizer step on the loaded batch.  Asynchronous on the GPU."""

@@ -42,12 +42,10 @@ class GradSync:
         self._done_buckets = set()
 
     def ready(self, layer: int):
-        b = self.arena.bucket_of_layer(layer)
-        if b.index in self._done_buckets:
-            return
-        if layer == min(b.layers):
-            self._done_buckets.add(b.index)
-            self._launch(b)
+        for b in self.arena.buckets_completed_by(layer):
+            if b.index not in self._done_buckets:
+                self._done_buckets.add(b.index)
+                self._launch(b)
 
     def _launch(self, bucket):
         pass
@@ -151,7 +149,7 @@ class NativeRcclSync(GradSync):
         self.bf16 = grad_dtype == "bf16"
         if self.inline and len(arena.buckets) > 1:
             # serial all-reduce: one call over the whole arena amortises the collective latency
-            arena.buckets = arena._plan_buckets(float(1 << 62), 4)
+            arena.replan_single_bucket()
         from .. import native
         self.native = native
         self.comm = native_comm

@@ -155,3 +155,29 @@ def test_rccl_reference_golden_p2_scatterv():
         assert out[r]["losses"] == pytest.approx(GOLDEN_LOSSES[2][r], rel=1e-5), r
         assert torch.allclose(out[r]["final"], torch.tensor(GOLDEN_PARAMS[2]), atol=5e-6)
     _replicas_equal(out)
+
+
+def test_rccl_grouped_overlap_two_ranks_bitwise():
+    """512-wide (grouped backward kernels) at P=2: per-bucket all-reduce overlapped on the comm
+    stream == one inline all-reduce == the gloo all-reduce, bit for bit."""
+    kw = dict(widths=[512, 512, 512, 1], n_features=512, n_samples=4096, lr=1e-4)
+    a = run_ranks_proc(_cfg(comm="native", comm_mode="overlap", **kw), 2, env_per_rank=rccl_env)
+    b = run_ranks_proc(_cfg(comm="native", comm_mode="inline", **kw), 2, env_per_rank=rccl_env)
+    c = run_ranks_proc(_cfg(comm="gloo", graph=False, **kw), 2)
+    _replicas_equal(a)
+    assert torch.equal(a[0]["final"], b[0]["final"])
+    assert torch.equal(a[0]["final"], c[0]["final"])
+
+
+def test_rccl_chunked_buckets_two_ranks_bitwise():
+    """Sub-layer (output-row chunk) buckets at P=2 on 1024-wide layers (chunking forced small
+    with NNMPI_CHUNK_MIN_TILES): chunk all-reduces overlapped == inline, bit for bit."""
+    kw = dict(widths=[1024, 1024, 1024, 1], n_features=1024, n_samples=1024, lr=1e-4,
+              bucket_mb=1.0)
+
+    def env(r):
+        return dict(rccl_env(r), NNMPI_CHUNK_MIN_TILES="4")
+    a = run_ranks_proc(_cfg(comm="native", comm_mode="overlap", **kw), 2, env_per_rank=env)
+    b = run_ranks_proc(_cfg(comm="native", comm_mode="inline", **kw), 2, env_per_rank=env)
+    _replicas_equal(a)
+    assert torch.equal(a[0]["final"], b[0]["final"])

@@ -198,3 +198,24 @@ def test_profile_steps_phase_breakdown(capsys):
                                  "comm->update"}
     assert all(v >= 0 for v in res.phase_ms.values())
     assert "[profile] mean ms per step" in capsys.readouterr().out
+
+
+def test_arena_tiny_bucket_merge_and_row_chunks():
+    """The few-KB output layer rides with the next layer's bucket; a layer bigger than a bucket
+    is cut into output-row chunks (full 256-tile waves), the last chunk holding the bias."""
+    ar = Arena([(512, 512), (512, 512), (512, 512), (1, 512)], "meta", bucket_bytes=1 << 20)
+    assert [b.layers for b in ar.buckets] == [(3, 2), (1,), (0,)]
+    big = Arena([(8192, 8192), (8192, 8192), (1, 8192)], "meta", bucket_bytes=1 << 20)
+    assert big.layer_chunks == {0: 4, 1: 4}
+    ch = big.chunk_buckets(1)
+    assert [b.rows for b in ch] == [(0, 2048), (2048, 4096), (4096, 6144), (6144, 8192)]
+    s, e = big.layer_range[1]
+    assert ch[0].offset == s and ch[-1].offset + ch[-1].numel == e        # bias in the last
+    assert all(b.numel == 2048 * 8192 for b in ch[:-1])
+    covered = sorted((b.offset, b.offset + b.numel) for b in big.buckets)
+    for (s0, e0), (s1, e1) in zip(covered, covered[1:]):
+        assert e0 == s1
+    assert big.bucket_of_layer(1) is ch[-1]
+    assert big.buckets_completed_by(1) == ch
+    # buckets larger than the layer: no chunks
+    assert Arena([(8192, 8192), (1, 8192)], "meta", bucket_bytes=1 << 30).layer_chunks == {}
