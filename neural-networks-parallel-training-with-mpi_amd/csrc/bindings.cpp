@@ -127,6 +127,16 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
                    P<const float>(y), P<const int64_t>(labels), loss, inv_count, act_prev, P<void>(dz),
                    P<float>(dl), P<float>(lp), S(s)), "head_fwd");
   });
+  m.def("head_general_workspace_bytes", &head_general_workspace_bytes);
+  m.def("head_general", [](uptr a, int a_bf16, int rows, int in, uptr W, uptr b, int out, uptr y,
+                           uptr labels, int loss, float inv_count, int act_prev, uptr dz, uptr gW,
+                           uptr gb, uptr dlogits, uptr ws, float loss_scale, uptr loss_out, uptr s) {
+    check(head_general(P<const void>(a), a_bf16, rows, in, P<const float>(W), P<const float>(b), out,
+                       P<const float>(y), P<const int64_t>(labels), loss, inv_count, act_prev,
+                       P<void>(dz), P<float>(gW), P<float>(gb), P<float>(dlogits), P<float>(ws),
+                       loss_scale, P<float>(loss_out), S(s)),
+          "head_general");
+  });
   m.def("head_can_fuse", &head_can_fuse);
   m.def("head_fused_workspace_bytes", &head_fused_workspace_bytes);
   m.def("head_fused", [](uptr a, int a_bf16, int rows, int in, uptr W, uptr b, uptr y, float inv_count,

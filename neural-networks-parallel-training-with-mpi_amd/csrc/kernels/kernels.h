@@ -127,6 +127,15 @@ hipError_t head_wgrad(const void* a, int a_bf16, int rows, int in, const float* 
                       float loss_scale, float* loss_out, hipStream_t s, const SgdFuse* sgd = nullptr,
                       SlabReduce* pending = nullptr);
 
+// ---- output layer + loss of any shape (head_general.hip): logits GEMM, loss + dlogits, dZ GEMM,
+// weight/bias gradient (split partials + ordered reduce), loss_out[0] = sum * loss_scale.
+// dlogits_out (may be null) receives a copy of dlogits [rows][out].
+size_t head_general_workspace_bytes(int rows, int in, int out);
+hipError_t head_general(const void* a, int a_bf16, int rows, int in, const float* W, const float* b,
+                        int out, const float* y, const int64_t* labels, int loss, float inv_count,
+                        int act_prev, void* dz_out, float* gW, float* gb, float* dlogits_out,
+                        float* ws, float loss_scale, float* loss_out, hipStream_t s);
+
 // ---- whole tiny MLP in one launch (tiny_mlp.hip), fp32, widths <= 16, layers <= 4 ----
 struct TinyMLPDesc {
   int n_layers;

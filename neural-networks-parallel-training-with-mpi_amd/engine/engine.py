@@ -126,10 +126,7 @@ class MLPEngine:
                 for i in range(self.L - 1):
                     if w[i] % 8 or w[i + 1] % 8:
                         raise ValueError(f"bf16 GPU path needs hidden/input widths % 8 == 0: {w}")
-            if w[-1] > 16 or w[-2] % 8:
-                raise ValueError(f"GPU head needs out <= 16 and in % 8 == 0: {w}")
-            if w[-1] * w[-2] * 4 > 65536:
-                raise ValueError("GPU head weight must fit 64 KiB of LDS")
+            # (any output layer: heads beyond the skinny kernels run on the general path)
 
     def _workspace_bytes(self) -> int:
         ops, R, w = self.ops, self.R, self.spec.widths

@@ -106,20 +106,40 @@ class HipOps:
         parts = self.head_parts(rows, in_f, out_f)
         return parts, (parts + 3) // 4 * 4 + 4   # keep the slab region 16-byte aligned
 
+    @staticmethod
+    def head_is_general(out_f: int, in_f: int) -> bool:
+        """Heads the skinny kernels (head.hip: out <= 16, an fp32 weight image within 64 KiB of
+        LDS, in % 8 == 0) do not take run on the general path (head_general.hip)."""
+        return out_f > 16 or out_f * in_f * 4 > 65536 or in_f % 8 != 0
+
     def head_workspace_bytes(self, rows, in_f, out_f, loss="mse") -> int:
+        if self.head_is_general(out_f, in_f):
+            return int(self.lib.head_general_workspace_bytes(max(rows, 1), in_f, out_f))
         _, off = self._head_split(rows, in_f, out_f)
         return max(int(self.lib.head_wgrad_workspace_bytes(rows, in_f, out_f)),
                    int(self.lib.head_fused_workspace_bytes(rows, in_f))) + 4 * off
 
     def head_can_fuse_sgd(self, out_f, in_f, loss) -> bool:
-        # both head forms end in a slab combine that can apply the update: the fused regression
-        # kernel's (out == 1, MSE) and the separate weight-gradient kernel's
-        return True
+        # both skinny head forms end in a slab combine that can apply the update: the fused
+        # regression kernel's (out == 1, MSE) and the separate weight-gradient kernel's; the
+        # general head's reducer does not (its update is a separate pass)
+        return not self.head_is_general(out_f, in_f)
 
     def head(self, a, W, b, y, labels, loss: str, inv_count: float, act_prev: str, dz_out,
              gW, gb, dlogits, loss_out, loss_scale: float, ws=None, sgd=None):
         rows, in_f = a.shape
         out_f = W.shape[0]
+        if self.head_is_general(out_f, in_f):
+            _check(sgd is None, "the general head does not fuse the optimizer update")
+            self._check_ws(ws, self.head_workspace_bytes(rows, in_f, out_f), "head")
+            _check(a.is_contiguous() and (dz_out is None or dz_out.is_contiguous()),
+                   "general head needs contiguous activations")
+            self.lib.head_general(_p(a), 1 if a.dtype == torch.bfloat16 else 0, rows, in_f, _p(W),
+                                  _p(b), out_f, _p(y), _p(labels), LOSS_CODES[loss],
+                                  float(inv_count), ACT_CODES[act_prev], _p(dz_out), _p(gW),
+                                  _p(gb), _p(dlogits), _p(ws), float(loss_scale), _p(loss_out),
+                                  self.stream)
+            return
         _check(in_f % 8 == 0, f"head needs in%8==0 (in={in_f})")
         parts, off = self._head_split(rows, in_f, out_f)
         self._check_ws(ws, self.head_workspace_bytes(rows, in_f, out_f), "head")

@@ -430,3 +430,33 @@ def test_grouped_backward_with_comm_overlap_bitwise_equal():
     b = trainer.run_worker(_cfg512(comm="none", nepochs=4))
     assert a.losses == b.losses
     assert torch.equal(a.final_params, b.final_params)
+
+
+@pytest.mark.parametrize("widths,loss", [([512, 256, 100], "xent"), ([8192, 256, 10], "xent"),
+                                         ([256, 256, 40], "mse")])
+def test_general_head_engine_vs_cpu_oracle(widths, loss):
+    """Output layers beyond the skinny head kernels train end to end (grouped / fused
+    schedules with the head's update as a separate pass) and track the CPU oracle."""
+    kw = dict(widths=widths, n_features=widths[0], loss=loss, n_samples=1024, dtype="fp32",
+              nepochs=3, lr=0.05 if loss == "xent" else 1e-4, print_rank="none",
+              data_gen="device", data_dist="local", scaling="none")
+    gpu = trainer.run_worker(TrainConfig(device="cuda", **kw))
+    import nnmpi_amd.engine.trainer as tr
+    orig = tr.build_shard
+
+    def shard_from_gpu(j):
+        jj = type("J", (), {})()
+        jj.__dict__.update(j.__dict__)
+        jj.device = torch.device("cuda")
+        X, Y, lab, part = orig(jj)
+        return X.cpu(), (Y.cpu() if Y is not None else None), (lab.cpu() if lab is not None
+                                                               else None), part
+    tr.build_shard = shard_from_gpu
+    try:
+        cpu = trainer.run_worker(TrainConfig(device="cpu", **kw))
+    finally:
+        tr.build_shard = orig
+    assert gpu.losses == pytest.approx(cpu.losses, rel=1e-4)
+    assert torch.allclose(gpu.final_params, cpu.final_params, atol=1e-5, rtol=1e-4)
+    bf = trainer.run_worker(TrainConfig(device="cuda", **dict(kw, dtype="bf16")))
+    assert bf.losses[-1] == bf.losses[-1] and bf.losses == pytest.approx(cpu.losses, rel=3e-2)
