@@ -479,8 +479,13 @@ class MLPEngine:
         collectives and updates instead of parking a later collective behind an update that
         waits for its weights' last reader."""
         if b.index not in self._reduced:
-            self._reduced[b.index] = self.sync.launch_bucket(b, stream)
-            self._flush_sgd(1)
+            if self.comm_overlap and b is self.arena.buckets[-1]:
+                # the step's last bucket: reduced on the compute stream, updated there after
+                # the join (see NativeRcclSync.launch_bucket)
+                self._reduced[b.index] = self.sync.launch_bucket(b, stream, inline=True)
+            else:
+                self._reduced[b.index] = self.sync.launch_bucket(b, stream)
+                self._flush_sgd(1)
         return self._reduced[b.index]
 
     def _layer_done(self, layer: int, stream):

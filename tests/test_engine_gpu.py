@@ -460,3 +460,27 @@ def test_general_head_engine_vs_cpu_oracle(widths, loss):
     assert torch.allclose(gpu.final_params, cpu.final_params, atol=1e-5, rtol=1e-4)
     bf = trainer.run_worker(TrainConfig(device="cuda", **dict(kw, dtype="bf16")))
     assert bf.losses[-1] == bf.losses[-1] and bf.losses == pytest.approx(cpu.losses, rel=3e-2)
+
+
+@pytest.mark.parametrize("cfg", ["bf16_512", "mnist_xent", "reference_fp32"])
+def test_gpu_checkpoint_resume_is_bitwise(tmp_path, cfg):
+    """Checkpoint after 3 epochs (rank-0 reference-format state_dict + momentum arena), resume
+    in a fresh job and finish: bitwise equal to the uninterrupted run (bf16 compute: the shadow
+    is re-derived from the fp32 master on load, the momentum-first-step flag from the step
+    counter)."""
+    ck = str(tmp_path / "model.pt")
+    if cfg == "bf16_512":
+        mk = lambda **k: _cfg512(**k)  # noqa: E731
+    elif cfg == "mnist_xent":
+        mk = lambda **k: TrainConfig(device="cuda", widths=[784, 1024, 1024, 10], n_features=784,  # noqa: E731
+                                     loss="xent", n_samples=2048, dtype="bf16", lr=0.05,
+                                     print_rank="none", data_gen="device", data_dist="local", **k)
+    else:
+        mk = lambda **k: TrainConfig(device="cuda", print_rank="none", **k)  # noqa: E731
+    full = trainer.run_worker(mk(nepochs=5))
+    trainer.run_worker(mk(nepochs=3, checkpoint=ck))
+    res = trainer.run_worker(mk(nepochs=5, resume=ck))
+    assert res.losses == full.losses[3:]
+    assert torch.equal(res.final_params, full.final_params)
+    sd = torch.load(ck, weights_only=True)
+    assert all(k.startswith("layers.") for k in sd)
