@@ -479,13 +479,8 @@ class MLPEngine:
         collectives and updates instead of parking a later collective behind an update that
         waits for its weights' last reader."""
         if b.index not in self._reduced:
-            if self.comm_overlap and b is self.arena.buckets[-1]:
-                # the step's last bucket: reduced on the compute stream, updated there after
-                # the join (see NativeRcclSync.launch_bucket)
-                self._reduced[b.index] = self.sync.launch_bucket(b, stream, inline=True)
-            else:
-                self._reduced[b.index] = self.sync.launch_bucket(b, stream)
-                self._flush_sgd(1)
+            self._reduced[b.index] = self.sync.launch_bucket(b, stream)
+            self._flush_sgd(1)
         return self._reduced[b.index]
 
     def _layer_done(self, layer: int, stream):
@@ -513,8 +508,25 @@ class MLPEngine:
                 n -= 1
 
     def _join_comm(self):
-        self._flush_sgd()
+        """Join the comm stream into the compute stream.  Updates still queued at this point
+        (the last buckets) run after the join on the compute stream, merged into one SGD launch
+        per contiguous range, instead of as a serial tail of small launches on the comm stream
+        in front of the join."""
+        tail = self._pending_sgd
+        self._pending_sgd = []
         self.sync.finish()   # joins the comm stream into the compute stream
+        tail.sort(key=lambda br: br[0].offset)
+        i = 0
+        while i < len(tail):
+            s0 = tail[i][0].offset
+            e0 = s0 + tail[i][0].numel
+            j = i + 1
+            while j < len(tail) and tail[j][0].offset == e0:
+                e0 += tail[j][0].numel
+                j += 1
+            self.ops.sgd(self.arena, self.hp, self.nesterov, self._first, offset=s0,
+                         numel=e0 - s0)
+            i = j
 
     def step(self):
         """One optimizer step on the loaded batch.  Asynchronous on the GPU."""

@@ -160,7 +160,7 @@ class NativeRcclSync(GradSync):
                      if self.bf16 else None)
         self._comm_stream = torch.cuda.ExternalStream(self.gs.comm_stream)
 
-    def _launch(self, bucket, stream=None, inline=None):
+    def _launch(self, bucket, stream=None):
         view = self.arena.grad[bucket.offset:bucket.offset + bucket.numel]
         self.seq += 1
         h = int(stream.cuda_stream) if stream is not None else self.native.stream_handle()
@@ -169,7 +169,7 @@ class NativeRcclSync(GradSync):
         if self.bf16:
             ptr, dt = self.gbuf[bucket.offset:].data_ptr(), 1
             lib.cast_f32_bf16(view.data_ptr(), ptr, bucket.numel, h)
-        if self.inline or inline:
+        if self.inline:
             if self.mode == "root":
                 # reference pattern (ref.py:185-203): everything through rank 0
                 self.comm.reduce(ptr, bucket.numel, dt, 0, 0, h)
@@ -184,13 +184,13 @@ class NativeRcclSync(GradSync):
             lib.cast_bf16_f32(ptr, view.data_ptr(), bucket.numel, self.gs.comm_stream)
         self._launched = True
 
-    def launch_bucket(self, bucket, stream, inline: bool = False):
-        """``inline=True``: this bucket's collective on ``stream`` itself even in the
-        comm-stream schedule (the step's LAST bucket: nothing is left to overlap it with, and a
-        hop to the comm stream and back would only add two cross-queue dependencies to the
-        step's critical path)."""
-        self._launch(bucket, stream, inline=inline)
-        return None if (self.inline or inline) else self._comm_stream
+    def launch_bucket(self, bucket, stream):
+        # NB: every collective of one communicator stays on ONE stream -- a bucket issued on
+        # the compute stream while earlier ones are still queued on the comm stream lets the two
+        # run concurrently on the GPU, in different orders on different ranks: measured to hang
+        # (and, inside a capture, to crash) at P = 2 / 3
+        self._launch(bucket, stream)
+        return None if self.inline else self._comm_stream
 
     def capture_origin(self):
         return None if self.inline else self._comm_stream
