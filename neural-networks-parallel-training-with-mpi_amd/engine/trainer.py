@@ -278,6 +278,27 @@ def _gather_state(eng, sync):
         sync.gather_state()
 
 
+def _comm_only_ms(j: "Job", sync, reps: int = 10) -> float:
+    """Milliseconds per repetition of one step's gradient collectives alone (same buckets,
+    dtype and order; max over ranks)."""
+    cuda = j.device.type == "cuda"
+
+    def sync_dev():
+        if cuda:
+            torch.cuda.synchronize()
+    sync.comm_only()           # warm-up (RCCL sets up channels lazily)
+    sync_dev()
+    j.pg.barrier()
+    t0 = time.perf_counter()
+    for _ in range(reps):
+        sync.comm_only()
+    sync_dev()
+    el = torch.tensor([(time.perf_counter() - t0) / reps * 1e3], dtype=torch.float64)
+    import torch.distributed as dist
+    j.pg.allreduce_cpu(el, op=dist.ReduceOp.MAX)
+    return float(el.item())
+
+
 def _fault_injection(rank: int) -> Optional[int]:
     """``NNMPI_FAULT_INJECT=<rank>:<epoch>``: that rank raises at the start of that epoch while
     its peers are blocked in the step's collectives -- the reference's deadlock scenario
@@ -447,8 +468,13 @@ def _run(j: Job) -> TrainResult:
             res.phase_ms = eng.timer.summary_ms()
             _print(cfg, rank, "[profile] mean ms per step: " +
                    ", ".join(f"{k} {v:.4f}" for k, v in res.phase_ms.items()))
-            comm_ms = res.phase_ms.get("bwd->comm")
-            metrics.write(profile_ms_per_step=res.phase_ms, rank=rank,
+            # the phase times come from eagerly launched, event-bracketed steps (a replayed
+            # graph has no host-visible phase boundaries); the bus bandwidth is NOT derived from
+            # them -- in the overlapped schedule "bwd->comm" is only the join tail -- but from
+            # the step's collectives timed alone
+            comm_ms = _comm_only_ms(j, sync) if world > 1 else None
+            metrics.write(profile_ms_per_step=res.phase_ms, phase_timing="eager", rank=rank,
+                          comm_only_ms=comm_ms,
                           comm_bus_GBps=comm_bus_gbps(cvol["wire_bytes_per_rank"], comm_ms))
         _gather_state(eng, sync)
         if cfg.checkpoint and rank == 0:

@@ -36,6 +36,7 @@ class GradSync:
     def __init__(self, arena):
         self.arena = arena
         self._pending_layers = set()
+        self._done_buckets = set()
         self.seq = 0  # collective sequence number (for the sequence checker)
 
     def begin(self):

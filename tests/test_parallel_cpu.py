@@ -305,3 +305,16 @@ def test_one_rank_failure_ends_every_rank(fail_rank):
     assert elapsed < timeout_s + 10 + 30, elapsed
     err = procs[fail_rank].stderr.read()
     assert "injected fault" in err
+
+
+def test_profile_metrics_bus_bandwidth_from_comm_only(tmp_path):
+    """--profile_steps: the per-phase times are labelled eager, and the bus bandwidth comes from
+    the step's collectives timed alone (not from the join tail of the overlapped step)."""
+    import json
+    mj = str(tmp_path / "m.jsonl")
+    run_ranks(TrainConfig(device="cpu", print_rank="none", metrics_json=mj, profile_steps=True,
+                          widths=[64, 64, 1], n_features=64, n_samples=256), 2)
+    lines = [json.loads(l) for l in open(mj)]
+    prof = [l for l in lines if "profile_ms_per_step" in l]
+    assert prof and prof[0]["phase_timing"] == "eager"
+    assert prof[0]["comm_only_ms"] > 0 and prof[0]["comm_bus_GBps"] > 0
