@@ -265,7 +265,7 @@ def run(a, job):
             labels = None
         return part, X.to(dtype), Y, labels
 
-    def build(mode, data, comm=True):
+    def build(mode, data, comm=True, bucket_mb=None):
         """One arena + gradient-sync strategy + engine over ``data`` (a shard()).
         mode: inline | overlap | zero1 | none (no gradient synchronisation at all)."""
         part, X, Y, labels = data
@@ -274,7 +274,8 @@ def run(a, job):
         zero1 = mode == "zero1" and comm
         arena = Arena([spec.layer_shape(i) for i in range(spec.n_layers)], dev,
                       shadow_dtype=torch.bfloat16 if dtype == torch.bfloat16 else None,
-                      bucket_bytes=a.bucket_mb * 2 ** 20, pad_to=64 * world if zero1 else 64)
+                      bucket_bytes=(bucket_mb or a.bucket_mb) * 2 ** 20,
+                      pad_to=64 * world if zero1 else 64)
         arena.bind_model(model)
         del model
         if not comm or not use_comm:
@@ -347,17 +348,25 @@ def run(a, job):
     elif native_comm is None and mode == "tune":
         mode = "inline"
     tune = None
+    bucket_mb = a.bucket_mb
     if mode == "tune":
         tune = {}
         eng = None
-        for m in ("inline", "zero1", "overlap"):
-            e = build(m, data)
+        # overlap candidates: --bucket_mb buckets, and ~two buckets (the first all-reduce
+        # larger, the exposed last one smaller than the whole gradient)
+        half_mb = round(grad_bytes / 2 ** 20 * 0.6, 3)
+        cands = [("inline", None), ("zero1", None), ("overlap", a.bucket_mb)]
+        if half_mb > a.bucket_mb:
+            cands.append(("overlap", half_mb))
+        for m, bmb in cands:
+            e = build(m, data, bucket_mb=bmb)
             e.run_steps(a.warmup, chunk)
             tm = min(timed(e, a.tune_steps, chunk) for _ in range(2))
-            tune[m] = round(tm / a.tune_steps * 1e3, 5)
+            key = m if bmb in (None, a.bucket_mb) else f"{m}_{bmb}mb"
+            tune[key] = round(tm / a.tune_steps * 1e3, 5)
             # every rank sees the same max-over-ranks times, so every rank keeps the same mode
             if eng is None or tm < best_t:
-                eng, best_t, mode = e, tm, m
+                eng, best_t, mode, bucket_mb = e, tm, m, (bmb or a.bucket_mb)
             del e
         if gpu:
             torch.cuda.empty_cache()
@@ -383,6 +392,7 @@ def run(a, job):
     ms = elapsed / a.steps * 1e3
     value = n_global * a.steps / elapsed
     sharded = mode == "zero1"
+    n_buckets = len(eng.arena.buckets)
     wire = comm_volume(eng.arena.numel, world, grad_dtype, sharded=sharded,
                        shadow=eng.arena.shadow is not None)["wire_bytes_per_rank"]
 
@@ -422,7 +432,7 @@ def run(a, job):
             # strong scaling: the reference's fixed dataset (the 1-GPU shard, 8192 rows for the
             # proxy) split over the N ranks
             sdata = shard(rows_pg)
-            e = build(mode if mode != "none" else "inline", sdata)
+            e = build(mode if mode != "none" else "inline", sdata, bucket_mb=bucket_mb)
             e.run_steps(min(a.warmup, 10) + 1, chunk)
             s_ms = timed(e, n_ex, chunk) / n_ex * 1e3
             del e, sdata
@@ -468,7 +478,8 @@ def run(a, job):
                        "comm_tune_ms_per_step": tune,
                        "grad_dtype": grad_dtype if use_comm else None,
                        "grad_wire_bytes_per_rank": wire,
-                       "bucket_mb": a.bucket_mb},
+                       "bucket_mb": bucket_mb,
+                       "n_buckets": n_buckets},
             "rccl_ranks": (native_comm.size if native_comm is not None else None),
             "shared_gpu_rehearsal": bool(a.shared_gpu_rehearsal),
             "model_tflops_per_s": round(tflops, 2),

@@ -102,7 +102,7 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
     assert d["n_gpus"] == 2 and d["rccl_ranks"] == 2 and d["shared_gpu_rehearsal"]
     assert d["config"]["comm"] == "rccl" and d["config"]["comm_mode"] in ("inline", "zero1",
                                                                          "overlap")
-    assert set(d["config"]["comm_tune_ms_per_step"]) == {"inline", "zero1", "overlap"}
+    assert {"inline", "zero1", "overlap"} <= set(d["config"]["comm_tune_ms_per_step"])
     assert d["parallel_efficiency"] is not None and d["comm_bus_gbps"] is not None
     assert d["strong_scaling"]["global_batch"] == 8192
     assert d["final_loss"] == d["final_loss"]
