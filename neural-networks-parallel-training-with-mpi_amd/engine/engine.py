@@ -398,8 +398,8 @@ class MLPEngine:
         main = self.stream
         if comm:
             # several ranks, per-bucket collectives: each combine's finished layer gradient goes
-            # straight to its bucket's all-reduce on the comm stream (its SGD follows on the
-            # update stream) while the next grouped launch computes
+            # straight to its bucket's all-reduce on the comm stream (its SGD follows there)
+            # while the next grouped launch computes
             self.sync.begin()
             self._sgd_done = set()
             self._reduced = {}
@@ -422,6 +422,7 @@ class MLPEngine:
         else:
             self._head(h, dz)
             pending = None
+            pending_layer = None          # the head's gradient is already final
             unfused.append(last)
             if comm:
                 main.record_event(self.ev_wfree[last])

@@ -539,3 +539,17 @@ def test_bf16_gradients_per_layer_vs_oracle(widths, loss):
             a, b = g[li][k], r[li][k]
             rel = float((a - b).norm() / b.norm().clamp_min(1e-30))
             assert rel < 1e-2, (li, k, rel)
+
+
+def test_general_head_with_comm_overlap_bitwise_equal():
+    """A head the skinny kernels do not take (its gradient is final right after the head, not
+    in the first grouped launch) through the comm-overlapped grouped schedule: every bucket
+    updated exactly once -- bitwise equal to the communication-free run."""
+    kw = dict(widths=[512, 256, 100], n_features=512, loss="xent", n_samples=2048, dtype="bf16",
+              nepochs=4, lr=0.05, print_rank="none", data_gen="device", data_dist="local",
+              scaling="none")
+    a = trainer.run_worker(TrainConfig(device="cuda", comm="native", comm_mode="overlap",
+                                       bucket_mb=0.1, **kw))
+    b = trainer.run_worker(TrainConfig(device="cuda", comm="none", **kw))
+    assert a.losses == b.losses
+    assert torch.equal(a.final_params, b.final_params)
