@@ -106,3 +106,22 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
     assert d["parallel_efficiency"] is not None and d["comm_bus_gbps"] is not None
     assert d["strong_scaling"]["global_batch"] == 8192
     assert d["final_loss"] == d["final_loss"]
+
+
+def test_bench_under_torchrun_driver_command():
+    """The driver's exact launch form: torch.distributed.run --nnodes=1 --nproc-per-node N
+    --master-addr 127.0.0.1 --master-port P bench.py --gpus N (CPU plumbing here)."""
+    import socket
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    e = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        str(port), BENCH, "--gpus", "2", "--device", "cpu", "--config", "ref",
+                        "--steps", "6", "--warmup", "2"], capture_output=True, text=True,
+                       timeout=300, env=e)
+    d = _line(r)
+    assert d["n_gpus"] == 2 and d["steps"] == 6 and d["config"]["parallelism"] == "dp2"
