@@ -77,6 +77,13 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
   m.def("set_gemm_tile", &set_gemm_tile);
   m.def("set_gemm_variant", &set_gemm_variant);
   m.def("set_fwd_variant", &set_fwd_variant);
+  m.def("set_store_policy", &set_store_policy);
+  m.def("linear_fwd_bf16_stamped", [](uptr X, int ldx, uptr W, int ldw, uptr bias, uptr Y, int ldy,
+                                      int M, int N, int K, uptr st, uptr s) {
+    check(linear_fwd_bf16_stamped(P<const bf16>(X), ldx, P<const bf16>(W), ldw, P<const float>(bias),
+                                  P<bf16>(Y), ldy, M, N, K, P<unsigned long long>(st), S(s)),
+          "linear_fwd_bf16_stamped");
+  });
   m.def("set_group_async", &set_group_async);
   m.def("set_wgrad_splits", &set_wgrad_splits);
   m.def("wgrad_workspace_bytes", &wgrad_workspace_bytes);

@@ -51,7 +51,27 @@ struct GemmParams {
   long long bg_split_stride;
   unsigned a_bytes, b_bytes;  // extents of A / B storage (buffer-resource range, DMA path)
   SgdFuse sg;                 // EPI_F32 without split-K: apply the optimizer instead of storing
+  int store_pol;              // epilogue output stores: 0 plain, 1 nt, 2 sc1 (write-through)
 };
+
+// Epilogue output store of 16 bytes with a selectable cache policy (experiments: what the
+// kernel leaves dirty in L2 is written back at the launch boundary, MI355X_MICROARCH.md
+// "boundary" row; nt / sc1 stores move that traffic into the epilogue).  Vector stores only.
+template <typename V>
+__device__ __forceinline__ void store16(V* ptr, const V& v, int pol) {
+  static_assert(sizeof(V) == 16, "16-byte store");
+  if (pol == 1) {
+    typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+    __builtin_nontemporal_store(__builtin_bit_cast(u32x4, v), reinterpret_cast<u32x4*>(ptr));
+  } else if (pol == 2) {
+    typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+    const u32x4 d = __builtin_bit_cast(u32x4, v);
+    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(ptr), "v"(d) : "memory");
+  } else {
+    *ptr = v;
+  }
+}
+static int g_store_pol = 0;   // host: store16 policy the launches put in GemmParams (0 plain)
 
 // s_waitcnt with only the vector-memory counter constrained (lgkm/exp counters left free).
 __device__ __forceinline__ constexpr int waitcnt_vm(int n) {
@@ -441,8 +461,8 @@ __device__ __forceinline__ void lds_epilogue(const GemmParams& p,
         sgd_fused_store4(p.sg, g, v0);
         sgd_fused_store4(p.sg, g + 4, v1);
       } else {
-        *reinterpret_cast<f32x4*>(g) = v0;
-        *reinterpret_cast<f32x4*>(g + 4) = v1;
+        store16(reinterpret_cast<f32x4*>(g), v0, p.store_pol);
+        store16(reinterpret_cast<f32x4*>(g + 4), v1, p.store_pol);
       }
     } else {
       bf16x8 o;
@@ -456,7 +476,8 @@ __device__ __forceinline__ void lds_epilogue(const GemmParams& p,
           o[e + 4] = (bf16)(v1[e] * act_bwd_t<ACT>((float)aux[it][e + 4]));
         }
       }
-      *reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(p.C) + (long long)gm * p.ldc + gn) = o;
+      store16(reinterpret_cast<bf16x8*>(reinterpret_cast<bf16*>(p.C) + (long long)gm * p.ldc + gn), o,
+              p.store_pol);
     }
   }
 }
@@ -713,6 +734,42 @@ __global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_dma_kernel(GemmParam
   const int gx = gridDim.x, gy = gridDim.y;
   const int bid = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy);
   dma_gemm_tile<BM, BN, WGM, WGN, LA, LB, EPI, ACT, BIASGRAD, NS>(p, smem, bid % gx, bid / gx, blockIdx.z);
+}
+
+// Diagnostic twin of gemm_bf16_dma_kernel: every block records the constant 100 MHz real-time
+// counter at entry and after its last store has retired (per-lane vector stores of two lanes,
+// never a scalar store), so dispatch skew, per-block span and the launch's own overhead can be
+// separated (scripts/stamp_fwd.py).  Not used by the training step.
+template <int BM, int BN, int WGM, int WGN, int LA, int LB, int EPI, int ACT, bool BIASGRAD, int NS>
+__global__ void __launch_bounds__(64 * WGM * WGN) gemm_bf16_dma_stamp_kernel(GemmParams p,
+                                                                           unsigned long long* st) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const unsigned long long t0 = __builtin_amdgcn_s_memrealtime();
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int lin = blockIdx.y * gx + blockIdx.x;
+  const int bid = xcd_remap(lin, gx * gy);
+  dma_gemm_tile<BM, BN, WGM, WGN, LA, LB, EPI, ACT, BIASGRAD, NS>(p, smem, bid % gx, bid / gx, blockIdx.z);
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  const unsigned long long t1 = __builtin_amdgcn_s_memrealtime();
+  if (threadIdx.x < 2) st[2 * lin + threadIdx.x] = threadIdx.x ? t1 : t0;
+}
+
+hipError_t linear_fwd_bf16_stamped(const bf16* X, int ldx, const bf16* W, int ldw, const float* bias,
+                                   bf16* Y, int ldy, int M, int N, int K, unsigned long long* stamps,
+                                   hipStream_t s) {
+  GemmParams p{};
+  p.A = X; p.lda = ldx; p.B = W; p.ldb = ldw; p.M = M; p.N = N; p.K = K;
+  p.k_per_split = ((K + GEMM_BK - 1) / GEMM_BK) * GEMM_BK;
+  p.C = Y; p.ldc = ldy; p.bias = bias;
+  const long long a = (long long)(p.M - 1) * p.lda + p.K, b = (long long)(p.N - 1) * p.ldb + p.K;
+  p.a_bytes = (unsigned)std::min<long long>(a * 2, DMA_OOB - 16);
+  p.b_bytes = (unsigned)std::min<long long>(b * 2, DMA_OOB - 16);
+  constexpr int smem = 2 * (128 + 128) * GEMM_BK * 2;
+  auto kfn = gemm_bf16_dma_stamp_kernel<128, 128, 2, 4, KMAJ, KMAJ, EPI_BIAS_ACT, ACT_RELU, false, 2>;
+  (void)hipFuncSetAttribute((const void*)kfn, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+  hipLaunchKernelGGL(kfn, dim3((N + 127) / 128, (M + 127) / 128, 1), dim3(512), smem, s, p, stamps);
+  return hipGetLastError();
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1102,6 +1159,7 @@ static hipError_t launch_dma(GemmParams p, int splits, hipStream_t s) {
   dim3 grid((p.N + BN - 1) / BN, (p.M + BM - 1) / BM, splits);
   constexpr int smem = NS * (BM + BN) * GEMM_BK * 2;
   set_extents<LA, LB>(p);
+  p.store_pol = g_store_pol;
   auto kfn = gemm_bf16_dma_kernel<BM, BN, WGM, WGN, LA, LB, EPI, ACT, BG, NS>;
   static bool attr = false;
   if (!attr) {
@@ -1125,6 +1183,7 @@ constexpr int GROUP_ASYNC_DEFAULT = 2;   // measured: 102.3 -> 97.9 us/step (pro
 void set_fwd_variant(int v) { g_fwd_variant = v; }
 void set_group_async(int m) { g_group_async = m; }
 void set_wgrad_splits(int s) { g_wgrad_splits = s; }
+void set_store_policy(int p) { g_store_pol = p; }
 
 template <int BM, int BN, int LA, int LB, int EPI, int ACT, bool BG>
 static hipError_t launch_t(GemmParams p, int splits, hipStream_t s, int variant = -1) {
@@ -1450,6 +1509,8 @@ hipError_t bwd_group(const DgradArgs* dg, const WgradArgs* wg, const SlabReduce*
     g.nb_main = nb_main;
     g.nb_bias = nb_bias;
   }
+  g.dg.store_pol = g_store_pol;
+  g.wg.store_pol = g_store_pol;
   const int nb = g.dg_blocks + g.wg_blocks + nbr;
   if (nb == 0) return hipSuccess;
   const int act = dg ? dg->act : ACT_NONE;

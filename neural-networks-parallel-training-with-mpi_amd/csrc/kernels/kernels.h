@@ -57,6 +57,12 @@ void set_gemm_tile(int t);     // 0 = heuristic, 64 / 128 = force (experiments)
 void set_gemm_variant(int v);  // DMA-path main-loop variant (experiments), 0 = default
 // step-level kernel-selection knobs (-1 / 0 = built-in default; scripts/step_ab.py)
 void set_fwd_variant(int v);   // forward GEMM (128x128 tiles) main-loop variant
+void set_store_policy(int p);  // LDS-epilogue output stores: 0 plain, 1 nt, 2 sc1 (experiments)
+// diagnostic: the default 128x128 forward kernel with per-block entry/exit real-time stamps
+// (stamps: 2 * grid uint64, 100 MHz counter)
+hipError_t linear_fwd_bf16_stamped(const bf16* X, int ldx, const bf16* W, int ldw, const float* bias,
+                                   bf16* Y, int ldy, int M, int N, int K, unsigned long long* stamps,
+                                   hipStream_t s);
 void set_group_async(int m);   // grouped backward LDS read mode: 0 compiler, 1 stage, 2 k-half
 void set_wgrad_splits(int s);  // upper bound on the weight-gradient split-K factor
 size_t wgrad_workspace_bytes(int M, int N, int K);
