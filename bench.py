@@ -116,6 +116,8 @@ def parse(argv=None):
                         "NCCL_HOSTID, RCCL over loopback) to rehearse the multi-rank code path on "
                         "a 1-GPU box; the JSON line says so and its numbers are not a measurement")
     p.add_argument("--fwd_variant", type=int, default=-1, help="forward GEMM variant (experiments)")
+    p.add_argument("--head_xcd_rows", type=int, default=0,
+                   help="head kernels take XCD-remapped row blocks (experiments)")
     p.add_argument("--store_policy", type=int, default=0,
                    help="GEMM epilogue output stores: 0 plain, 1 nt, 2 sc1 (experiments)")
     p.add_argument("--group_async", type=int, default=-1,
@@ -224,6 +226,7 @@ def run(a, job):
         native.lib().set_fwd_variant(a.fwd_variant)
         native.lib().set_group_async(a.group_async)
         native.lib().set_store_policy(a.store_policy)
+        native.lib().set_head_xcd_rows(a.head_xcd_rows)
         torch.cuda.set_device(job.local_rank % torch.cuda.device_count())
         dev = torch.device("cuda", torch.cuda.current_device())
         from nnmpi_amd.ops.hip_ops import HipOps

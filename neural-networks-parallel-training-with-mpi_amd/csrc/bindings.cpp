@@ -78,6 +78,7 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
   m.def("set_gemm_variant", &set_gemm_variant);
   m.def("set_fwd_variant", &set_fwd_variant);
   m.def("set_store_policy", &set_store_policy);
+  m.def("set_head_xcd_rows", &set_head_xcd_rows);
   m.def("linear_fwd_bf16_stamped", [](uptr X, int ldx, uptr W, int ldw, uptr bias, uptr Y, int ldy,
                                       int M, int N, int K, uptr st, uptr s) {
     check(linear_fwd_bf16_stamped(P<const bf16>(X), ldx, P<const bf16>(W), ldw, P<const float>(bias),

@@ -32,7 +32,11 @@ struct HeadArgs {
   void* dz_prev;
   float* dlogits;
   float* loss_part;
+  int xcd_rows;   // 1: rows of an XCD-remapped logical block (set_head_xcd_rows; experiment)
 };
+
+static int g_head_xcd_rows = 0;
+void set_head_xcd_rows(int v) { g_head_xcd_rows = v; }
 
 template <typename TA>
 __device__ __forceinline__ void load8(const TA* p, float (&v)[8]) {
@@ -121,7 +125,11 @@ __global__ void __launch_bounds__(64 * HW) head_fwd_kernel(HeadArgs p, float* __
 #pragma unroll
   for (int o = 0; o < OUTM; ++o) bias[o] = p.b[min(o, nout - 1)];
 
-  const int gw = blockIdx.x * HW + w, nwaves = gridDim.x * HW;
+  // rows of an XCD-contiguous logical block: the forward GEMM left these rows' activations in
+  // the L2 of the XCD this block runs on (its tiles use the same xcd_remap), and the backward
+  // launches read this block's dZ rows from there too
+  const int lb = p.xcd_rows ? xcd_remap(blockIdx.x, gridDim.x) : (int)blockIdx.x;
+  const int gw = lb * HW + w, nwaves = gridDim.x * HW;
   for (int r0 = gw * RPW; r0 < p.rows; r0 += nwaves * RPW) {
     // Multi-output heads read W from LDS for every row: an offset the compiler cannot see
     // through keeps it from hoisting all OUTM x CMAX x 8 weights into registers across the row
@@ -401,7 +409,13 @@ __global__ void __launch_bounds__(64 * MH_WAVES) head_mfma_kernel(HeadArgs p) {
   // software pipeline: the global loads of a block's next row group are issued before the
   // current one is computed (first group: before the W image is built)
   MhLoads<Q> cur, nxt;
-  mh_load<Q, LOSS>(cur, p, A, min((int)blockIdx.x * 16 + r, p.rows - 1), w, g);
+  // a contiguous run of row groups per XCD-remapped block (same XCD as the forward tiles that
+  // wrote these rows: L2 hits instead of Infinity-Cache reads)
+  const int per = p.xcd_rows ? (ngroups + (int)gridDim.x - 1) / (int)gridDim.x : 1;
+  const int g_beg = p.xcd_rows ? xcd_remap(blockIdx.x, gridDim.x) * per : (int)blockIdx.x;
+  const int g_end = p.xcd_rows ? min(ngroups, g_beg + per) : ngroups;
+  const int g_step = p.xcd_rows ? 1 : (int)gridDim.x;
+  mh_load<Q, LOSS>(cur, p, A, min(g_beg * 16 + r, p.rows - 1), w, g);
   // W image: 16-byte loads, all issued before the first LDS store (compile-time trip count)
   constexpr int NV = 16 * in / 4 / (64 * MH_WAVES);
   f32x4 wv[NV];
@@ -421,11 +435,11 @@ __global__ void __launch_bounds__(64 * MH_WAVES) head_mfma_kernel(HeadArgs p) {
 #pragma unroll
   for (int j = 0; j < 4; ++j) bias[j] = (4 * g + j) < out ? p.b[4 * g + j] : 0.f;
   float block_loss = 0.f;
-  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+  for (int grp = g_beg; grp < g_end; grp += g_step) {
     const int row = grp * 16 + r;
     const bool valid = row < p.rows;
     // next group's loads (past the end: the last row again, never read back)
-    mh_load<Q, LOSS>(nxt, p, A, min((grp + (int)gridDim.x) * 16 + r, p.rows - 1), w, g);
+    mh_load<Q, LOSS>(nxt, p, A, min((grp + g_step) * 16 + r, p.rows - 1), w, g);
     __builtin_amdgcn_sched_barrier(0);
     const bf16x8* xs = cur.xs;
     // ---- logits: this wave's quarter of the features ----
@@ -575,7 +589,8 @@ static hipError_t head_fwd_impl(const void* a, int a_bf16, int rows, int in, con
   if (out < 1 || out > HEAD_OMAX || in % 8 != 0 || in > 8192) return hipErrorInvalidValue;
   const size_t smem = (size_t)(out * in + (fuse ? head_waves(in) * in : 0)) * sizeof(float);
   if (smem > 65536 + 32768) return hipErrorInvalidValue;
-  HeadArgs h{a, rows, in, W, b, out, y, labels, inv_count, act_prev, dz_prev, dlogits, loss_part};
+  HeadArgs h{a, rows, in, W, b, out, y, labels, inv_count, act_prev, dz_prev, dlogits, loss_part,
+             g_head_xcd_rows};
   const int blocks = head_fwd_parts(rows, in, out);
   if (head_mfma_ok(a_bf16, in, out, fuse)) return head_mfma_launch(h, act_prev, loss, blocks, s);
 #define HL(TA, LS, FU, OM) head_launch_c<TA, LS, FU, OM>(h, act_prev, blocks, smem, wslab, bslab, s)
