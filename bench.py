@@ -405,7 +405,11 @@ def run(a, job):
     # ---------------- after the timed region: what the BASELINE metric derives from it ----------
     extras = {}
     strong = None
-    if not a.no_extras:
+    extras_error = None
+
+    def run_extras():
+        nonlocal eng, data
+        ex, st = {}, None
         n_ex = max(1, min(a.steps, EXTRA_STEPS))
         comm_ms = None
         if use_comm:
@@ -419,8 +423,7 @@ def run(a, job):
                                       max_over_ranks) * 1e3
             with torch.no_grad():
                 eng.arena.grad.zero_()
-        rows_local = data[0].rows(rank)
-        del eng
+        eng = None
         if gpu:
             torch.cuda.empty_cache()
         if use_comm:
@@ -431,9 +434,9 @@ def run(a, job):
             del e
         else:
             comp_ms = ms
-        extras = scaling_report(world, max(data[0].counts), n_global, ms, comp_ms, comm_ms, wire)
-        extras["single_gpu_ms_per_step"] = comp_ms
-        del data
+        ex = scaling_report(world, max(data[0].counts), n_global, ms, comp_ms, comm_ms, wire)
+        ex["single_gpu_ms_per_step"] = comp_ms
+        data = None
         if world > 1 and a.scaling == "weak":
             # strong scaling: the reference's fixed dataset (the 1-GPU shard, 8192 rows for the
             # proxy) split over the N ranks
@@ -444,13 +447,24 @@ def run(a, job):
             del e, sdata
             # S(1): the single-GPU step of the whole dataset = the compute-only step above
             # (weak scaling gives every rank rows_pg rows, the last one rows_pg - 1)
-            strong = {"global_batch": rows_pg, "ms_per_step": round(s_ms, 5),
-                      "samples_per_s": round(rows_pg / (s_ms * 1e-3), 1),
-                      "parallel_efficiency": round(comp_ms / (world * s_ms), 4)}
+            st = {"global_batch": rows_pg, "ms_per_step": round(s_ms, 5),
+                  "samples_per_s": round(rows_pg / (s_ms * 1e-3), 1),
+                  "parallel_efficiency": round(comp_ms / (world * s_ms), 4)}
             base = BASELINE_SAMPLES_PER_S.get(world) if a.config == "proxy512" else None
-            strong["vs_baseline"] = round(strong["samples_per_s"] / base, 2) if base else None
+            st["vs_baseline"] = round(st["samples_per_s"] / base, 2) if base else None
         if gpu:
             torch.cuda.empty_cache()
+        return ex, st
+
+    if not a.no_extras:
+        # the timed result above stands on its own: a failure in these extra measurements is
+        # reported in the JSON line instead of losing the line
+        try:
+            extras, strong = run_extras()
+        except Exception as exc:   # noqa: BLE001
+            extras_error = f"{type(exc).__name__}: {exc}"[:300]
+            print(f"[bench] extras failed on rank {rank}: {extras_error}", file=sys.stderr,
+                  flush=True)
 
     base = BASELINE_SAMPLES_PER_S.get(world) if a.config == "proxy512" else None
     tflops = spec.flops_per_sample() * n_global / (ms * 1e-3) / 1e12
@@ -497,6 +511,7 @@ def run(a, job):
             "overlap_pct": rnd(extras.get("overlap_pct"), 1),
             "comm_bus_gbps": rnd(extras.get("comm_bus_gbps"), 2),
             "strong_scaling": strong,
+            "extras_error": extras_error,
             "loss_after_warmup": loss0,
             "final_loss": loss,
         }
