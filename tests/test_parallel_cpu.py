@@ -318,3 +318,21 @@ def test_profile_metrics_bus_bandwidth_from_comm_only(tmp_path):
     prof = [l for l in lines if "profile_ms_per_step" in l]
     assert prof and prof[0]["phase_timing"] == "eager"
     assert prof[0]["comm_only_ms"] > 0 and prof[0]["comm_bus_GBps"] > 0
+
+
+def test_row_chunk_buckets_cpu_bitwise(monkeypatch):
+    """Layers cut into output-row chunk buckets (chunking forced on 512-wide layers) give the
+    same parameters bit for bit as whole-layer buckets, at P=2 over gloo."""
+    cfg = dict(print_rank="none", widths=[512, 512, 512, 1], n_features=512, n_samples=256,
+               nepochs=2, lr=1e-4, data_gen="device", data_dist="local", scaling="none",
+               bucket_mb=0.25)
+    monkeypatch.setenv("NNMPI_CHUNK_MIN_TILES", "2")
+    a = run_ranks(TrainConfig(device="cpu", **cfg), 2)
+    monkeypatch.setenv("NNMPI_CHUNK_MIN_TILES", "100000")
+    b = run_ranks(TrainConfig(device="cpu", **cfg), 2)
+    assert torch.equal(a[0]["final"], a[1]["final"])
+    assert torch.equal(a[0]["final"], b[0]["final"])
+    from nnmpi_amd.engine.arena import Arena
+    monkeypatch.setenv("NNMPI_CHUNK_MIN_TILES", "2")
+    ar = Arena([(512, 512), (512, 512), (1, 512)], "meta", bucket_bytes=0.25 * 2 ** 20)
+    assert ar.layer_chunks == {0: 2, 1: 2}
