@@ -266,6 +266,18 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
     check(sgd_momentum(P<float>(p), P<float>(g), P<float>(buf), P<bf16>(shadow), n, P<const float>(hp),
                        nesterov, first, zero_grad, S(s)), "sgd_momentum");
   });
+  m.def("sgd_momentum_bg", [](uptr p, uptr g, uptr buf, uptr shadow, long long n, uptr hp,
+                              int nesterov, int first, int zero_grad, int blocks, uptr s) {
+    check(sgd_momentum_bg(P<float>(p), P<float>(g), P<float>(buf), P<bf16>(shadow), n,
+                          P<const float>(hp), nesterov, first, zero_grad, blocks, S(s)),
+          "sgd_momentum_bg");
+  });
+  m.def("sgd_momentum_bf16grad", [](uptr p, uptr g, uptr buf, uptr shadow, long long n, uptr hp,
+                                    int nesterov, int first, uptr s) {
+    check(sgd_momentum_bf16grad(P<float>(p), P<const bf16>(g), P<float>(buf), P<bf16>(shadow), n,
+                                P<const float>(hp), nesterov, first, S(s)),
+          "sgd_momentum_bf16grad");
+  });
   m.def("cast_f32_bf16", [](uptr x, uptr y, long long n, uptr s) {
     check(cast_f32_bf16(P<const float>(x), P<bf16>(y), n, S(s)), "cast_f32_bf16");
   });

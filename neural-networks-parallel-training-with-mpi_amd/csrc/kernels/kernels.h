@@ -166,6 +166,13 @@ bool tiny_mlp_can_fuse_sgd(int rows);
 // hp = {lr, momentum, dampening, weight_decay, grad_scale}
 hipError_t sgd_momentum(float* p, float* g, float* buf, bf16* shadow, long long n,
                         const float* hp, int nesterov, int first, int zero_grad, hipStream_t s);
+// the same update on a fixed grid of `blocks` blocks (runs beside a GEMM, see optim.hip)
+hipError_t sgd_momentum_bg(float* p, float* g, float* buf, bf16* shadow, long long n,
+                           const float* hp, int nesterov, int first, int zero_grad, int blocks,
+                           hipStream_t s);
+// the same update with the gradient read from a bf16 buffer (the bf16 all-reduce payload)
+hipError_t sgd_momentum_bf16grad(float* p, const bf16* g, float* buf, bf16* shadow, long long n,
+                                 const float* hp, int nesterov, int first, hipStream_t s);
 hipError_t cast_f32_bf16(const float* x, bf16* y, long long n, hipStream_t s);
 hipError_t scale_f32(float* x, long long n, float a, hipStream_t s);
 hipError_t cast_bf16_f32(const bf16* x, float* y, long long n, hipStream_t s);

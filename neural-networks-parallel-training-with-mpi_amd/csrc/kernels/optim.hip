@@ -13,7 +13,21 @@
 
 namespace nnmpi {
 
-__global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* __restrict__ g,
+template <typename TG>
+__device__ __forceinline__ f32x4 load_grad4(TG* g, long long i) {
+  if constexpr (sizeof(TG) == 2) {
+    const bf16x4 v = reinterpret_cast<const bf16x4*>(g)[i];
+    return f32x4{(float)v[0], (float)v[1], (float)v[2], (float)v[3]};
+  } else {
+    return reinterpret_cast<const f32x4*>(g)[i];
+  }
+}
+
+// TG = bf16: the gradient is read straight from the bf16 all-reduce payload (the overlapped
+// schedule's bf16 buckets: no cast back to fp32 and no fp32 gradient round trip; the fp32
+// gradient arena is not touched -- every step rewrites it before reading it).
+template <typename TG>
+__global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, TG* __restrict__ g,
                                                   float* __restrict__ buf, bf16* __restrict__ shadow,
                                                   long long n4, const float* __restrict__ hp,
                                                   int nesterov, int first, int zero_grad) {
@@ -21,7 +35,7 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* 
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
-    f32x4 gv = reinterpret_cast<f32x4*>(g)[i];
+    f32x4 gv = load_grad4(g, i);
     f32x4 bv = (mom != 0.f && !first) ? reinterpret_cast<f32x4*>(buf)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
@@ -37,7 +51,9 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, float* 
       for (int r = 0; r < 4; ++r) s[r] = (bf16)pv[r];
       reinterpret_cast<bf16x4*>(shadow)[i] = s;
     }
-    if (zero_grad) reinterpret_cast<f32x4*>(g)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if constexpr (sizeof(TG) == 4) {
+      if (zero_grad) reinterpret_cast<f32x4*>(g)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
   }
 }
 
@@ -49,8 +65,28 @@ static int grid_for(long long n, int per_thread = 1) {
 hipError_t sgd_momentum(float* p, float* g, float* buf, bf16* shadow, long long n,
                         const float* hp, int nesterov, int first, int zero_grad, hipStream_t s) {
   if (n % 4 != 0) return hipErrorInvalidValue;
-  hipLaunchKernelGGL(sgd_kernel, dim3(grid_for(n / 4)), dim3(256), 0, s, p, g, buf, shadow, n / 4,
+  hipLaunchKernelGGL(sgd_kernel<float>, dim3(grid_for(n / 4)), dim3(256), 0, s, p, g, buf, shadow,
+                     n / 4, hp, nesterov, first, zero_grad);
+  return hipGetLastError();
+}
+
+// The same update as a "background" launch: a fixed grid of `blocks` grid-stride blocks (one
+// 4-wave block per CU at 256), so that it can run beside a 2-waves-per-SIMD GEMM whose
+// blocks leave 64 VGPRs per SIMD free, instead of queueing behind / in front of it.
+hipError_t sgd_momentum_bg(float* p, float* g, float* buf, bf16* shadow, long long n,
+                           const float* hp, int nesterov, int first, int zero_grad, int blocks,
+                           hipStream_t s) {
+  if (n % 4 != 0 || blocks < 1) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sgd_kernel<float>, dim3(blocks), dim3(256), 0, s, p, g, buf, shadow, n / 4,
                      hp, nesterov, first, zero_grad);
+  return hipGetLastError();
+}
+
+hipError_t sgd_momentum_bf16grad(float* p, const bf16* g, float* buf, bf16* shadow, long long n,
+                                 const float* hp, int nesterov, int first, hipStream_t s) {
+  if (n % 4 != 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(sgd_kernel<const bf16>, dim3(grid_for(n / 4)), dim3(256), 0, s, p, g, buf,
+                     shadow, n / 4, hp, nesterov, first, 0);
   return hipGetLastError();
 }
 

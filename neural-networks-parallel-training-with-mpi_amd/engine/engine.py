@@ -107,6 +107,9 @@ class MLPEngine:
         self.ws_pair = [self.ws, torch.zeros_like(self.ws)] if self.grouped else [self.ws, self.ws]
         if self.is_cuda:
             self.ev_wfree = [torch.cuda.Event(enable_timing=False) for _ in range(L)]
+        # bf16-payload overlapped schedule: per-bucket updates read the bf16 payload
+        self._upd_grad = (sync.update_grad() if (self.comm_overlap and hasattr(sync, "update_grad")
+                                                 and hasattr(ops, "sgd")) else None)
         self.rows = 0
         self.steps_done = 0
         self._graphs: Dict[tuple, object] = {}
@@ -480,7 +483,11 @@ class MLPEngine:
         collectives and updates instead of parking a later collective behind an update that
         waits for its weights' last reader."""
         if b.index not in self._reduced:
-            self._reduced[b.index] = self.sync.launch_bucket(b, stream)
+            if self._upd_grad is not None:
+                # bf16 payload: the bucket's update reads the reduced bf16 gradient directly
+                self._reduced[b.index] = self.sync.launch_bucket(b, stream, cast_back=False)
+            else:
+                self._reduced[b.index] = self.sync.launch_bucket(b, stream)
             self._flush_sgd(1)
         return self._reduced[b.index]
 
@@ -504,9 +511,12 @@ class MLPEngine:
                 for l in b.layers:
                     rs.wait_event(self.ev_wfree[l])
                 self.ops.sgd(self.arena, self.hp, self.nesterov, self._first, offset=b.offset,
-                             numel=b.numel)
+                             numel=b.numel, **self._upd_kw())
             if n is not None:
                 n -= 1
+
+    def _upd_kw(self):
+        return {} if self._upd_grad is None else {"grad_bf16": self._upd_grad}
 
     def _join_comm(self):
         """Join the comm stream into the compute stream.  Updates still queued at this point
@@ -526,7 +536,7 @@ class MLPEngine:
                 e0 += tail[j][0].numel
                 j += 1
             self.ops.sgd(self.arena, self.hp, self.nesterov, self._first, offset=s0,
-                         numel=e0 - s0)
+                         numel=e0 - s0, **self._upd_kw())
             i = j
 
     def step(self):

@@ -242,10 +242,19 @@ class HipOps:
 
     # ---------------- optimizer ----------------
     def sgd(self, arena, hp, nesterov: bool, first: bool, zero_grad: bool = True, offset: int = 0,
-            numel: int = None):
+            numel: int = None, grad_bf16=None):
+        """``grad_bf16``: read the gradient from this bf16 buffer (same layout as the arena)
+        instead of ``arena.grad`` -- the bf16 all-reduce payload, updated from directly."""
         n = arena.numel - offset if numel is None else numel
         e = 4  # bytes per fp32 element
         sh = _p(arena.shadow) + 2 * offset if arena.shadow is not None else 0
+        if grad_bf16 is not None:
+            _check(grad_bf16.dtype == torch.bfloat16 and grad_bf16.numel() >= offset + n,
+                   "sgd: bf16 gradient buffer too small")
+            self.lib.sgd_momentum_bf16grad(_p(arena.master) + e * offset, _p(grad_bf16) + 2 * offset,
+                                           _p(arena.momentum) + e * offset, sh, n, _p(hp),
+                                           int(nesterov), int(first), self.stream)
+            return
         self.lib.sgd_momentum(_p(arena.master) + e * offset, _p(arena.grad) + e * offset,
                               _p(arena.momentum) + e * offset, sh, n, _p(hp), int(nesterov),
                               int(first), int(zero_grad), self.stream)

@@ -81,11 +81,14 @@ class TorchOps:
         dst[:idx.numel()].copy_(src.index_select(0, idx))
 
     def sgd(self, arena, hp, nesterov: bool, first: bool, zero_grad: bool = True, offset: int = 0,
-            numel: int = None):
+            numel: int = None, grad_bf16=None):
         lr, mom, damp, wd, gs = [float(v) for v in hp.tolist()[:5]]
         n = arena.numel - offset if numel is None else numel
         sl = slice(offset, offset + n)
         p, g, buf = arena.master[sl], arena.grad[sl], arena.momentum[sl]
+        if grad_bf16 is not None:
+            g = grad_bf16[sl].float()
+            zero_grad = False
         with torch.no_grad():
             d = g * gs
             if wd != 0:

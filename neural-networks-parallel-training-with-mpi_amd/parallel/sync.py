@@ -161,7 +161,7 @@ class NativeRcclSync(GradSync):
                      if self.bf16 else None)
         self._comm_stream = torch.cuda.ExternalStream(self.gs.comm_stream)
 
-    def _launch(self, bucket, stream=None):
+    def _launch(self, bucket, stream=None, cast_back: bool = True):
         view = self.arena.grad[bucket.offset:bucket.offset + bucket.numel]
         self.seq += 1
         h = int(stream.cuda_stream) if stream is not None else self.native.stream_handle()
@@ -181,16 +181,21 @@ class NativeRcclSync(GradSync):
                 lib.cast_bf16_f32(ptr, view.data_ptr(), bucket.numel, h)
             return
         self.gs.bucket_ready(bucket.index, ptr, bucket.numel, dt, h)
-        if self.bf16:   # back to fp32 on the comm stream, ahead of the bucket's update there
+        if self.bf16 and cast_back:   # back to fp32 on the comm stream, ahead of its update
             lib.cast_bf16_f32(ptr, view.data_ptr(), bucket.numel, self.gs.comm_stream)
         self._launched = True
 
-    def launch_bucket(self, bucket, stream):
+    def update_grad(self):
+        """The buffer the engine's per-bucket updates read after :meth:`launch_bucket` with
+        ``cast_back=False``: the bf16 payload itself (None: the fp32 gradient arena)."""
+        return self.gbuf if (self.bf16 and not self.inline) else None
+
+    def launch_bucket(self, bucket, stream, cast_back: bool = True):
         # NB: every collective of one communicator stays on ONE stream -- a bucket issued on
         # the compute stream while earlier ones are still queued on the comm stream lets the two
         # run concurrently on the GPU, in different orders on different ranks: measured to hang
         # (and, inside a capture, to crash) at P = 2 / 3
-        self._launch(bucket, stream)
+        self._launch(bucket, stream, cast_back=cast_back)
         return None if self.inline else self._comm_stream
 
     def capture_origin(self):
