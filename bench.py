@@ -95,8 +95,9 @@ def parse(argv=None):
     p.add_argument("--no_group", action="store_true",
                    help="separate dgrad / wgrad / combine launches instead of the grouped one")
     p.add_argument("--even", action="store_true", help="no uneven extra rows")
-    p.add_argument("--graph_chunk", type=int, default=16,
-                   help="steps per replayed hipGraph (1 = one graph launch per step)")
+    p.add_argument("--graph_chunk", type=int, default=0,
+                   help="steps per replayed hipGraph (1 = one graph launch per step; 0 = auto: "
+                        "each run of n steps as few graphs as possible, at most 128 steps each)")
     p.add_argument("--lr", type=float, default=1e-5)
     p.add_argument("--comm_mode", choices=["auto", "tune", "overlap", "inline", "zero1"],
                    default="auto",
@@ -337,7 +338,12 @@ def run(a, job):
         pg.barrier()
         return max_over_ranks(el)
 
-    chunk = max(1, a.graph_chunk)
+    def chunk_for(n: int) -> int:
+        # one replay's fixed cost (launch + drain) per graph: a short timed region (the
+        # driver's 20 steps) is one graph launch, not 16 + 4
+        return a.graph_chunk if a.graph_chunk > 0 else max(1, min(n, 128))
+
+    chunk = chunk_for(a.steps)
     if a.scaling == "weak":
         n_global = rows_pg * world - (0 if (a.even or world == 1) else 1)
     else:
@@ -353,6 +359,23 @@ def run(a, job):
         mode = "none"
     elif native_comm is None and mode == "tune":
         mode = "inline"
+    late_capture = os.environ.get("NNMPI_BENCH_LATE_CAPTURE") == "1"   # A/B only
+
+    def warm(e, n):
+        """n untimed steps.  The timed region's graphs are captured FIRST (after the eager first
+        step), so the warm-up steps run right before the timed region: capturing is host-only
+        work, and a GPU left idle meanwhile drops its clocks, which a 20-step timed region
+        (2 ms) would otherwise start with."""
+        if late_capture:
+            e.run_steps(n, chunk_for(n))
+            return
+        if n > 0 and e.steps_done == 0:
+            e.run_steps(1, 1)
+            n -= 1
+        e.prepare_steps(a.steps, chunk)
+        e.prepare_steps(n, chunk_for(n))
+        e.run_steps(n, chunk_for(n))
+
     tune = None
     bucket_mb = a.bucket_mb
     if mode == "tune":
@@ -366,8 +389,8 @@ def run(a, job):
             cands.append(("overlap", half_mb))
         for m, bmb in cands:
             e = build(m, data, bucket_mb=bmb)
-            e.run_steps(a.warmup, chunk)
-            tm = min(timed(e, a.tune_steps, chunk) for _ in range(2))
+            e.run_steps(a.warmup, chunk_for(a.warmup))
+            tm = min(timed(e, a.tune_steps, chunk_for(a.tune_steps)) for _ in range(2))
             key = m if bmb in (None, a.bucket_mb) else f"{m}_{bmb}mb"
             tune[key] = round(tm / a.tune_steps * 1e3, 5)
             # every rank sees the same max-over-ranks times, so every rank keeps the same mode
@@ -376,9 +399,12 @@ def run(a, job):
             del e
         if gpu:
             torch.cuda.empty_cache()
+        # the chosen engine idled while the other candidates ran: warm it again (untimed, like
+        # the tuning runs themselves)
+        warm(eng, a.warmup)
     else:
         eng = build(mode, data)
-        eng.run_steps(a.warmup, chunk)
+        warm(eng, a.warmup)
 
     # ---------------- the timed region: exactly K steps -------------------------------------
     # graph mode: steps replayed as hipGraphs of `chunk` complete consecutive steps (one
@@ -419,7 +445,7 @@ def run(a, job):
                 eng.arena.grad.zero_()
             if gpu:
                 torch.cuda.synchronize()
-            comm_ms = _time_comm_only(sync, n_ex, chunk, gpu and not a.no_graph, barrier,
+            comm_ms = _time_comm_only(sync, n_ex, chunk_for(n_ex), gpu and not a.no_graph, barrier,
                                       max_over_ranks) * 1e3
             with torch.no_grad():
                 eng.arena.grad.zero_()
@@ -429,8 +455,8 @@ def run(a, job):
         if use_comm:
             # the same per-rank work with the gradient sync off: every rank alone (1-GPU step)
             e = build("none", data, comm=False)
-            e.run_steps(min(a.warmup, 10) + 1, chunk)
-            comp_ms = timed(e, n_ex, chunk) / n_ex * 1e3
+            e.run_steps(min(a.warmup, 10) + 1, chunk_for(min(a.warmup, 10)))
+            comp_ms = timed(e, n_ex, chunk_for(n_ex)) / n_ex * 1e3
             del e
         else:
             comp_ms = ms
@@ -442,8 +468,8 @@ def run(a, job):
             # proxy) split over the N ranks
             sdata = shard(rows_pg)
             e = build(mode if mode != "none" else "inline", sdata, bucket_mb=bucket_mb)
-            e.run_steps(min(a.warmup, 10) + 1, chunk)
-            s_ms = timed(e, n_ex, chunk) / n_ex * 1e3
+            e.run_steps(min(a.warmup, 10) + 1, chunk_for(min(a.warmup, 10)))
+            s_ms = timed(e, n_ex, chunk_for(n_ex)) / n_ex * 1e3
             del e, sdata
             # S(1): the single-GPU step of the whole dataset = the compute-only step above
             # (weak scaling gives every rank rows_pg rows, the last one rows_pg - 1)
@@ -492,7 +518,7 @@ def run(a, job):
                        "comm": (("rccl" if native_comm is not None else
                                  ("nccl" if pg.nccl is not None else "gloo"))
                                 if use_comm else "none"),
-                       "graph": gpu and not a.no_graph, "graph_chunk": a.graph_chunk,
+                       "graph": gpu and not a.no_graph, "graph_chunk": chunk,
                        "overlap": not a.no_overlap, "grouped": not a.no_group,
                        "comm_mode": mode if use_comm else None,
                        "comm_tune_ms_per_step": tune,

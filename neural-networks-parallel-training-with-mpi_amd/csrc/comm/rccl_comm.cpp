@@ -1,3 +1,4 @@
+#include <cstdlib>
 #include "rccl_comm.h"
 
 #include <cstring>
@@ -198,6 +199,7 @@ void GraphRunner::begin(hipStream_t s, int mode) {
 }
 
 void GraphRunner::end() {
+  hipStream_t s = cap_;
   const hipError_t e = hipStreamEndCapture(cap_, &graph_);
   cap_ = nullptr;
   if (e != hipSuccess) {
@@ -207,6 +209,14 @@ void GraphRunner::end() {
                              " at hipStreamEndCapture");
   }
   HIP_THROW(hipGraphInstantiate(&exec_, graph_, nullptr, nullptr, 0));
+  // Upload the executable graph now (asynchronously on the capture stream), so its first
+  // replay -- often inside a timed region -- does not pay for it.  NNMPI_GRAPH_UPLOAD=0 skips
+  // it (A/B).
+  static const bool upload = [] {
+    const char* v = std::getenv("NNMPI_GRAPH_UPLOAD");
+    return !(v && v[0] == '0');
+  }();
+  if (upload) HIP_THROW(hipGraphUpload(exec_, s));
 }
 
 void GraphRunner::cancel() {
