@@ -359,16 +359,12 @@ def run(a, job):
         mode = "none"
     elif native_comm is None and mode == "tune":
         mode = "inline"
-    late_capture = os.environ.get("NNMPI_BENCH_LATE_CAPTURE") == "1"   # A/B only
-
     def warm(e, n):
         """n untimed steps.  The timed region's graphs are captured FIRST (after the eager first
         step), so the warm-up steps run right before the timed region: capturing is host-only
         work, and a GPU left idle meanwhile drops its clocks, which a 20-step timed region
-        (2 ms) would otherwise start with."""
-        if late_capture:
-            e.run_steps(n, chunk_for(n))
-            return
+        (2 ms) would otherwise start with (measured: within noise either way,
+        profiles/r2_experiments.md section 9)."""
         if n > 0 and e.steps_done == 0:
             e.run_steps(1, 1)
             n -= 1
