@@ -97,6 +97,13 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
                             M, N, K, P<float>(ws), S(s), fu ? &f : nullptr), "linear_wgrad_bf16");
   }, py::arg("dZ"), py::arg("lddz"), py::arg("X"), py::arg("ldx"), py::arg("dW"), py::arg("db"),
      py::arg("M"), py::arg("N"), py::arg("K"), py::arg("ws"), py::arg("s"), py::arg("sgd") = py::none());
+  m.def("linear_wgrad_bf16_out16", [](uptr dZ, int lddz, uptr X, int ldx, uptr dW16, uptr db16,
+                                      int M, int N, int K, uptr s) {
+    check(linear_wgrad_bf16_ex(P<const bf16>(dZ), lddz, P<const bf16>(X), ldx, nullptr, nullptr,
+                               M, N, K, nullptr, S(s),
+                               nullptr, nullptr, P<bf16>(dW16), P<bf16>(db16)),
+          "linear_wgrad_bf16_out16");
+  });
   m.def("gemm_bf16", [](uptr A, int lda, int la, uptr B, int ldb, int lb, int M, int N, int K, uptr C,
                         int ldc, uptr s) {
     check(gemm_bf16_generic(P<const bf16>(A), lda, la, P<const bf16>(B), ldb, lb, M, N, K, P<float>(C),

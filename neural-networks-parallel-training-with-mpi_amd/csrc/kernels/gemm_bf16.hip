@@ -52,6 +52,8 @@ struct GemmParams {
   unsigned a_bytes, b_bytes;  // extents of A / B storage (buffer-resource range, DMA path)
   SgdFuse sg;                 // EPI_F32 without split-K: apply the optimizer instead of storing
   int store_pol;              // epilogue output stores: 0 plain, 1 nt, 2 sc1 (write-through)
+  bf16* c16;                  // EPI_F32 without split-K: store the gradient as bf16 here instead
+  bf16* bg16;                 // (same ldc as C) and the bias gradient here -- the bf16 payload
 };
 
 // Epilogue output store of 16 bytes with a selectable cache policy (experiments: what the
@@ -265,6 +267,13 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& p, f32x4 (&acc)
 #pragma unroll
       for (int j = 0; j < NJ; ++j) {
         if (ncol[j] >= p.N) continue;
+        if (p.c16) {   // the bf16 all-reduce payload, rounded as cast_f32_bf16 rounds
+          bf16x4 o;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) o[r] = (bf16)acc[i][j][r];
+          *reinterpret_cast<bf16x4*>(p.c16 + (long long)mrow[i] * p.ldc + ncol[j]) = o;
+          continue;
+        }
         float* g = cbase + (long long)mrow[i] * p.ldc + ncol[j];
         if (fuse) sgd_fused_store4(p.sg, g, acc[i][j]);
         else *reinterpret_cast<f32x4*>(g) = acc[i][j];
@@ -278,6 +287,7 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& p, f32x4 (&acc)
       for (int i = 0; i < MI; ++i) {
         const int m = mrow[i];
         if (m >= p.M) continue;
+        if (p.bg16) { p.bg16[m] = (bf16)accb[i][0]; continue; }
         float* g = p.bias_grad + split * p.bg_split_stride + m;
         if (p.sg.g_base) sgd_fused_store(p.sg, g, accb[i][0]);
         else *g = accb[i][0];
@@ -402,7 +412,8 @@ template <int EPI>
 __device__ __forceinline__ bool lepi_ok(const GemmParams& p) {
   // whole 16-byte column chunks, 16-byte aligned rows (the fragment epilogue covers the rest)
   if (p.N % 8) return false;
-  if constexpr (EPI == EPI_F32) return (p.ldc % 4) == 0 && ((uintptr_t)p.C & 15) == 0;
+  if constexpr (EPI == EPI_F32)
+    return p.c16 == nullptr && (p.ldc % 4) == 0 && ((uintptr_t)p.C & 15) == 0;
   else if constexpr (EPI == EPI_DACT)
     return (p.ldc % 8) == 0 && ((uintptr_t)p.C & 15) == 0 && (p.ldaux % 8) == 0 &&
            ((uintptr_t)p.aux & 15) == 0;
@@ -1340,6 +1351,7 @@ static int make_wgrad(const WgradArgs& a, GemmParams& p, SlabReduce& pending) {
     p.C = a.dW; p.ldc = N; p.c_split_stride = 0;
     p.bias_grad = a.db; p.bg_split_stride = 0;
     p.sg = a.sg;          // (g_base null: plain gradient store)
+    p.c16 = a.dW16; p.bg16 = a.db16;
     return splits;
   }
   p.C = a.ws; p.ldc = N; p.c_split_stride = (long long)M * N;
@@ -1355,19 +1367,28 @@ static int make_wgrad(const WgradArgs& a, GemmParams& p, SlabReduce& pending) {
 hipError_t linear_wgrad_bf16_deferred(const bf16* dZ, int lddz, const bf16* X, int ldx, float* dW,
                                       float* db, int M, int N, int K, float* ws, hipStream_t s,
                                       const SgdFuse* sgd, SlabReduce* pending) {
-  WgradArgs a{dZ, lddz, X, ldx, dW, db, M, N, K, ws, SgdFuse{}};
+  return linear_wgrad_bf16_ex(dZ, lddz, X, ldx, dW, db, M, N, K, ws, s, sgd, pending, nullptr,
+                              nullptr);
+}
+
+hipError_t linear_wgrad_bf16_ex(const bf16* dZ, int lddz, const bf16* X, int ldx, float* dW,
+                                float* db, int M, int N, int K, float* ws, hipStream_t s,
+                                const SgdFuse* sgd, SlabReduce* pending, bf16* dW16, bf16* db16) {
+  WgradArgs a{dZ, lddz, X, ldx, dW, db, M, N, K, ws, SgdFuse{}, dW16, db16};
   if (sgd) a.sg = *sgd;
+  if (dW16 && (sgd || wgrad_splits(M, N, K) > 1)) return hipErrorInvalidValue;
   GemmParams p;
   SlabReduce r;
   const int splits = make_wgrad(a, p, r);
   if (splits > 1 && ws == nullptr) return hipErrorInvalidValue;
   hipError_t e;
   const int wt = wgrad_tile(M, N);
-  if (wt == 256) e = db ? launch_t<256, 256, XMAJ, XMAJ, EPI_F32, ACT_NONE, true>(p, splits, s)
+  const bool bg = db != nullptr || db16 != nullptr;
+  if (wt == 256) e = bg ? launch_t<256, 256, XMAJ, XMAJ, EPI_F32, ACT_NONE, true>(p, splits, s)
                         : launch_t<256, 256, XMAJ, XMAJ, EPI_F32, ACT_NONE, false>(p, splits, s);
-  else if (wt == 128) e = db ? launch_t<128, 128, XMAJ, XMAJ, EPI_F32, ACT_NONE, true>(p, splits, s)
+  else if (wt == 128) e = bg ? launch_t<128, 128, XMAJ, XMAJ, EPI_F32, ACT_NONE, true>(p, splits, s)
                              : launch_t<128, 128, XMAJ, XMAJ, EPI_F32, ACT_NONE, false>(p, splits, s);
-  else e = db ? launch_t<64, 64, XMAJ, XMAJ, EPI_F32, ACT_NONE, true>(p, splits, s)
+  else e = bg ? launch_t<64, 64, XMAJ, XMAJ, EPI_F32, ACT_NONE, true>(p, splits, s)
               : launch_t<64, 64, XMAJ, XMAJ, EPI_F32, ACT_NONE, false>(p, splits, s);
   if (e != hipSuccess) return e;
   if (pending) {

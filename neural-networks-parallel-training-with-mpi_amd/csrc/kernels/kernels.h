@@ -81,6 +81,12 @@ hipError_t splitk_reduce(const float* ws, int S, long long stride, int M, int N,
 hipError_t slab_reduce(const SlabReduce& r, hipStream_t s);
 // Weight gradient whose split-K combine is NOT launched: *pending describes it (S == 0: the
 // GEMM wrote dW / db directly, nothing pending).
+// Un-split weight gradient stored as bf16 (dW16 / db16, same leading dimension as dW) instead of
+// fp32: the bf16 all-reduce payload written by the GEMM epilogue itself (no fp32 round trip and
+// no cast pass).  Refused (hipErrorInvalidValue) with an SGD fusion or when the launch would split.
+hipError_t linear_wgrad_bf16_ex(const bf16* dZ, int lddz, const bf16* X, int ldx, float* dW,
+                                float* db, int M, int N, int K, float* ws, hipStream_t s,
+                                const SgdFuse* sgd, SlabReduce* pending, bf16* dW16, bf16* db16);
 hipError_t linear_wgrad_bf16_deferred(const bf16* dZ, int lddz, const bf16* X, int ldx, float* dW,
                                       float* db, int M, int N, int K, float* ws, hipStream_t s,
                                       const SgdFuse* sgd, SlabReduce* pending);
@@ -96,6 +102,7 @@ struct DgradArgs {
 struct WgradArgs {
   const bf16* dZ; int lddz; const bf16* X; int ldx; float* dW; float* db; int M, N, K;
   float* ws; SgdFuse sg;
+  bf16* dW16 = nullptr; bf16* db16 = nullptr;   // un-split only: bf16 gradient outputs
 };
 void set_bwd_group(int on);   // 1 = grouped kernel (default), 0 = separate launches (A/B)
 bool bwd_group_supported(int rows, int out_f, int in_f);   // this layer shape runs grouped

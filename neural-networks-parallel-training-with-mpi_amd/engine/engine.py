@@ -22,7 +22,7 @@ on the CPU (gloo) — that is the reference-semantics path and the test oracle.
 from __future__ import annotations
 
 import math
-from typing import Dict, Optional
+from typing import Dict, List, Optional, Tuple
 
 import torch
 
@@ -110,6 +110,10 @@ class MLPEngine:
         # bf16-payload overlapped schedule: per-bucket updates read the bf16 payload
         self._upd_grad = (sync.update_grad() if (self.comm_overlap and hasattr(sync, "update_grad")
                                                  and hasattr(ops, "sgd")) else None)
+        # ... and the chunked weight gradients store that bf16 payload themselves
+        self._w16 = (self._upd_grad is not None and dtype == torch.bfloat16
+                     and hasattr(ops, "wgrad_can_write_bf16"))
+        self._written16: List[Tuple[int, int]] = []
         self.rows = 0
         self.steps_done = 0
         self._graphs: Dict[tuple, object] = {}
@@ -243,21 +247,38 @@ class MLPEngine:
                 dz = dz_next
         self._mark("bwd")
 
-    def _wgrad_chunks(self, i: int, dz, x_in):
+    def _wgrad_chunks(self, i: int, dz, x_in, bf16_out: bool = False):
         """Weight gradient of layer i; a layer cut into output-row chunk buckets (Arena
         .layer_chunks) is computed chunk by chunk, yielding each chunk's bucket as soon as its
         launch is queued (so its all-reduce can start while the next chunk computes).  Every
         output tile is the same GEMM tile over the same K either way: the result is bitwise
-        independent of the chunking."""
+        independent of the chunking.
+
+        ``bf16_out`` (bf16-payload overlapped schedule): the chunks' GEMM epilogues store the
+        gradient straight into the bf16 payload buffer -- no fp32 gradient write and no cast
+        pass; the layer's arena range is recorded in ``self._written16`` so its buckets skip the
+        cast.  Same rounding as the cast: bitwise identical payload."""
         ar = self.arena
         gW, gb = ar.grad_weight(i), ar.grad_bias(i)
         chunks = ar.chunk_buckets(i)
         if not chunks:
             self.ops.linear_wgrad(dz, x_in, gW, gb, ws=self.ws)
             return
+        g16 = self._upd_grad if bf16_out else None
+        if g16 is not None:
+            out_f, in_f = self.spec.layer_shape(i)
+            if all(self.ops.wgrad_can_write_bf16(dz.shape[0], b.rows[1] - b.rows[0], in_f)
+                   for b in chunks):
+                self._written16.append(ar.layer_range[i])
+            else:
+                g16 = None
         for b in chunks:
             r0, r1 = b.rows
-            self.ops.linear_wgrad(dz[:, r0:r1], x_in, gW[r0:r1], gb[r0:r1], ws=self.ws)
+            if g16 is not None:
+                self.ops.linear_wgrad(dz[:, r0:r1], x_in, None, None, out_bf16=(
+                    ar.weight(i, g16)[r0:r1], ar.bias(i, g16)[r0:r1]))
+            else:
+                self.ops.linear_wgrad(dz[:, r0:r1], x_in, gW[r0:r1], gb[r0:r1], ws=self.ws)
             yield b
 
     def _forward(self, x):
@@ -321,6 +342,7 @@ class MLPEngine:
         self._sgd_done = set()
         self._reduced = {}
         self._pending_sgd = []
+        self._written16 = []
         self._first = first
         x = self.X[:rows]
         h = self._forward(x)
@@ -333,7 +355,7 @@ class MLPEngine:
         self._layer_done(last, main)
         for i in range(L - 2, -1, -1):
             x_in = self.acts[i - 1][:rows] if i > 0 else x
-            for b in self._wgrad_chunks(i, dz, x_in):
+            for b in self._wgrad_chunks(i, dz, x_in, bf16_out=self._w16):
                 self._bucket_reduce(b, main)      # chunk's all-reduce starts right away
             if i > 0:
                 dz_next = self._dzl(i - 1, rows)
@@ -349,7 +371,8 @@ class MLPEngine:
             self._update(first)                             # one pass over the whole arena
         else:
             for b in rest:
-                ops.sgd(ar, self.hp, self.nesterov, first, offset=b.offset, numel=b.numel)
+                ops.sgd(ar, self.hp, self.nesterov, first, offset=b.offset, numel=b.numel,
+                        **self._upd_kw())
 
     # Single rank: a layer's gradient is final as soon as its split-K partials are combined, so
     # the reducer applies the SGD update itself (no gradient round trip through HBM, no separate
@@ -407,6 +430,7 @@ class MLPEngine:
             self._sgd_done = set()
             self._reduced = {}
             self._pending_sgd = []
+            self._written16 = []
             self._first = first
         x = self.X[:rows]
         h = self._forward(x)
@@ -485,7 +509,8 @@ class MLPEngine:
         if b.index not in self._reduced:
             if self._upd_grad is not None:
                 # bf16 payload: the bucket's update reads the reduced bf16 gradient directly
-                self._reduced[b.index] = self.sync.launch_bucket(b, stream, cast_back=False)
+                self._reduced[b.index] = self.sync.launch_bucket(
+                    b, stream, cast_back=False, written=self._written16)
             else:
                 self._reduced[b.index] = self.sync.launch_bucket(b, stream)
             self._flush_sgd(1)

@@ -85,9 +85,27 @@ class HipOps:
         return (_p(arena.grad), _p(arena.master), _p(arena.momentum), sh, _p(hp), int(nesterov),
                 int(first))
 
-    def linear_wgrad(self, dz, x, gW, gb, ws=None, sgd=None):
+    def wgrad_can_write_bf16(self, rows, out_f, in_f) -> bool:
+        """True when the (un-split) weight gradient can store bf16 gradients itself."""
+        return bool(out_f % 8 == 0 and in_f % 8 == 0 and
+                    int(self.lib.wgrad_splits(out_f, in_f, rows)) == 1)
+
+    def linear_wgrad(self, dz, x, gW, gb, ws=None, sgd=None, out_bf16=None):
+        """``out_bf16=(gW16, gb16)``: store the gradient as bf16 there instead of into gW / gb
+        (un-split shapes only, see wgrad_can_write_bf16)."""
         rows, M = dz.shape
         N = x.shape[1]
+        if out_bf16 is not None:
+            gW16, gb16 = out_bf16
+            _check(dz.dtype == torch.bfloat16 and sgd is None and
+                   self.wgrad_can_write_bf16(rows, M, N), "bf16 wgrad output: un-split bf16 only")
+            _check(gW16.dtype == torch.bfloat16 and tuple(gW16.shape) == (M, N) and
+                   gW16.stride(0) == N and gW16.stride(1) == 1, "bf16 wgrad output: dense [M, N]")
+            _check(gb16 is None or (gb16.dtype == torch.bfloat16 and gb16.numel() == M),
+                   "bf16 wgrad bias output")
+            self.lib.linear_wgrad_bf16_out16(_p(dz), dz.stride(0), _p(x), x.stride(0), _p(gW16),
+                                             _p(gb16), M, N, rows, self.stream)
+            return
         if dz.dtype == torch.bfloat16:
             _check(M % 8 == 0 and N % 8 == 0, f"bf16 wgrad needs out%8==0, in%8==0 ({M}, {N})")
             self._check_ws(ws, self.lib.wgrad_workspace_bytes(M, N, rows), "wgrad")

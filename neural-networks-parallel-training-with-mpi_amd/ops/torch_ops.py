@@ -49,9 +49,12 @@ class TorchOps:
         out.copy_(g * act_bwd_from_out(a_prev.float(), act))
 
     # gW = dz^T @ x ; gb = sum(dz, 0)
-    def linear_wgrad(self, dz, x, gW, gb, ws=None):
+    def linear_wgrad(self, dz, x, gW, gb, ws=None, out_bf16=None):
+        if out_bf16 is not None:
+            gW, gb = out_bf16
         gW.copy_(dz.float().t().mm(x.float()))
-        gb.copy_(dz.float().sum(0))
+        if gb is not None:
+            gb.copy_(dz.float().sum(0))
 
     def head(self, a, W, b, y, labels, loss: str, inv_count: float, act_prev: str, dz_out,
              gW, gb, dlogits, loss_out, loss_scale: float, ws=None):

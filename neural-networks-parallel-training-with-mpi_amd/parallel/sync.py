@@ -30,6 +30,23 @@ import torch
 import torch.distributed as dist
 
 
+def _subtract(rng, cuts):
+    """The parts of the half-open range ``rng`` not covered by any of the ranges ``cuts``."""
+    lo, hi = rng
+    out = []
+    for a, b in sorted(cuts):
+        if b <= lo or a >= hi:
+            continue
+        if a > lo:
+            out.append((lo, a))
+        lo = max(lo, b)
+        if lo >= hi:
+            break
+    if lo < hi:
+        out.append((lo, hi))
+    return out
+
+
 class GradSync:
     world = 1
 
@@ -157,11 +174,13 @@ class NativeRcclSync(GradSync):
         self.world = world
         self.gs = native.lib().GradSync(native_comm, len(arena.buckets), priority)
         self._launched = False
-        self.gbuf = (torch.empty(arena.numel, dtype=torch.bfloat16, device=arena.grad.device)
+        # zeros: ranges the engine's bf16 weight-gradient epilogues write directly are never
+        # cast into, so their alignment padding must start (and stay) zero
+        self.gbuf = (torch.zeros(arena.numel, dtype=torch.bfloat16, device=arena.grad.device)
                      if self.bf16 else None)
         self._comm_stream = torch.cuda.ExternalStream(self.gs.comm_stream)
 
-    def _launch(self, bucket, stream=None, cast_back: bool = True):
+    def _launch(self, bucket, stream=None, cast_back: bool = True, written=()):
         view = self.arena.grad[bucket.offset:bucket.offset + bucket.numel]
         self.seq += 1
         h = int(stream.cuda_stream) if stream is not None else self.native.stream_handle()
@@ -169,7 +188,11 @@ class NativeRcclSync(GradSync):
         ptr, dt = view.data_ptr(), 0
         if self.bf16:
             ptr, dt = self.gbuf[bucket.offset:].data_ptr(), 1
-            lib.cast_f32_bf16(view.data_ptr(), ptr, bucket.numel, h)
+            # cast the fp32 gradient into the payload, except the `written` arena ranges whose
+            # bf16 values the producing kernels stored there themselves
+            for lo, hi in _subtract((bucket.offset, bucket.offset + bucket.numel), written):
+                lib.cast_f32_bf16(self.arena.grad[lo:].data_ptr(), self.gbuf[lo:].data_ptr(),
+                                  hi - lo, h)
         if self.inline:
             if self.mode == "root":
                 # reference pattern (ref.py:185-203): everything through rank 0
@@ -190,12 +213,14 @@ class NativeRcclSync(GradSync):
         ``cast_back=False``: the bf16 payload itself (None: the fp32 gradient arena)."""
         return self.gbuf if (self.bf16 and not self.inline) else None
 
-    def launch_bucket(self, bucket, stream, cast_back: bool = True):
+    def launch_bucket(self, bucket, stream, cast_back: bool = True, written=()):
+        """``written``: (lo, hi) arena ranges already holding their bf16 gradient in the payload
+        buffer (bf16 payload only)."""
         # NB: every collective of one communicator stays on ONE stream -- a bucket issued on
         # the compute stream while earlier ones are still queued on the comm stream lets the two
         # run concurrently on the GPU, in different orders on different ranks: measured to hang
         # (and, inside a capture, to crash) at P = 2 / 3
-        self._launch(bucket, stream, cast_back=cast_back)
+        self._launch(bucket, stream, cast_back=cast_back, written=written)
         return None if self.inline else self._comm_stream
 
     def capture_origin(self):

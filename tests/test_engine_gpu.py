@@ -423,6 +423,17 @@ def test_wide_chunked_buckets_overlap_bitwise_equal():
     assert torch.equal(a.final_params, b.final_params)
 
 
+def test_wide_chunked_bf16_payload_written_by_wgrad_bitwise_equal():
+    """bf16 payload, overlapped: the chunk weight gradients store bf16 straight into the
+    all-reduce buffer (no fp32 gradient, no cast pass) and the SGD reads it -- bitwise equal to
+    the inline bf16 path (fp32 gradient -> cast -> all-reduce -> cast back -> SGD)."""
+    a = trainer.run_worker(_wide_cfg(comm="native", comm_mode="overlap", bucket_mb=16,
+                                     grad_dtype="bf16"))
+    b = trainer.run_worker(_wide_cfg(comm="native", comm_mode="inline", grad_dtype="bf16"))
+    assert a.losses == b.losses
+    assert torch.equal(a.final_params, b.final_params)
+
+
 def test_grouped_backward_with_comm_overlap_bitwise_equal():
     """Grouped backward (dgrad + wgrad + combine in one launch) with per-bucket all-reduce on
     the comm stream and SGD on the update stream == the fused single-rank path."""

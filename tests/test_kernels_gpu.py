@@ -165,6 +165,74 @@ def test_sgd_matches_torch_optim(first, nesterov, wd, damp):
     assert torch.count_nonzero(ar.grad) == 0
 
 
+@pytest.mark.parametrize("M,N,K", [(1024, 512, 256), (520, 264, 200), (2048, 8192, 512)])
+def test_wgrad_bf16_output_equals_cast_of_fp32(M, N, K):
+    """The weight gradient stored as bf16 by its own epilogue == the fp32 gradient cast to bf16
+    (the bf16 all-reduce payload), bit for bit, bias gradient included."""
+    from nnmpi_amd.ops.hip_ops import HipOps
+    ops = HipOps()
+    assert ops.wgrad_can_write_bf16(K, M, N)
+    dz = _rand(K, M, seed=40).to(torch.bfloat16)
+    x = _rand(K, N, seed=41).to(torch.bfloat16)
+    gW = torch.empty(M, N, device=DEV)
+    gb = torch.empty(M, device=DEV)
+    ops.linear_wgrad(dz, x, gW, gb)
+    gW16 = torch.full((M, N), float("nan"), device=DEV, dtype=torch.bfloat16)
+    gb16 = torch.full((M,), float("nan"), device=DEV, dtype=torch.bfloat16)
+    ops.linear_wgrad(dz, x, None, None, out_bf16=(gW16, gb16))
+    assert torch.equal(gW16, gW.to(torch.bfloat16))
+    assert torch.equal(gb16, gb.to(torch.bfloat16))
+    ref = dz.float().t() @ x.float()
+    torch.testing.assert_close(gW16.float(), ref, rtol=1e-2, atol=1e-2 * ref.abs().max().item())
+
+
+@pytest.mark.parametrize("first", [True, False])
+def test_sgd_bf16_gradient_and_background_grid(first):
+    """The bf16-gradient update (the overlapped schedule's bf16 payload) against torch.optim.SGD
+    on the same bf16 values in fp32, and the fixed-grid launch against the default one."""
+    from nnmpi_amd.engine.arena import Arena
+    from nnmpi_amd.ops.hip_ops import HipOps
+    ar = Arena([(64, 200), (1, 64)], DEV, shadow_dtype=torch.bfloat16)
+    ar.master.copy_(_rand(ar.numel, seed=30))
+    ar.grad.copy_(_rand(ar.numel, seed=31))
+    ar.momentum.copy_(_rand(ar.numel, seed=32))
+    g16 = _rand(ar.numel, seed=33).to(torch.bfloat16)
+    m0, v0, g0 = ar.master.clone(), ar.momentum.clone(), ar.grad.clone()
+    p = torch.nn.Parameter(m0.clone())
+    opt = torch.optim.SGD([p], lr=0.01, momentum=0.9, weight_decay=1e-3)
+    if not first:
+        opt.state[p]["momentum_buffer"] = v0.clone()
+    p.grad = g16.float() * 0.5
+    opt.step()
+    hp = torch.tensor([0.01, 0.9, 0.0, 1e-3, 0.5, 0, 0, 0], device=DEV)
+    ops = HipOps()
+    # two halves: offsets into the master/momentum/shadow AND the bf16 buffer
+    h = (ar.numel // 2) // 4 * 4
+    ops.sgd(ar, hp, False, first, offset=0, numel=h, grad_bf16=g16)
+    ops.sgd(ar, hp, False, first, offset=h, numel=ar.numel - h, grad_bf16=g16)
+    torch.testing.assert_close(ar.master, p.detach(), rtol=1e-6, atol=1e-6)
+    torch.testing.assert_close(ar.momentum, opt.state[p]["momentum_buffer"], rtol=1e-6, atol=1e-6)
+    assert torch.equal(ar.shadow, ar.master.to(torch.bfloat16))
+    assert torch.equal(ar.grad, g0), "the fp32 gradient arena must stay untouched"
+    # the same update from the fp32 copy of those values is bitwise identical
+    ar2 = Arena([(64, 200), (1, 64)], DEV, shadow_dtype=torch.bfloat16)
+    ar2.master.copy_(m0)
+    ar2.momentum.copy_(v0)
+    ar2.grad.copy_(g16.float())
+    ops.sgd(ar2, hp, False, first)
+    assert torch.equal(ar2.master, ar.master) and torch.equal(ar2.momentum, ar.momentum)
+    # fixed-grid ("background") launch == default launch, bitwise
+    ar3 = Arena([(64, 200), (1, 64)], DEV, shadow_dtype=torch.bfloat16)
+    ar3.master.copy_(m0)
+    ar3.momentum.copy_(v0)
+    ar3.grad.copy_(g16.float())
+    _lib().sgd_momentum_bg(ar3.master.data_ptr(), ar3.grad.data_ptr(), ar3.momentum.data_ptr(),
+                           ar3.shadow.data_ptr(), ar3.numel, hp.data_ptr(), 0, int(first), 1, 3,
+                           torch.cuda.current_stream().cuda_stream)
+    assert torch.equal(ar3.master, ar.master) and torch.equal(ar3.momentum, ar.momentum)
+    assert torch.count_nonzero(ar3.grad) == 0
+
+
 @pytest.mark.parametrize("tile", [256, 128])
 @pytest.mark.parametrize("M,N,K", [(600, 520, 200), (4096, 1024, 512)])
 def test_forced_tile_fwd_dgrad_wgrad(tile, M, N, K):

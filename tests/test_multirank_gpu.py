@@ -169,11 +169,14 @@ def test_rccl_grouped_overlap_two_ranks_bitwise():
     assert torch.equal(a[0]["final"], c[0]["final"])
 
 
-def test_rccl_chunked_buckets_two_ranks_bitwise():
+@pytest.mark.parametrize("grad_dtype", ["fp32", "bf16"])
+def test_rccl_chunked_buckets_two_ranks_bitwise(grad_dtype):
     """Sub-layer (output-row chunk) buckets at P=2 on 1024-wide layers (chunking forced small
-    with NNMPI_CHUNK_MIN_TILES): chunk all-reduces overlapped == inline, bit for bit."""
-    kw = dict(widths=[1024, 1024, 1024, 1], n_features=1024, n_samples=1024, lr=1e-4,
-              bucket_mb=1.0)
+    with NNMPI_CHUNK_MIN_TILES): chunk all-reduces overlapped == inline, bit for bit.  With the
+    bf16 payload (256 rows per rank: un-split weight gradients) the overlapped chunks' GEMM
+    epilogues write the bf16 payload themselves."""
+    kw = dict(widths=[1024, 1024, 1024, 1], n_features=1024, lr=1e-4, bucket_mb=1.0,
+              grad_dtype=grad_dtype, n_samples=1024 if grad_dtype == "fp32" else 512)
 
     def env(r):
         return dict(rccl_env(r), NNMPI_CHUNK_MIN_TILES="4")

@@ -219,3 +219,12 @@ def test_arena_tiny_bucket_merge_and_row_chunks():
     assert big.buckets_completed_by(1) == ch
     # buckets larger than the layer: no chunks
     assert Arena([(8192, 8192), (1, 8192)], "meta", bucket_bytes=1 << 30).layer_chunks == {}
+
+
+def test_subtract_ranges():
+    from nnmpi_amd.parallel.sync import _subtract
+    assert _subtract((0, 10), []) == [(0, 10)]
+    assert _subtract((0, 10), [(0, 10)]) == []
+    assert _subtract((0, 10), [(2, 4), (6, 8)]) == [(0, 2), (4, 6), (8, 10)]
+    assert _subtract((5, 10), [(0, 6), (9, 20)]) == [(6, 9)]
+    assert _subtract((5, 10), [(10, 12), (0, 5)]) == [(5, 10)]
