@@ -78,6 +78,7 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
   m.def("set_gemm_variant", &set_gemm_variant);
   m.def("set_fwd_variant", &set_fwd_variant);
   m.def("set_store_policy", &set_store_policy);
+  m.def("set_pp256_order", &set_pp256_order);
   m.def("set_head_xcd_rows", &set_head_xcd_rows);
   m.def("linear_fwd_bf16_stamped", [](uptr X, int ldx, uptr W, int ldw, uptr bias, uptr Y, int ldy,
                                       int M, int N, int K, uptr st, uptr s) {
@@ -103,6 +104,11 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
                                M, N, K, nullptr, S(s),
                                nullptr, nullptr, P<bf16>(dW16), P<bf16>(db16)),
           "linear_wgrad_bf16_out16");
+  });
+  m.def("gemm_bf16_tile", [](uptr A, int lda, int la, uptr B, int ldb, int lb, int M, int N, int K,
+                             uptr C, int ldc, int tile, uptr s) {
+    check(gemm_bf16_generic_tile(P<const bf16>(A), lda, la, P<const bf16>(B), ldb, lb, M, N, K,
+                                 P<float>(C), ldc, tile, S(s)), "gemm_bf16_tile");
   });
   m.def("gemm_bf16", [](uptr A, int lda, int la, uptr B, int ldb, int lb, int M, int N, int K, uptr C,
                         int ldc, uptr s) {

@@ -1184,6 +1184,12 @@ static hipError_t launch_dma(GemmParams p, int splits, hipStream_t s) {
 // DMA-path variants (experiments select one with set_gemm_variant; 0 = default).
 static int g_variant = 0;
 void set_gemm_variant(int v) { g_variant = v; }
+// 256x256 ping-pong kernel tile order per epilogue (index into its kernel table: 0 GM 4,
+// 1 early reads GM 1, 2 GM 1, 3 GM 8): forward, dgrad, weight gradient
+static int g_pp_order[3] = {0, 0, 2};
+void set_pp256_order(int epi, int idx) {
+  if (epi >= 0 && epi < 3 && idx >= 0 && idx < 4) g_pp_order[epi] = idx;
+}
 
 // Kernel-selection knobs of the training step (scripts/step_ab.py A/Bs them; -1 / 0 = default).
 static int g_fwd_variant = -1;    // forward GEMM main-loop variant (launch_t's switch)
@@ -1205,7 +1211,8 @@ static hipError_t launch_t(GemmParams p, int splits, hipStream_t s, int variant 
     dim3 grid((p.N + 255) / 256, (p.M + 255) / 256, splits);
     set_extents<LA, LB>(p);
     // default: reads retired after the barrier + grouped tile order (GM 4); A/B variants:
-    // 16 = both off (previous default), 17 = late reads + row-major order, 18 = GM 8
+    // 15 = GM 4 (the non-fp32 default), 16 = both off (previous default), 17 = late reads +
+    // row-major order (the fp32 default), 18 = GM 8
     using K = void (*)(GemmParams);
     static const K kfns[4] = {gemm_bf16_pp256_kernel<LA, LB, EPI, ACT, BG, true, 4>,
                               gemm_bf16_pp256_kernel<LA, LB, EPI, ACT, BG, false, 1>,
@@ -1213,8 +1220,8 @@ static hipError_t launch_t(GemmParams p, int splits, hipStream_t s, int variant 
                               gemm_bf16_pp256_kernel<LA, LB, EPI, ACT, BG, true, 8>};
     // (the weight gradient -- XMAJ x XMAJ, 4 waves of tiles at 8192 wide -- measured 2-3 %
     // faster in row-major order: profiles/gemm_wide8192_pp256_variants.json)
-    const int dflt = EPI == EPI_F32 ? 2 : 0;
-    const K kfn = kfns[(variant >= 16 && variant <= 18) ? variant - 15 : dflt];
+    const int dflt = g_pp_order[EPI];
+    const K kfn = kfns[(variant >= 15 && variant <= 18) ? variant - 15 : dflt];
     static bool attr = false;
     if (!attr) {
       for (K f : kfns)
@@ -1402,6 +1409,28 @@ hipError_t linear_wgrad_bf16(const bf16* dZ, int lddz, const bf16* X, int ldx, f
                              float* db, int M, int N, int K, float* ws, hipStream_t s,
                              const SgdFuse* sgd) {
   return linear_wgrad_bf16_deferred(dZ, lddz, X, ldx, dW, db, M, N, K, ws, s, sgd, nullptr);
+}
+
+hipError_t gemm_bf16_generic(const bf16* A, int lda, int la, const bf16* B, int ldb, int lb,
+                             int M, int N, int K, float* C, int ldc, hipStream_t s);
+
+hipError_t gemm_bf16_generic_tile(const bf16* A, int lda, int la, const bf16* B, int ldb, int lb,
+                                  int M, int N, int K, float* C, int ldc, int tile, hipStream_t s) {
+  // The same plain GEMM through the 256x256 ping-pong kernel (tile 256) or the 128x128 DMA
+  // kernel (tile 128): operand-layout experiments on the production tiles.
+  if (tile != 256 && tile != 128) return gemm_bf16_generic(A, lda, la, B, ldb, lb, M, N, K, C, ldc, s);
+  GemmParams p{};
+  p.A = A; p.lda = lda; p.B = B; p.ldb = ldb; p.M = M; p.N = N; p.K = K;
+  p.k_per_split = ((K + GEMM_BK - 1) / GEMM_BK) * GEMM_BK;
+  p.C = C; p.ldc = ldc;
+#define NNMPI_GT(T)                                                                              \
+  if (la == KMAJ && lb == KMAJ) return launch_t<T, T, KMAJ, KMAJ, EPI_F32, ACT_NONE, false>(p, 1, s); \
+  if (la == KMAJ && lb == XMAJ) return launch_t<T, T, KMAJ, XMAJ, EPI_F32, ACT_NONE, false>(p, 1, s); \
+  if (la == XMAJ && lb == KMAJ) return launch_t<T, T, XMAJ, KMAJ, EPI_F32, ACT_NONE, false>(p, 1, s); \
+  return launch_t<T, T, XMAJ, XMAJ, EPI_F32, ACT_NONE, false>(p, 1, s);
+  if (tile == 256) { NNMPI_GT(256) }
+  NNMPI_GT(128)
+#undef NNMPI_GT
 }
 
 hipError_t gemm_bf16_generic(const bf16* A, int lda, int la, const bf16* B, int ldb, int lb,

@@ -57,6 +57,7 @@ void set_gemm_tile(int t);     // 0 = heuristic, 64 / 128 = force (experiments)
 void set_gemm_variant(int v);  // DMA-path main-loop variant (experiments), 0 = default
 // step-level kernel-selection knobs (-1 / 0 = built-in default; scripts/step_ab.py)
 void set_fwd_variant(int v);   // forward GEMM (128x128 tiles) main-loop variant
+void set_pp256_order(int epi, int idx);   // 256x256 kernel tile order per epilogue (A/B)
 void set_store_policy(int p);  // LDS-epilogue output stores: 0 plain, 1 nt, 2 sc1 (experiments)
 void set_head_xcd_rows(int v);  // head kernels: rows of XCD-remapped logical blocks (experiment)
 // diagnostic: the default 128x128 forward kernel with per-block entry/exit real-time stamps
@@ -72,6 +73,8 @@ hipError_t linear_wgrad_bf16(const bf16* dZ, int lddz, const bf16* X, int ldx, f
                              const SgdFuse* sgd = nullptr);
 hipError_t gemm_bf16_generic(const bf16* A, int lda, int la, const bf16* B, int ldb, int lb,
                              int M, int N, int K, float* C, int ldc, hipStream_t s);
+hipError_t gemm_bf16_generic_tile(const bf16* A, int lda, int la, const bf16* B, int ldb, int lb,
+                                  int M, int N, int K, float* C, int ldc, int tile, hipStream_t s);
 // sgd != nullptr: instead of storing the reduced gradients, apply the optimizer update to the
 // parameters at the same arena positions (single-rank fast path: gradient final once reduced).
 hipError_t splitk_reduce(const float* ws, int S, long long stride, int M, int N, float* out,
