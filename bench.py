@@ -25,8 +25,11 @@ fastest schedule depends on the node's collective latency, so the candidates (on
 all-reduce; ZeRO-1 reduce-scatter + sharded SGD + bf16 all-gather; per-bucket all-reduce on a
 comm stream overlapped with backward) are each timed for ``--tune_steps`` steps BEFORE the timed
 region and the fastest (max over ranks, so every rank agrees) is kept; its time per candidate
-is reported in ``config.comm_tune_ms_per_step``.  Large gradients always overlap, with a bf16
-payload (``--grad_dtype auto``).
+is reported in ``config.comm_tune_ms_per_step``.  Large gradients (bf16 payload above 64 MB,
+``--grad_dtype auto``) are tuned too, overlap first: RCCL's all-reduce kernels hold CUs
+(256 threads, ~280 registers per wave, read from the gfx950 code object) that a one-wave
+256x256 GEMM launch needs, so on a real node whether the overlapped schedule beats one inline
+all-reduce is measured, not assumed.
 
 Rank 0 prints ONE JSON line.  The timed region is exactly K full training steps (forward,
 loss, backward, gradient all-reduce, optimizer update), bracketed by barrier + device sync on
@@ -355,10 +358,10 @@ def run(a, job):
     data = shard(n_global)
     mode = a.comm_mode
     if mode == "auto":
-        # small (latency-bound) gradients: the best collective schedule depends on the link
-        # latency of the node, so it is measured (untimed, before the timed region) rather than
-        # assumed; large gradients always overlap per-bucket all-reduces with the backward.
-        mode = "tune" if grad_bytes <= INLINE_MAX_GRAD_BYTES else "overlap"
+        # the best collective schedule depends on the node (link latency for small gradients,
+        # comm kernels competing with the GEMMs for CUs for large ones), so it is measured
+        # (untimed, before the timed region) rather than assumed
+        mode = "tune"
     if not use_comm:
         mode = "none"
     elif native_comm is None and mode == "tune":
@@ -384,9 +387,12 @@ def run(a, job):
         # overlap candidates: --bucket_mb buckets, and ~two buckets (the first all-reduce
         # larger, the exposed last one smaller than the whole gradient)
         half_mb = round(grad_bytes / 2 ** 20 * 0.6, 3)
-        cands = [("inline", None), ("zero1", None), ("overlap", a.bucket_mb)]
-        if half_mb > a.bucket_mb:
-            cands.append(("overlap", half_mb))
+        if grad_bytes > INLINE_MAX_GRAD_BYTES:
+            cands = [("overlap", a.bucket_mb), ("inline", None), ("zero1", None)]
+        else:
+            cands = [("inline", None), ("zero1", None), ("overlap", a.bucket_mb)]
+            if half_mb > a.bucket_mb:
+                cands.append(("overlap", half_mb))
         for m, bmb in cands:
             e = build(m, data, bucket_mb=bmb)
             e.run_steps(a.warmup, chunk_for(a.warmup))
