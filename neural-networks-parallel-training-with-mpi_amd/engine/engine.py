@@ -33,6 +33,9 @@ TINY_MAX_WIDTH = 16
 TINY_MAX_LAYERS = 4
 
 
+LOSS_HIST_MAX = 1024   # steps per loss-recording graph (run_steps(..., losses=...))
+
+
 class MLPEngine:
     def __init__(self, spec: MLPSpec, arena: Arena, ops, sync, *, device, dtype: torch.dtype,
                  rows_capacity: int, lr: float, momentum: float, dampening: float = 0.0,
@@ -605,40 +608,71 @@ class MLPEngine:
             n -= c
         return out
 
-    def prepare_steps(self, n: int, chunk: int = 16):
-        """Capture (without running) every graph that run_steps(n, chunk) will replay."""
+    def prepare_steps(self, n: int, chunk: int = 16, losses: bool = False):
+        """Capture (without running) every graph that run_steps(n, chunk) will replay
+        (``losses``: the form that records every step's loss, see run_steps)."""
         if not (self.is_cuda and self.use_graph and self.timer is None and self.steps_done > 0):
             return
         with torch.cuda.stream(self.stream):
             for c in set(self._chunks(n, chunk)):
-                key = (self.rows, self.inv_count, self.loss_scale, c)
+                key = (self.rows, self.inv_count, self.loss_scale, c, losses)
                 if key not in self._graphs:
-                    self._graphs[key] = self._capture(c)
+                    self._graphs[key] = self._capture(c, hist=losses)
 
-    def run_steps(self, n: int, chunk: int = 16):
+    def run_steps(self, n: int, chunk: int = 16, losses: Optional[torch.Tensor] = None):
         """n optimizer steps (asynchronous on the GPU).  In graph mode the steps are replayed as
-        graphs of up to `chunk` consecutive steps; results are identical to n step() calls."""
+        graphs of up to `chunk` consecutive steps; results are identical to n step() calls.
+
+        ``losses``: a device fp32 tensor of >= n entries; step k's loss (what loss() would
+        return right after it) lands in losses[k] -- per-step losses without a host sync per
+        step (the compat trainer's full-batch epochs).  Written on the engine's stream:
+        synchronize() before reading them on the host."""
+        k0 = 0
+
+        def keep(k):
+            if losses is not None:
+                losses[k:k + 1].copy_(self.loss_out[:1])
         if not (self.is_cuda and self.use_graph and self.timer is None):
-            for _ in range(n):
+            ctx = torch.cuda.stream(self.stream) if self.is_cuda else _nullctx()
+            for k in range(n):
                 self.step()
+                with ctx:
+                    keep(k)
             return
         if n > 0 and self.steps_done == 0:
             self.step()          # eager first step (momentum initialisation semantics)
+            with torch.cuda.stream(self.stream):
+                keep(0)
             n -= 1
+            k0 = 1
+        hist = losses is not None
         try:
-            self.prepare_steps(n, chunk)
+            self.prepare_steps(n, chunk, losses=hist)
         except RuntimeError:
-            for _ in range(n):   # capture unavailable: step() falls back to eager by itself
+            for k in range(n):   # capture unavailable: step() falls back to eager by itself
                 self.step()
+                with torch.cuda.stream(self.stream):
+                    keep(k0 + k)
             return
         with torch.cuda.stream(self.stream):
             for c in self._chunks(n, chunk):
-                self._graphs[(self.rows, self.inv_count, self.loss_scale, c)].launch(
+                self._graphs[(self.rows, self.inv_count, self.loss_scale, c, hist)].launch(
                     int(self.stream.cuda_stream))
+                if hist:
+                    losses[k0:k0 + c].copy_(self._loss_hist[:c])
                 self.steps_done += c
+                k0 += c
 
-    def _capture(self, nsteps: int = 1):
+    def _capture(self, nsteps: int = 1, hist: bool = False):
+        """One graph of ``nsteps`` consecutive steps; ``hist``: step k also copies its loss into
+        self._loss_hist[k] (a node inside the graph)."""
         from .. import native
+        if hist:
+            # allocated once: captured graphs keep writing to this address
+            if getattr(self, "_loss_hist", None) is None:
+                self._loss_hist = torch.zeros(LOSS_HIST_MAX, dtype=torch.float32, device=self.device)
+            if nsteps > LOSS_HIST_MAX:
+                raise ValueError(f"loss-recording graphs hold at most {LOSS_HIST_MAX} steps")
         g = native.lib().GraphRunner()
         origin = self.sync.capture_origin()
         if origin is None:
@@ -649,8 +683,10 @@ class MLPEngine:
                 # collectives live on the comm stream: it is the capture origin, the compute
                 # stream forks from it here and joins back below (see GradSync.capture_origin)
                 self.stream.wait_stream(origin)
-            for _ in range(nsteps):
+            for k in range(nsteps):
                 self._step_body(False)
+                if hist:
+                    self._loss_hist[k:k + 1].copy_(self.loss_out[:1])
             if origin is not self.stream:
                 origin.wait_stream(self.stream)
         except Exception:

@@ -74,6 +74,7 @@ class TrainConfig:
     bucket_mb: float = 1.0
     overlap: bool = True
     graph: bool = True                # capture the steady-state step in a HIP graph
+    fast_epochs: bool = True          # full-batch GPU epochs replayed 64 per graph (same output)
     grad_dtype: str = "fp32"          # fp32 | bf16 (all-reduce payload dtype)
     shard_optimizer: bool = False     # ZeRO-1: reduce-scatter grads, SGD on own 1/P, all-gather
     deterministic: bool = True
@@ -157,6 +158,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--bucket_mb", type=float, default=1.0)
     p.add_argument("--no_overlap", dest="overlap", action="store_false")
     p.add_argument("--no_graph", dest="graph", action="store_false")
+    p.add_argument("--no_fast_epochs", dest="fast_epochs", action="store_false",
+                   help="one graph replay + loss readback per epoch (default: 64 epochs per "
+                        "replay, losses recorded on the device; identical output)")
     p.add_argument("--grad_dtype", choices=["fp32", "bf16"], default="fp32")
     p.add_argument("--shard_optimizer", "--zero1", dest="shard_optimizer", action="store_true",
                    help="sharded optimizer state (ZeRO-1): reduce-scatter gradients, SGD on this "

@@ -564,3 +564,25 @@ def test_general_head_with_comm_overlap_bitwise_equal():
     b = trainer.run_worker(TrainConfig(device="cuda", comm="none", **kw))
     assert a.losses == b.losses
     assert torch.equal(a.final_params, b.final_params)
+
+
+@pytest.mark.parametrize("widths", [[512, 512, 512, 1], [2, 3, 1]])
+def test_fast_epochs_same_output_as_per_epoch_steps(widths, capsys):
+    """Full-batch epochs replayed 64 per graph with per-step losses recorded on the device print
+    the same lines with the same losses, and end with the same parameters, as one replay + one
+    loss readback per epoch (70 epochs: an eager first step, a 63-step and a 6-step graph)."""
+    kw = dict(widths=widths, n_features=widths[0], nepochs=70, lr=1e-5, print_rank="0")
+    if widths[0] == 2:
+        kw = dict(nepochs=70, print_rank="0", dtype="fp32")
+        a = trainer.run_worker(TrainConfig(device="cuda", **kw))
+        out_a = capsys.readouterr().out
+        b = trainer.run_worker(TrainConfig(device="cuda", fast_epochs=False, **kw))
+    else:
+        a = trainer.run_worker(_cfg(device="cuda", n_samples=4096, **kw))
+        out_a = capsys.readouterr().out
+        b = trainer.run_worker(_cfg(device="cuda", n_samples=4096, fast_epochs=False, **kw))
+    out_b = capsys.readouterr().out
+    assert a.losses == b.losses and len(a.losses) == 70
+    assert torch.equal(a.final_params, b.final_params)
+    lines = lambda o: [l for l in o.splitlines() if l.startswith(("[ = =", "loss in worker"))]  # noqa: E731
+    assert lines(out_a) == lines(out_b) and len(lines(out_a)) == 140
