@@ -548,8 +548,45 @@ def run(a, job):
             "final_loss": loss,
         }
         print(json.dumps(out), flush=True)
+    # Teardown, in order, each step timed on stderr (NNMPI_TEARDOWN_TRACE=1): the graphs (which
+    # hold captured RCCL kernels) and engines first, then the communicator, then the process
+    # group.  The result is already printed: a teardown that stalls (a communicator destroy
+    # waiting on a peer that has gone) must not keep the job alive, so a watchdog ends the
+    # process after TEARDOWN_S seconds.
+    _exit_watchdog(TEARDOWN_S)
+    if gpu:
+        torch.cuda.synchronize()
+    _trace("teardown: engines and graphs")
+    eng = None
+    import gc
+    gc.collect()
+    _trace("teardown: communicator")
     native_comm = None
+    gc.collect()
+    _trace("teardown: process group")
     pg.destroy()
+    _trace("teardown: done")
+
+
+TEARDOWN_S = 60.0
+
+
+def _trace(msg: str):
+    if os.environ.get("NNMPI_TEARDOWN_TRACE") == "1":
+        print(f"[bench rank {os.environ.get('RANK', '0')} {time.strftime('%H:%M:%S')}] {msg}",
+              file=sys.stderr, flush=True)
+
+
+def _exit_watchdog(seconds: float):
+    import threading
+
+    def fire():
+        print(f"[bench] teardown did not finish in {seconds:.0f} s: exiting (result already "
+              "printed)", file=sys.stderr, flush=True)
+        os._exit(0)
+    t = threading.Timer(seconds, fire)
+    t.daemon = True
+    t.start()
 
 
 def _time_comm_only(sync, n, chunk, use_graph, barrier, max_over_ranks) -> float:
