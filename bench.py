@@ -205,7 +205,12 @@ def main(argv=None):
         a.device = "cuda" if torch.cuda.device_count() > 0 else "cpu"
     if a.device == "cuda":
         have = torch.cuda.device_count()
-        if have < job.local_world and not a.shared_gpu_rehearsal:
+        # a launcher may hand every rank exactly one device through a visibility variable
+        # (then each rank sees 1 GPU and uses it); otherwise fewer GPUs than local ranks is
+        # refused before anything runs
+        isolated = have == 1 and any(os.environ.get(v) for v in (
+            "HIP_VISIBLE_DEVICES", "ROCR_VISIBLE_DEVICES", "CUDA_VISIBLE_DEVICES"))
+        if have < job.local_world and not isolated and not a.shared_gpu_rehearsal:
             _fail(f"{job.local_world} local ranks need as many GPUs; {have} visible "
                   "(one rank per GPU: RCCL refuses two ranks on one device)")
     run(a, job)
