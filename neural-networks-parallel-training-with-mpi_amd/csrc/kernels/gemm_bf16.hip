@@ -1500,7 +1500,10 @@ static bool group_enabled() {
 
 bool bwd_group_supported(int rows, int out_f, int in_f) {
   // the grouped kernel covers the 128x128 tile shapes of the default DMA main loop
-  return group_enabled() && gemm_impl() == 2 && g_variant == 0 && pick_tile(rows, in_f) == 128 &&
+  // (small batches, whose standalone dgrad would take 64x64 tiles, run grouped too: the grouped
+  // launch saves two launch boundaries per layer, which is what a small-batch step is made of;
+  // the accumulation order does not depend on the tile, so results are identical)
+  return group_enabled() && gemm_impl() == 2 && g_variant == 0 && pick_tile(rows, in_f) != 256 &&
          wgrad_tile(out_f, in_f) == 128;
 }
 
@@ -1518,7 +1521,7 @@ hipError_t bwd_group(const DgradArgs* dg, const WgradArgs* wg, const SlabReduce*
   if (dg && wg && splits == 1 && wg->sg.g_base) return hipErrorInvalidValue;
   // the grouped kernel covers the 128x128 tile shapes of the default DMA main loop
   bool ok = group_enabled() && gemm_impl() == 2 && g_variant == 0;
-  if (dg) ok = ok && pick_tile(dg->M, dg->N) == 128;
+  if (dg) ok = ok && pick_tile(dg->M, dg->N) != 256;
   if (wg) ok = ok && wgrad_tile(wg->M, wg->N) == 128 && wg->db != nullptr &&
                (splits == 1 || wg->ws != nullptr);
   if (!ok) {

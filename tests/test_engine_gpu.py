@@ -154,6 +154,19 @@ def test_grouped_backward_is_bitwise_equal(comm):
     assert torch.equal(a.final_params, b.final_params)
 
 
+@pytest.mark.parametrize("rows", [1024, 16])
+def test_grouped_backward_small_batches_bitwise_equal(rows):
+    """Small per-rank batches (strong-scaling shards: 8192 / 8 rows) run the grouped backward
+    with 128x128 tiles where the standalone dgrad takes 64x64: same accumulation order, so bit
+    for bit the separate launches."""
+    kw = dict(device="cuda", widths=[512, 512, 512, 1], n_features=512, n_samples=rows,
+              lr=1e-5, nepochs=5)
+    a = trainer.run_worker(_cfg(**kw))
+    b = _run_ungrouped(_cfg(**kw))
+    assert a.losses == b.losses
+    assert torch.equal(a.final_params, b.final_params)
+
+
 def test_grouped_backward_xent_head_bitwise_equal():
     cfg = TrainConfig(device="cuda", widths=[784, 1024, 1024, 10], n_features=784, loss="xent",
                       n_samples=2048, dtype="bf16", nepochs=4, lr=0.05, print_rank="none",
