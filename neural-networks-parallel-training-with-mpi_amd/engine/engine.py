@@ -102,8 +102,11 @@ class MLPEngine:
         self.comm_overlap = isinstance(sync, NativeRcclSync) and not sync.inline
         # (shapes the grouped kernel does not cover -- e.g. the 256x256-tile 8192-wide layers --
         # take the sequential fused schedule, whose un-split wgrads apply SGD in their epilogue)
+        # (layers cut into output-row chunk buckets are reduced chunk by chunk behind their own
+        # weight-gradient launches: the sequential schedule, never the grouped one)
         self.grouped = (bool(grouped) and self.overlap and dtype == torch.bfloat16
                         and (inline_sync or self.comm_overlap)
+                        and not any(getattr(b, "rows", None) is not None for b in arena.buckets)
                         and hasattr(ops, "bwd_group") and L > 1 and
                         all(ops.bwd_group_supported(self.R, *spec.layer_shape(i))
                             for i in range(L - 1)))
