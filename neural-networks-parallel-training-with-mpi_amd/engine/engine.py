@@ -159,12 +159,14 @@ class MLPEngine:
         # there, so the write is ordered before the next step and after the previous one
         ctx = torch.cuda.stream(self.stream) if self.is_cuda else _nullctx()
         with ctx, torch.no_grad():
+            # fill_ with a scalar is a kernel launch (capturable inside a graph, e.g. the
+            # per-step scales of run_epoch); item assignment would copy a host tensor
             if lr is not None:
-                self.hp[0] = lr
+                self.hp[0:1].fill_(float(lr))
             if momentum is not None:
-                self.hp[1] = momentum
+                self.hp[1:2].fill_(float(momentum))
             if grad_scale is not None:
-                self.hp[4] = grad_scale
+                self.hp[4:5].fill_(float(grad_scale))
 
     def set_scales(self, inv_count: float, loss_scale: float, grad_scale: float):
         """Loss-gradient scale (1/count), reported-loss scale, optimizer gradient scale (1/P)."""
@@ -666,16 +668,63 @@ class MLPEngine:
                 self.steps_done += c
                 k0 += c
 
+    def run_epoch(self, X: torch.Tensor, Y: Optional[torch.Tensor],
+                  labels: Optional[torch.Tensor], perm: torch.Tensor, plan) -> None:
+        """One mini-batch epoch as ONE graph replay: for every ``(lo, hi, inv_count, loss_scale,
+        grad_scale)`` of ``plan`` the rows ``perm[lo:hi]`` of the resident shard are gathered
+        into the input buffers and a step is taken with those scales -- exactly what
+        load_batch_indexed + set_scales + step() do per step, with the per-step host work
+        gone.  ``perm`` must be the same device buffer every epoch (rewrite its contents; the
+        graph holds its address).  Falls back to those per-step calls when graphs are off or
+        no step has run yet."""
+        plan = [tuple(p) for p in plan]
+
+        def body():
+            for lo, hi, inv, lsc, gsc in plan:
+                self.load_batch_indexed(X, Y, labels, perm[lo:hi])
+                self.set_scales(inv, lsc, gsc)
+                self._step_body(False)
+        if not (self.is_cuda and self.use_graph and self.timer is None and self.steps_done > 0):
+            for lo, hi, inv, lsc, gsc in plan:
+                self.load_batch_indexed(X, Y, labels, perm[lo:hi])
+                self.set_scales(inv, lsc, gsc)
+                self.step()
+            return
+        key = ("epoch", tuple(plan), X.data_ptr(), perm.data_ptr(),
+               None if Y is None else Y.data_ptr(), None if labels is None else labels.data_ptr())
+        with torch.cuda.stream(self.stream):
+            g = self._graphs.get(key)
+            if g is None:
+                g = self._capture_fn(body)
+                self._graphs[key] = g
+            else:
+                # the host-side state the per-step calls would leave behind (rows, scales)
+                lo, hi, inv, lsc, gsc = plan[-1]
+                self.rows = hi - lo
+                self.inv_count, self.loss_scale = float(inv), float(lsc)
+            g.launch(int(self.stream.cuda_stream))
+        self.steps_done += len(plan)
+
     def _capture(self, nsteps: int = 1, hist: bool = False):
         """One graph of ``nsteps`` consecutive steps; ``hist``: step k also copies its loss into
         self._loss_hist[k] (a node inside the graph)."""
-        from .. import native
         if hist:
             # allocated once: captured graphs keep writing to this address
             if getattr(self, "_loss_hist", None) is None:
                 self._loss_hist = torch.zeros(LOSS_HIST_MAX, dtype=torch.float32, device=self.device)
             if nsteps > LOSS_HIST_MAX:
                 raise ValueError(f"loss-recording graphs hold at most {LOSS_HIST_MAX} steps")
+
+        def body():
+            for k in range(nsteps):
+                self._step_body(False)
+                if hist:
+                    self._loss_hist[k:k + 1].copy_(self.loss_out[:1])
+        return self._capture_fn(body)
+
+    def _capture_fn(self, body):
+        """Capture ``body()`` (work on the engine's streams) as one replayable graph."""
+        from .. import native
         g = native.lib().GraphRunner()
         origin = self.sync.capture_origin()
         if origin is None:
@@ -686,10 +735,7 @@ class MLPEngine:
                 # collectives live on the comm stream: it is the capture origin, the compute
                 # stream forks from it here and joins back below (see GradSync.capture_origin)
                 self.stream.wait_stream(origin)
-            for k in range(nsteps):
-                self._step_body(False)
-                if hist:
-                    self._loss_hist[k:k + 1].copy_(self.loss_out[:1])
+            body()
             if origin is not self.stream:
                 origin.wait_stream(self.stream)
         except Exception:

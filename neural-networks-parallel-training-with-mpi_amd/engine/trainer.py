@@ -390,6 +390,10 @@ def _run(j: Job) -> TrainResult:
     # loop, ref.py:150-224): replay FAST_EPOCHS epochs per graph, each step recording its loss
     # on the device, and print the lines after each replay -- same lines, same order, same
     # values, one host sync per replay instead of per epoch.
+    # mini-batch epochs (--batch_size): every epoch one graph replay of all its steps
+    mb_graph = (cfg.fast_epochs and j.device.type == "cuda" and eng.use_graph
+                and eng.timer is None and bool(bs) and K == 1)
+    perm_dev = None
     fast = (cfg.fast_epochs and j.device.type == "cuda" and eng.use_graph and eng.timer is None and not bs and K == 1
             and not (cfg.global_loss and world > 1) and cfg.val_fraction == 0 and seqchk is None
             and not (cfg.checkpoint and cfg.checkpoint_every) and fault is None)
@@ -453,6 +457,25 @@ def _run(j: Job) -> TrainResult:
                         full_loaded = True
                     rows_all = list(train_counts)
                 else:
+                    if mb_graph and s == 0 and eng.steps_done > 0:
+                        # the whole epoch's mini-batches as one graph replay (same gathers,
+                        # scales and steps as the per-step branch below)
+                        if perm_dev is None:
+                            perm_dev = torch.empty(rows_local, dtype=torch.int64, device=j.device)
+                        with torch.cuda.stream(eng.stream):
+                            perm_dev.copy_(perm if perm is not None else
+                                           torch.arange(rows_local, device=j.device))
+                        plan = []
+                        for s2 in range(steps_per_epoch):
+                            lo, hi = s2 * bs, min((s2 + 1) * bs, rows_local)
+                            ra = [max(0, min(bs, c - s2 * bs)) for c in train_counts]
+                            plan.append((lo, max(lo, hi)) + tuple(
+                                loss_scales(cfg, max(0, hi - lo), ra, cfg.widths[-1])))
+                        eng.run_epoch(Xc, Y, labels, perm_dev, plan)
+                        step_rows = eng.rows
+                        if wd:
+                            wd.kick()
+                        break
                     lo, hi = s * bs, min((s + 1) * bs, rows_local)
                     idx = perm[lo:hi] if perm is not None else torch.arange(lo, max(lo, hi), device=j.device)
                     eng.load_batch_indexed(Xc, Y, labels, idx.contiguous())

@@ -599,3 +599,15 @@ def test_fast_epochs_same_output_as_per_epoch_steps(widths, capsys):
     assert torch.equal(a.final_params, b.final_params)
     lines = lambda o: [l for l in o.splitlines() if l.startswith(("[ = =", "loss in worker"))]  # noqa: E731
     assert lines(out_a) == lines(out_b) and len(lines(out_a)) == 140
+
+
+@pytest.mark.parametrize("comm", ["none", "native"])
+def test_minibatch_epoch_graph_same_as_per_step(comm):
+    """--batch_size epochs replayed as one graph each (device gathers from a fixed permutation
+    buffer, per-step scales baked in, a short last batch) == the per-step loop, bit for bit."""
+    kw = dict(device="cuda", widths=[512, 512, 512, 1], n_features=512, n_samples=4000,
+              batch_size=1024, lr=1e-5, nepochs=5, comm=comm)
+    a = trainer.run_worker(_cfg(**kw))
+    b = trainer.run_worker(_cfg(fast_epochs=False, **kw))
+    assert a.losses == b.losses and a.steps == b.steps == 20
+    assert torch.equal(a.final_params, b.final_params)
