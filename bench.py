@@ -120,6 +120,8 @@ def parse(argv=None):
                         "NCCL_HOSTID, RCCL over loopback) to rehearse the multi-rank code path on "
                         "a 1-GPU box; the JSON line says so and its numbers are not a measurement")
     p.add_argument("--fwd_variant", type=int, default=-1, help="forward GEMM variant (experiments)")
+    p.add_argument("--gemm_variant", type=int, default=0,
+                   help="GEMM main-loop variant of every launch (experiments; 19 = deep-ring 256x256)")
     p.add_argument("--pp_order", default="",
                    help="256x256 GEMM tile order for fwd,dgrad,wgrad (0 GM4, 2 GM1, 3 GM8; experiments)")
     p.add_argument("--head_xcd_rows", type=int, default=0,
@@ -235,6 +237,7 @@ def run(a, job):
     if gpu:
         from nnmpi_amd import native
         native.lib().set_fwd_variant(a.fwd_variant)
+        native.lib().set_gemm_variant(a.gemm_variant)
         for epi, idx in enumerate(a.pp_order.split(",") if a.pp_order else []):
             native.lib().set_pp256_order(epi, int(idx))
         native.lib().set_group_async(a.group_async)

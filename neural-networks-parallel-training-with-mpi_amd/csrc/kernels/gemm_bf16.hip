@@ -983,6 +983,166 @@ __global__ void __launch_bounds__(PP_THREADS) gemm_bf16_pp256_kernel(GemmParams 
   epilogue_store<8, 4, EPI, ACT, BIASGRAD>(p, acc, accb, do_bg, mrow, ncol, lane, split);
 }
 
+// ------------------------------------------------------------------------------------------
+// Deep-ring twin of gemm_bf16_pp256_kernel: the same tile, waves, phases, fragment reads and
+// MFMA sections, but the LDS holds a RING of PP_RING = 10 half images (160 KiB, all of it)
+// instead of 2 K-tile buffers (8 halves), and DMA issue is uniform: the phase that reads half
+// q (read order q = 4t + ph: A0(t), B1(t), A1(t), B0(t+1); B0(0) is q = -1) issues half q + 8.
+//   slot(q) = (q + 1) mod 10;  slot(q + 8) == slot(q - 2): a half is restaged two phases after
+//   its read (the WAR margin of the 8-slot kernel, see LATE_LGKM above);
+//   before phase q's first barrier a counted vmcnt(14) retires half q + 1 (7 newer halves x 2
+//   DMA instructions per wave stay in flight), read in phase q + 1 (RAW, as above).
+// So 7-8 halves (112-128 KiB) are in flight per CU instead of 5-6: the L2/MALL -> LDS stream of
+// a 256x256 tile needs ~75 GB/s per CU at the MFMA rate, and the deeper issue-ahead is the
+// lever docs/PERF.md §4 names for the gap to hipBLASLt.
+// ------------------------------------------------------------------------------------------
+constexpr int PP_RING = 10;
+constexpr int PP_RING_SMEM = PP_RING * PP_HALF;   // 160 KiB
+
+template <int LA, int LB, int EPI, int ACT, bool BIASGRAD, int GM = 4>
+__global__ void __launch_bounds__(PP_THREADS) gemm_bf16_pp256_ring_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  constexpr int BK = GEMM_BK;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w >> 2, wn = w & 3;
+  const int gx = gridDim.x, gy = gridDim.y;
+  const int bid = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy);
+  int tx, ty;
+  grouped_tile(bid, gx, gy, GM, tx, ty);
+  const int split = blockIdx.z;
+  const int m0 = ty * 256, n0 = tx * 256;
+  const int kbeg = split * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int nt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+
+  const __amdgpu_buffer_rsrc_t rsA = __builtin_amdgcn_make_buffer_rsrc((void*)p.A, (short)0, (int)p.a_bytes, 0x00020000);
+  const __amdgpu_buffer_rsrc_t rsB = __builtin_amdgcn_make_buffer_rsrc((void*)p.B, (short)0, (int)p.b_bytes, 0x00020000);
+  DmaPlan<128, LA, 8> pa0, pa1;
+  DmaPlan<128, LB, 8> pb0, pb1;
+  pa0.init(w, lane, m0, p.M, p.lda);
+  pa1.init(w, lane, m0 + 128, p.M, p.lda);
+  pb0.init(w, lane, n0, p.N, p.ldb);
+  pb1.init(w, lane, n0 + 128, p.N, p.ldb);
+  auto slot = [&](int q) { return smem + ((q + 1 + PP_RING) % PP_RING) * PP_HALF; };
+  auto kof = [&](int t) { return kbeg + t * BK; };
+  // issue half q of the read order (its type is q & 3; q = -1 is B0(0))
+  auto issue = [&](int q) {
+    const int r = q & 3, t = q >> 2;   // arithmetic shift: q = -1 -> r 3, t -1 -> B0(0)
+    char* dst = slot(q);
+    if (r == 0) pa0.issue(rsA, dst, w, kof(t), kend);
+    else if (r == 1) pb1.issue(rsB, dst, w, kof(t), kend);
+    else if (r == 2) pa1.issue(rsA, dst, w, kof(t), kend);
+    else pb0.issue(rsB, dst, w, kof(t + 1), kend);
+  };
+
+  f32x4 acc[8][4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  float rsum[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) rsum[i] = 0.f;
+  const bool do_bg = BIASGRAD && tx == 0 && wn == 0;
+
+  // prologue: halves -1 .. 7 (B0(0), then K-tiles 0 and 1, then B0(2)); retire -1 and 0
+#pragma unroll
+  for (int q = -1; q < 8; ++q) issue(q);
+  wait_vm<14>();
+  __builtin_amdgcn_s_barrier();
+
+  bf16x8 af[4][2], b0f[2][2], b0n[2][2], b1f[2][2];
+#pragma unroll
+  for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) b0n[jj][kk] = read_frag_async<128, LB>(slot(-1), wn * 32 + jj * 16, kk, lane);
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_sched_barrier(0);
+  if (wm == 1) __builtin_amdgcn_s_barrier();   // wave row 1 runs one barrier behind
+
+  for (int t = 0; t < nt; ++t) {
+#pragma unroll
+    for (int ph = 0; ph < 4; ++ph) {
+      const int q = 4 * t + ph;
+      const char* cur = slot(q);
+      if (ph == 0 || ph == 2) {
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) af[i][kk] = read_frag_async<128, LA>(cur, wm * 64 + i * 16, kk, lane);
+      }
+      if (ph == 0) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) b0f[jj][kk] = b0n[jj][kk];
+      } else if (ph == 1) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) b1f[jj][kk] = read_frag_async<128, LB>(cur, wn * 32 + jj * 16, kk, lane);
+      } else if (ph == 3) {
+#pragma unroll
+        for (int jj = 0; jj < 2; ++jj)
+#pragma unroll
+          for (int kk = 0; kk < 2; ++kk) b0n[jj][kk] = read_frag_async<128, LB>(cur, wn * 32 + jj * 16, kk, lane);
+      }
+      // half q + 8 (same type as q: compile-time per phase) into the slot of half q - 2
+      if (ph == 0) pa0.issue(rsA, slot(q + 8), w, kof(t + 2), kend);
+      else if (ph == 1) pb1.issue(rsB, slot(q + 8), w, kof(t + 2), kend);
+      else if (ph == 2) pa1.issue(rsA, slot(q + 8), w, kof(t + 2), kend);
+      else pb0.issue(rsB, slot(q + 8), w, kof(t + 3), kend);
+      wait_vm<14>();                                 // half q + 1 has landed (this wave's part)
+      __builtin_amdgcn_sched_barrier(0);
+      __builtin_amdgcn_s_barrier();
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+      const int hA = ph >> 1;
+      const int hB = (ph == 1 || ph == 2) ? 1 : 0;
+      __builtin_amdgcn_s_setprio(1);
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 4; ++i)
+#pragma unroll
+          for (int jj = 0; jj < 2; ++jj)
+            acc[hA * 4 + i][hB * 2 + jj] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(
+                hB ? b1f[jj][kk] : b0f[jj][kk], af[i][kk], acc[hA * 4 + i][hB * 2 + jj], 0, 0, 0);
+      if constexpr (BIASGRAD) {
+        if (do_bg && (ph == 0 || ph == 2)) {
+#pragma unroll
+          for (int i = 0; i < 4; ++i)
+#pragma unroll
+            for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+              for (int e = 0; e < 8; ++e) rsum[hA * 4 + i] += (float)af[i][kk][e];
+        }
+      }
+      __builtin_amdgcn_s_setprio(0);
+      __builtin_amdgcn_s_barrier();
+    }
+  }
+  if (wm == 0) __builtin_amdgcn_s_barrier();   // balance the stagger
+  wait_vm<0>();                                  // trailing out-of-range DMAs
+  f32x4 accb[8];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    float v = rsum[i];
+    if constexpr (BIASGRAD) {
+      v += __shfl_xor(v, 16);
+      v += __shfl_xor(v, 32);
+    }
+    accb[i] = f32x4{v, v, v, v};
+  }
+  int mrow[8], ncol[4];
+#pragma unroll
+  for (int i = 0; i < 8; ++i) mrow[i] = m0 + (i >> 2) * 128 + wm * 64 + (i & 3) * 16 + (lane & 15);
+#pragma unroll
+  for (int j = 0; j < 4; ++j) ncol[j] = n0 + (j >> 1) * 128 + wn * 32 + (j & 1) * 16 + (lane >> 4) * 4;
+  epilogue_store<8, 4, EPI, ACT, BIASGRAD>(p, acc, accb, do_bg, mrow, ncol, lane, split);
+}
+
 // Deterministic split-K / partial-slab combine (the three jobs a backward needs), 512-thread
 // blocks (8 waves):
 //   main blocks   out[m][n] = sum_z ws[z][m][n]     (float4 columns)
@@ -1221,13 +1381,22 @@ static hipError_t launch_t(GemmParams p, int splits, hipStream_t s, int variant 
     // (the weight gradient -- XMAJ x XMAJ, 4 waves of tiles at 8192 wide -- measured 2-3 %
     // faster in row-major order: profiles/gemm_wide8192_pp256_variants.json)
     const int dflt = g_pp_order[EPI];
-    const K kfn = kfns[(variant >= 15 && variant <= 18) ? variant - 15 : dflt];
+    // 19 / 20: the 10-slot deep-ring twin, grouped (GM 4) / row-major tile order
+    static const K rfns[2] = {gemm_bf16_pp256_ring_kernel<LA, LB, EPI, ACT, BG, 4>,
+                              gemm_bf16_pp256_ring_kernel<LA, LB, EPI, ACT, BG, 1>};
     static bool attr = false;
     if (!attr) {
       for (K f : kfns)
         (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, PP_SMEM);
+      for (K f : rfns)
+        (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, PP_RING_SMEM);
       attr = true;
     }
+    if (variant == 19 || variant == 20) {
+      hipLaunchKernelGGL(rfns[variant - 19], grid, dim3(PP_THREADS), PP_RING_SMEM, s, p);
+      return hipGetLastError();
+    }
+    const K kfn = kfns[(variant >= 15 && variant <= 18) ? variant - 15 : dflt];
     hipLaunchKernelGGL(kfn, grid, dim3(PP_THREADS), PP_SMEM, s, p);
     return hipGetLastError();
   } else {
