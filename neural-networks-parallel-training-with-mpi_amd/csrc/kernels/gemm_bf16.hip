@@ -997,10 +997,16 @@ __global__ void __launch_bounds__(PP_THREADS) gemm_bf16_pp256_kernel(GemmParams 
 // lever docs/PERF.md §4 names for the gap to hipBLASLt.
 // ------------------------------------------------------------------------------------------
 constexpr int PP_RING = 10;
-constexpr int PP_RING_SMEM = PP_RING * PP_HALF;   // 160 KiB
+constexpr int PP_RING_SMEM = PP_RING * PP_HALF;   // 160 KiB (the R = 8 forms use 128 KiB of it)
 
-template <int LA, int LB, int EPI, int ACT, bool BIASGRAD, int GM = 4>
+// MODE 0: one half per phase, half q + D (D = R - 2) in phase q;  MODE 1: two halves in each
+// light phase (P2, P4: 4 fragment reads), q + D - 1 and q + D, none in P1 / P3 (8 reads each).
+// Either way the slot of the newest half is the slot of half q - 2 (WAR margin 2 phases) and the
+// vmcnt before phase q's barrier leaves (newest issued - (q + 1)) halves x 2 instructions.
+template <int LA, int LB, int EPI, int ACT, bool BIASGRAD, int R = 10, int MODE = 0, int GM = 4>
 __global__ void __launch_bounds__(PP_THREADS) gemm_bf16_pp256_ring_kernel(GemmParams p) {
+  static_assert(R == 8 || R == 10, "ring of 8 or 10 half images");
+  constexpr int D = R - 2;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   constexpr int BK = GEMM_BK;
   const int tid = threadIdx.x, lane = tid & 63;
@@ -1024,7 +1030,7 @@ __global__ void __launch_bounds__(PP_THREADS) gemm_bf16_pp256_ring_kernel(GemmPa
   pa1.init(w, lane, m0 + 128, p.M, p.lda);
   pb0.init(w, lane, n0, p.N, p.ldb);
   pb1.init(w, lane, n0 + 128, p.N, p.ldb);
-  auto slot = [&](int q) { return smem + ((q + 1 + PP_RING) % PP_RING) * PP_HALF; };
+  auto slot = [&](int q) { return smem + ((q + 1 + R) % R) * PP_HALF; };
   auto kof = [&](int t) { return kbeg + t * BK; };
   // issue half q of the read order (its type is q & 3; q = -1 is B0(0))
   auto issue = [&](int q) {
@@ -1046,10 +1052,10 @@ __global__ void __launch_bounds__(PP_THREADS) gemm_bf16_pp256_ring_kernel(GemmPa
   for (int i = 0; i < 8; ++i) rsum[i] = 0.f;
   const bool do_bg = BIASGRAD && tx == 0 && wn == 0;
 
-  // prologue: halves -1 .. 7 (B0(0), then K-tiles 0 and 1, then B0(2)); retire -1 and 0
+  // prologue: halves -1 .. D - 1; retire -1 and 0
 #pragma unroll
-  for (int q = -1; q < 8; ++q) issue(q);
-  wait_vm<14>();
+  for (int q = -1; q < D; ++q) issue(q);
+  wait_vm<2 * (D - 1)>();
   __builtin_amdgcn_s_barrier();
 
   bf16x8 af[4][2], b0f[2][2], b0n[2][2], b1f[2][2];
@@ -1088,12 +1094,16 @@ __global__ void __launch_bounds__(PP_THREADS) gemm_bf16_pp256_ring_kernel(GemmPa
 #pragma unroll
           for (int kk = 0; kk < 2; ++kk) b0n[jj][kk] = read_frag_async<128, LB>(cur, wn * 32 + jj * 16, kk, lane);
       }
-      // half q + 8 (same type as q: compile-time per phase) into the slot of half q - 2
-      if (ph == 0) pa0.issue(rsA, slot(q + 8), w, kof(t + 2), kend);
-      else if (ph == 1) pb1.issue(rsB, slot(q + 8), w, kof(t + 2), kend);
-      else if (ph == 2) pa1.issue(rsA, slot(q + 8), w, kof(t + 2), kend);
-      else pb0.issue(rsB, slot(q + 8), w, kof(t + 3), kend);
-      wait_vm<14>();                                 // half q + 1 has landed (this wave's part)
+      // newest half(s) (types compile-time per phase) into the slot(s) of halves q - 3, q - 2
+      if constexpr (MODE == 0) {
+        issue(q + D);
+      } else if (ph & 1) {
+        issue(q + D - 1);
+        issue(q + D);
+      }
+      // half q + 1 has landed (this wave's part): (newest - (q + 1)) halves stay in flight
+      if (MODE == 0 || (ph & 1)) wait_vm<2 * (D - 1)>();
+      else wait_vm<2 * (D - 2)>();
       __builtin_amdgcn_sched_barrier(0);
       __builtin_amdgcn_s_barrier();
       asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
@@ -1381,9 +1391,12 @@ static hipError_t launch_t(GemmParams p, int splits, hipStream_t s, int variant 
     // (the weight gradient -- XMAJ x XMAJ, 4 waves of tiles at 8192 wide -- measured 2-3 %
     // faster in row-major order: profiles/gemm_wide8192_pp256_variants.json)
     const int dflt = g_pp_order[EPI];
-    // 19 / 20: the 10-slot deep-ring twin, grouped (GM 4) / row-major tile order
-    static const K rfns[2] = {gemm_bf16_pp256_ring_kernel<LA, LB, EPI, ACT, BG, 4>,
-                              gemm_bf16_pp256_ring_kernel<LA, LB, EPI, ACT, BG, 1>};
+    // 19..22: the ring twin -- 10 slots / 8 slots, one half per phase; 10 / 8 slots, two
+    // halves in each light phase (all GM 4)
+    static const K rfns[4] = {gemm_bf16_pp256_ring_kernel<LA, LB, EPI, ACT, BG, 10, 0>,
+                              gemm_bf16_pp256_ring_kernel<LA, LB, EPI, ACT, BG, 8, 0>,
+                              gemm_bf16_pp256_ring_kernel<LA, LB, EPI, ACT, BG, 10, 1>,
+                              gemm_bf16_pp256_ring_kernel<LA, LB, EPI, ACT, BG, 8, 1>};
     static bool attr = false;
     if (!attr) {
       for (K f : kfns)
@@ -1392,8 +1405,9 @@ static hipError_t launch_t(GemmParams p, int splits, hipStream_t s, int variant 
         (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, PP_RING_SMEM);
       attr = true;
     }
-    if (variant == 19 || variant == 20) {
-      hipLaunchKernelGGL(rfns[variant - 19], grid, dim3(PP_THREADS), PP_RING_SMEM, s, p);
+    if (variant >= 19 && variant <= 22) {
+      const int smem = (variant & 1) ? PP_RING_SMEM : PP_SMEM;   // 19, 21: 10 slots
+      hipLaunchKernelGGL(rfns[variant - 19], grid, dim3(PP_THREADS), smem, s, p);
       return hipGetLastError();
     }
     const K kfn = kfns[(variant >= 15 && variant <= 18) ? variant - 15 : dflt];
