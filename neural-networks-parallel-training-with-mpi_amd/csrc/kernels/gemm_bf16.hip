@@ -1005,7 +1005,7 @@ constexpr int PP_RING_SMEM = PP_RING * PP_HALF;   // 160 KiB (the R = 8 forms us
 // vmcnt before phase q's barrier leaves (newest issued - (q + 1)) halves x 2 instructions.
 template <int LA, int LB, int EPI, int ACT, bool BIASGRAD, int R = 10, int MODE = 0, int GM = 4>
 __global__ void __launch_bounds__(PP_THREADS) gemm_bf16_pp256_ring_kernel(GemmParams p) {
-  static_assert(R == 8 || R == 10, "ring of 8 or 10 half images");
+  static_assert(R == 6 || R == 8 || R == 10, "ring of 6, 8 or 10 half images");
   constexpr int D = R - 2;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   constexpr int BK = GEMM_BK;
@@ -1391,12 +1391,14 @@ static hipError_t launch_t(GemmParams p, int splits, hipStream_t s, int variant 
     // (the weight gradient -- XMAJ x XMAJ, 4 waves of tiles at 8192 wide -- measured 2-3 %
     // faster in row-major order: profiles/gemm_wide8192_pp256_variants.json)
     const int dflt = g_pp_order[EPI];
-    // 19..22: the ring twin -- 10 slots / 8 slots, one half per phase; 10 / 8 slots, two
-    // halves in each light phase (all GM 4)
-    static const K rfns[4] = {gemm_bf16_pp256_ring_kernel<LA, LB, EPI, ACT, BG, 10, 0>,
+    // 19..24: the ring twin -- 10 slots / 8 slots, one half per phase; 10 / 8 slots, two
+    // halves in each light phase; 6 slots, one / two (all GM 4)
+    static const K rfns[6] = {gemm_bf16_pp256_ring_kernel<LA, LB, EPI, ACT, BG, 10, 0>,
                               gemm_bf16_pp256_ring_kernel<LA, LB, EPI, ACT, BG, 8, 0>,
                               gemm_bf16_pp256_ring_kernel<LA, LB, EPI, ACT, BG, 10, 1>,
-                              gemm_bf16_pp256_ring_kernel<LA, LB, EPI, ACT, BG, 8, 1>};
+                              gemm_bf16_pp256_ring_kernel<LA, LB, EPI, ACT, BG, 8, 1>,
+                              gemm_bf16_pp256_ring_kernel<LA, LB, EPI, ACT, BG, 6, 0>,
+                              gemm_bf16_pp256_ring_kernel<LA, LB, EPI, ACT, BG, 6, 1>};
     static bool attr = false;
     if (!attr) {
       for (K f : kfns)
@@ -1405,8 +1407,8 @@ static hipError_t launch_t(GemmParams p, int splits, hipStream_t s, int variant 
         (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, PP_RING_SMEM);
       attr = true;
     }
-    if (variant >= 19 && variant <= 22) {
-      const int smem = (variant & 1) ? PP_RING_SMEM : PP_SMEM;   // 19, 21: 10 slots
+    if (variant >= 19 && variant <= 24) {
+      const int smem = variant >= 23 ? 6 * PP_HALF : (variant & 1) ? PP_RING_SMEM : PP_SMEM;
       hipLaunchKernelGGL(rfns[variant - 19], grid, dim3(PP_THREADS), smem, s, p);
       return hipGetLastError();
     }
