@@ -98,6 +98,32 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
                             M, N, K, P<float>(ws), S(s), fu ? &f : nullptr), "linear_wgrad_bf16");
   }, py::arg("dZ"), py::arg("lddz"), py::arg("X"), py::arg("ldx"), py::arg("dW"), py::arg("db"),
      py::arg("M"), py::arg("N"), py::arg("K"), py::arg("ws"), py::arg("s"), py::arg("sgd") = py::none());
+  m.def("wide_pair_wgrad_ok", &wide_pair_wgrad_ok);
+  m.def("wide_pair_dgrad_ok", &wide_pair_dgrad_ok);
+  m.def("set_wide_pair", &set_wide_pair);
+  m.def("wide_pair_wgrad_dgrad_bf16", [](uptr dZ, int lddz, uptr X, int ldx, uptr dW, uptr db, int M,
+                                         int N, int K, py::object sgd, uptr dZ2, int lddz2, uptr W2,
+                                         int ldw2, uptr Ap2, int ldap2, uptr dX2, int lddx2, int M2,
+                                         int N2, int K2, int act2, uptr s) {
+    WgradArgs w{P<const bf16>(dZ), lddz, P<const bf16>(X), ldx, P<float>(dW), P<float>(db), M, N, K,
+                nullptr, SgdFuse{}};
+    to_sgd(sgd, w.sg);
+    DgradArgs d{P<const bf16>(dZ2), lddz2, P<const bf16>(W2), ldw2, P<const bf16>(Ap2), ldap2,
+                P<bf16>(dX2), lddx2, M2, N2, K2, act2};
+    check(wide_pair(w, &d, nullptr, S(s)), "wide_pair_wgrad_dgrad_bf16");
+  });
+  m.def("wide_pair_wgrad_wgrad_bf16", [](uptr dZ, int lddz, uptr X, int ldx, uptr dW, uptr db, int M,
+                                         int N, int K, py::object sgd, uptr dZ2, int lddz2, uptr X2,
+                                         int ldx2, uptr dW2, uptr db2, int M2, int N2, int K2,
+                                         py::object sgd2, uptr s) {
+    WgradArgs w{P<const bf16>(dZ), lddz, P<const bf16>(X), ldx, P<float>(dW), P<float>(db), M, N, K,
+                nullptr, SgdFuse{}};
+    to_sgd(sgd, w.sg);
+    WgradArgs w2{P<const bf16>(dZ2), lddz2, P<const bf16>(X2), ldx2, P<float>(dW2), P<float>(db2), M2,
+                 N2, K2, nullptr, SgdFuse{}};
+    to_sgd(sgd2, w2.sg);
+    check(wide_pair(w, nullptr, &w2, S(s)), "wide_pair_wgrad_wgrad_bf16");
+  });
   m.def("linear_wgrad_bf16_out16", [](uptr dZ, int lddz, uptr X, int ldx, uptr dW16, uptr db16,
                                       int M, int N, int K, uptr s) {
     check(linear_wgrad_bf16_ex(P<const bf16>(dZ), lddz, P<const bf16>(X), ldx, nullptr, nullptr,

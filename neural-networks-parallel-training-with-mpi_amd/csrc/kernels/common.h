@@ -109,6 +109,39 @@ __device__ __forceinline__ void sgd_fused_store(const SgdFuse& f, const float* g
   if (f.s_base) f.s_base[off] = (bf16)pn;
 }
 
+// sgd_fused_store4 in two halves, so a caller can issue the master / momentum / hyper-parameter
+// loads BEFORE the loads that produce the gradient (a split-K combine: the slab sums), keeping
+// them off the dependent chain.  Same arithmetic: bitwise identical.
+struct SgdPre4 {
+  f32x4 p, b;
+  long long off;
+  float lr, mom, damp, wd, gs;
+};
+__device__ __forceinline__ SgdPre4 sgd_pre4(const SgdFuse& f, const float* gaddr) {
+  SgdPre4 q;
+  q.off = gaddr - f.g_base;
+  q.p = *reinterpret_cast<const f32x4*>(f.p_base + q.off);
+  q.b = *reinterpret_cast<const f32x4*>(f.m_base + q.off);
+  q.lr = f.hp[0]; q.mom = f.hp[1]; q.damp = f.hp[2]; q.wd = f.hp[3]; q.gs = f.hp[4];
+  return q;
+}
+__device__ __forceinline__ void sgd_apply4(const SgdFuse& f, SgdPre4 q, f32x4 g) {
+#pragma unroll
+  for (int r = 0; r < 4; ++r) {
+    float bb = q.b[r];
+    q.p[r] = sgd_elem(q.p[r], g[r], bb, q.lr, q.mom, q.damp, q.wd, q.gs, f.nesterov != 0, f.first != 0);
+    q.b[r] = bb;
+  }
+  *reinterpret_cast<f32x4*>(f.p_base + q.off) = q.p;
+  if (q.mom != 0.f) *reinterpret_cast<f32x4*>(f.m_base + q.off) = q.b;
+  if (f.s_base) {
+    bf16x4 sv;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) sv[r] = (bf16)q.p[r];
+    *reinterpret_cast<bf16x4*>(f.s_base + q.off) = sv;
+  }
+}
+
 __device__ __forceinline__ void sgd_fused_store4(const SgdFuse& f, const float* gaddr, f32x4 g) {
   const long long off = gaddr - f.g_base;
   f32x4 p = *reinterpret_cast<const f32x4*>(f.p_base + off);

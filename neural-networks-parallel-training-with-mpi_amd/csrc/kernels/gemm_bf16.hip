@@ -54,7 +54,16 @@ struct GemmParams {
   int store_pol;              // epilogue output stores: 0 plain, 1 nt, 2 sc1 (write-through)
   bf16* c16;                  // EPI_F32 without split-K: store the gradient as bf16 here instead
   bf16* bg16;                 // (same ldc as C) and the bias gradient here -- the bf16 payload
+  int sgd_serial;             // 1: the per-fragment SGD epilogue (A/B of sgd_epilogue_batched)
 };
+static int g_sgd_serial = -1;   // NNMPI_SGD_SERIAL=1: per-fragment SGD epilogue (experiments)
+static int sgd_serial() {
+  if (g_sgd_serial < 0) {
+    const char* e = std::getenv("NNMPI_SGD_SERIAL");
+    g_sgd_serial = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_sgd_serial;
+}
 
 // Epilogue output store of 16 bytes with a selectable cache policy (experiments: what the
 // kernel leaves dirty in L2 is written back at the launch boundary, MI355X_MICROARCH.md
@@ -193,6 +202,62 @@ __device__ __forceinline__ bf16x8 read_frag_async(const char* lds, int xb, int k
   }
 }
 
+// SGD-momentum update of an accumulator tile in the epilogue (un-split weight gradient, single
+// rank), batched: the master and momentum vectors of RB fragment rows (RB x NJ fragments) are
+// loaded together BEFORE any of their results is stored, so a tile pays MI/RB memory round trips
+// instead of MI x NJ (sgd_fused_store4 per fragment: the compiler cannot hoist the next
+// fragment's loads above this one's stores -- the arena pointers may alias).  The
+// hyper-parameters are read once.  Same arithmetic as sgd_fused_store4: bitwise identical.
+template <int MI, int NJ, int RB = 1>
+__device__ __forceinline__ void sgd_epilogue_batched(const SgdFuse& f, const f32x4 (&acc)[MI][NJ],
+                                                     const int (&mrow)[MI], const int (&ncol)[NJ],
+                                                     const float* cbase, int ldc, int M, int N) {
+  const float lr = f.hp[0], mom = f.hp[1], damp = f.hp[2], wd = f.hp[3], gs = f.hp[4];
+  const bool nest = f.nesterov != 0, first = f.first != 0;
+  const long long base = cbase - f.g_base;
+  auto offset = [&](int i, int j) {
+    // clamped (always in range) so every load issues unconditionally; out-of-range fragments
+    // are skipped at the store
+    return base + (long long)min(mrow[i], M - 1) * ldc + min(ncol[j], N - 4);
+  };
+#pragma unroll
+  for (int i0 = 0; i0 < MI; i0 += RB) {
+    f32x4 pv[RB][NJ], bv[RB][NJ];
+#pragma unroll
+    for (int ii = 0; ii < RB; ++ii)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        const long long o = offset(i0 + ii, j);
+        pv[ii][j] = *reinterpret_cast<const f32x4*>(f.p_base + o);
+        bv[ii][j] = *reinterpret_cast<const f32x4*>(f.m_base + o);
+      }
+#pragma unroll
+    for (int ii = 0; ii < RB; ++ii) {
+      if (mrow[i0 + ii] >= M) continue;
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        if (ncol[j] >= N) continue;
+        const long long o = offset(i0 + ii, j);
+        f32x4 p = pv[ii][j], b = bv[ii][j];
+#pragma unroll
+        for (int r = 0; r < 4; ++r) {
+          float bb = b[r];
+          p[r] = sgd_elem(p[r], acc[i0 + ii][j][r], bb, lr, mom, damp, wd, gs, nest, first);
+          b[r] = bb;
+        }
+        *reinterpret_cast<f32x4*>(f.p_base + o) = p;
+        if (mom != 0.f) *reinterpret_cast<f32x4*>(f.m_base + o) = b;
+        if (f.s_base) {
+          bf16x4 sv;
+#pragma unroll
+          for (int r = 0; r < 4; ++r) sv[r] = (bf16)p[r];
+          *reinterpret_cast<bf16x4*>(f.s_base + o) = sv;
+        }
+      }
+    }
+  }
+}
+
 // Epilogue shared by both main loops: lane holds C[m][n..n+3] for each (i, j) fragment.
 // All epilogue operands (bias, activation aux) are loaded up front, then every fragment is
 // finished and stored: no load waits behind the stores (stores count in vmcnt on gfx950).
@@ -261,22 +326,31 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& p, f32x4 (&acc)
     // a final (un-split) weight gradient on a single rank: the optimizer update is applied
     // here, in the epilogue -- no gradient store and no separate optimizer pass over it
     const bool fuse = p.sg.g_base != nullptr;
+    bool batched = false;
+    {
+      if (fuse && !p.c16 && !p.sgd_serial) {
+        sgd_epilogue_batched<MI, NJ>(p.sg, acc, mrow, ncol, cbase, p.ldc, p.M, p.N);
+        batched = true;
+      }
+    }
+    if (!batched) {
 #pragma unroll
-    for (int i = 0; i < MI; ++i) {
-      if (mrow[i] >= p.M) continue;
+      for (int i = 0; i < MI; ++i) {
+        if (mrow[i] >= p.M) continue;
 #pragma unroll
-      for (int j = 0; j < NJ; ++j) {
-        if (ncol[j] >= p.N) continue;
-        if (p.c16) {   // the bf16 all-reduce payload, rounded as cast_f32_bf16 rounds
-          bf16x4 o;
+        for (int j = 0; j < NJ; ++j) {
+          if (ncol[j] >= p.N) continue;
+          if (p.c16) {   // the bf16 all-reduce payload, rounded as cast_f32_bf16 rounds
+            bf16x4 o;
 #pragma unroll
-          for (int r = 0; r < 4; ++r) o[r] = (bf16)acc[i][j][r];
-          *reinterpret_cast<bf16x4*>(p.c16 + (long long)mrow[i] * p.ldc + ncol[j]) = o;
-          continue;
+            for (int r = 0; r < 4; ++r) o[r] = (bf16)acc[i][j][r];
+            *reinterpret_cast<bf16x4*>(p.c16 + (long long)mrow[i] * p.ldc + ncol[j]) = o;
+            continue;
+          }
+          float* g = cbase + (long long)mrow[i] * p.ldc + ncol[j];
+          if (fuse) sgd_fused_store4(p.sg, g, acc[i][j]);
+          else *reinterpret_cast<f32x4*>(g) = acc[i][j];
         }
-        float* g = cbase + (long long)mrow[i] * p.ldc + ncol[j];
-        if (fuse) sgd_fused_store4(p.sg, g, acc[i][j]);
-        else *reinterpret_cast<f32x4*>(g) = acc[i][j];
       }
     }
   }
@@ -819,18 +893,17 @@ constexpr int PP_THREADS = 512;
 // barrier later stays inside it.
 // GM: grouped tile order (grouped_tile) -- 32 blocks resident per XCD read 4 A + 8 B panels per
 // K-tile instead of 1 A + 32 B at the 8192-wide shape.
+// One 256x256 output tile: `bid` is the tile's XCD-remapped id in a gx x gy grid (the standalone
+// launch below, or one job of gemm_bf16_pp256_pair_kernel).
 template <int LA, int LB, int EPI, int ACT, bool BIASGRAD, bool LATE_LGKM = true, int GM = 4>
-__global__ void __launch_bounds__(PP_THREADS) gemm_bf16_pp256_kernel(GemmParams p) {
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
+__device__ __forceinline__ void pp256_tile(const GemmParams& p, char* smem, int bid, int gx, int gy,
+                                           int split) {
   constexpr int BK = GEMM_BK;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int wm = w >> 2, wn = w & 3;
-  const int gx = gridDim.x, gy = gridDim.y;
-  const int bid = xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy);
   int tx, ty;
   grouped_tile(bid, gx, gy, GM, tx, ty);
-  const int split = blockIdx.z;
   const int m0 = ty * 256, n0 = tx * 256;
   const int kbeg = split * p.k_per_split;
   const int kend = min(p.K, kbeg + p.k_per_split);
@@ -981,6 +1054,43 @@ __global__ void __launch_bounds__(PP_THREADS) gemm_bf16_pp256_kernel(GemmParams 
 #pragma unroll
   for (int j = 0; j < 4; ++j) ncol[j] = n0 + (j >> 1) * 128 + wn * 32 + (j & 1) * 16 + (lane >> 4) * 4;
   epilogue_store<8, 4, EPI, ACT, BIASGRAD>(p, acc, accb, do_bg, mrow, ncol, lane, split);
+}
+
+template <int LA, int LB, int EPI, int ACT, bool BIASGRAD, bool LATE_LGKM = true, int GM = 4>
+__global__ void __launch_bounds__(PP_THREADS) gemm_bf16_pp256_kernel(GemmParams p) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int gx = gridDim.x, gy = gridDim.y;
+  pp256_tile<LA, LB, EPI, ACT, BIASGRAD, LATE_LGKM, GM>(
+      p, smem, xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy), gx, gy, blockIdx.z);
+}
+
+// Two independent 256x256 GEMMs in ONE launch (the wide model's backward: the weight gradient of
+// layer i with its SGD epilogue beside the dgrad of layer i-1).  A weight-gradient tile ends in a
+// memory-bound SGD epilogue (~18 B per parameter: master, momentum, bf16 shadow), a dgrad tile is
+// compute-bound with a light epilogue; as separate launches every CU runs its SGD epilogues at
+// the same time and HBM idles during the main loops.  Here the two jobs' blocks are interleaved
+// in groups of 8 (one per XCD), so while some CUs stream an SGD epilogue others run MFMA main
+// loops, and the launch boundary between them is gone.  Each job keeps its own tile order: job
+// block j of n lands on XCD j % 8 exactly as in its own launch (n1, n2 multiples of 8), so
+// xcd_remap / grouped_tile see the same ids.  Bitwise identical to the two launches.
+template <int LA1, int LB1, int EPI1, int ACT1, bool BG1, int GM1,
+          int LA2, int LB2, int EPI2, int ACT2, bool BG2, int GM2>
+__global__ void __launch_bounds__(PP_THREADS) gemm_bf16_pp256_pair_kernel(GemmParams p1, GemmParams p2,
+                                                                          int gx1, int gy1, int gx2,
+                                                                          int gy2) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int n1 = gx1 * gy1, n2 = gx2 * gy2, m = min(n1, n2);
+  const int b = blockIdx.x;
+  int job, j;
+  if (b < 2 * m) {
+    job = (b >> 3) & 1;
+    j = ((b >> 4) << 3) | (b & 7);
+  } else {
+    job = n1 > n2 ? 0 : 1;
+    j = m + (b - 2 * m);
+  }
+  if (job == 0) pp256_tile<LA1, LB1, EPI1, ACT1, BG1, true, GM1>(p1, smem, xcd_remap(j, n1), gx1, gy1, 0);
+  else pp256_tile<LA2, LB2, EPI2, ACT2, BG2, true, GM2>(p2, smem, xcd_remap(j, n2), gx2, gy2, 0);
 }
 
 // ------------------------------------------------------------------------------------------
@@ -1191,6 +1301,11 @@ __device__ __forceinline__ void slab_reduce_block(const SlabReduce& r, int b, in
       n = (v % nv) * 4;
     }
     const float* p = r.ws + m * N + n;
+    float* o = r.out + m * r.ldo + n;
+    // the combiner's optimizer operands are loaded first, beside the slab loads
+    const bool upd = combiner && v < nvec && r.sg.g_base && !r.sgd_serial;
+    SgdPre4 pre{};
+    if (upd) pre = sgd_pre4(r.sg, o);
 #pragma unroll
     for (int j = 0; j < SS::VPW; ++j) {
       const int vw = w0 + j * SLAB_NW;
@@ -1206,8 +1321,8 @@ __device__ __forceinline__ void slab_reduce_block(const SlabReduce& r, int b, in
       f32x4 t = part[cg * WS * 64 + lane];
 #pragma unroll
       for (int k = 1; k < WS; ++k) t += part[(cg * WS + k) * 64 + lane];
-      float* o = r.out + m * r.ldo + n;
-      if (r.sg.g_base) sgd_fused_store4(r.sg, o, t);
+      if (upd) sgd_apply4(r.sg, pre, t);
+      else if (r.sg.g_base) sgd_fused_store4(r.sg, o, t);
       else *reinterpret_cast<f32x4*>(o) = t;
     }
     return;
@@ -1536,6 +1651,7 @@ static int make_wgrad(const WgradArgs& a, GemmParams& p, SlabReduce& pending) {
   const int splits = wgrad_splits(M, N, K);
   const int ksteps = (K + GEMM_BK - 1) / GEMM_BK;
   p = GemmParams{};
+  p.sgd_serial = sgd_serial();
   p.A = a.dZ; p.lda = a.lddz; p.B = a.X; p.ldb = a.ldx; p.M = M; p.N = N; p.K = K;
   p.k_per_split = ((ksteps + splits - 1) / splits) * GEMM_BK;
   pending = SlabReduce{};
@@ -1648,7 +1764,9 @@ static void slab_blocks(const SlabReduce& r, int& nb_main, int& nb_bias, int& nb
   nb = nb_main + nb_bias + (r.loss_out ? 1 : 0);
 }
 
-hipError_t slab_reduce(const SlabReduce& r, hipStream_t s) {
+hipError_t slab_reduce(const SlabReduce& r0, hipStream_t s) {
+  SlabReduce r = r0;
+  r.sgd_serial = sgd_serial();
   int nb_main, nb_bias, nb;
   slab_blocks(r, nb_main, nb_bias, nb);
   if (nb == 0) return hipSuccess;
@@ -1743,6 +1861,7 @@ hipError_t bwd_group(const DgradArgs* dg, const WgradArgs* wg, const SlabReduce*
   }
   if (red) {
     g.red = *red;
+    g.red.sgd_serial = sgd_serial();
     g.red_ws = slab_ws(*red);
     g.nb_main = nb_main;
     g.nb_bias = nb_bias;
@@ -1772,6 +1891,84 @@ hipError_t bwd_group(const DgradArgs* dg, const WgradArgs* wg, const SlabReduce*
     return slab_reduce(pend, s);
   }
   return hipGetLastError();
+}
+
+// ---- wide backward pairs (gemm_bf16_pp256_pair_kernel) ------------------------------------
+// Off by default: measured on the 8192-wide step (3 interleaved rounds, one box) 5.575 ms
+// paired vs 5.540 separate -- the SGD epilogue is bound per CU (latency), not by HBM, so
+// spreading it beside other CUs' main loops buys nothing, and the interleaved tile orders cost
+// L2 locality (profiles/r2s2_wide_sgd_epilogue_pair_ab.txt).
+static int g_pair = -1;   // 1 on, 0 off (default; NNMPI_PAIR=1 / set_wide_pair)
+void set_wide_pair(int on) { g_pair = on; }
+static bool pair_enabled() {
+  if (g_pair < 0) {
+    const char* e = std::getenv("NNMPI_PAIR");
+    g_pair = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_pair == 1 && gemm_impl() == 2 && g_force_tile == 0 && g_variant == 0;
+}
+static bool tiles256_x8(int M, int N) {
+  const long long t = (long long)((M + 255) / 256) * ((N + 255) / 256);
+  return t >= 256 && t % 8 == 0;
+}
+bool wide_pair_wgrad_ok(int rows, int out_f, int in_f) {
+  return pair_enabled() && wgrad_tile(out_f, in_f) == 256 && tiles256_x8(out_f, in_f) &&
+         wgrad_splits(out_f, in_f, rows) == 1;
+}
+bool wide_pair_dgrad_ok(int rows, int out_f, int in_f) {
+  // dgrad output: rows x in_f
+  return pair_enabled() && pick_tile(rows, in_f) == 256 && tiles256_x8(rows, in_f);
+}
+
+template <typename F>
+static void pp_attr_once(F f) {
+  static bool done = false;
+  if (!done) {
+    (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, PP_SMEM);
+    done = true;
+  }
+}
+
+hipError_t wide_pair(const WgradArgs& w1, const DgradArgs* dg, const WgradArgs* w2, hipStream_t s) {
+  if ((dg == nullptr) == (w2 == nullptr)) return hipErrorInvalidValue;
+  if (!wide_pair_wgrad_ok(w1.K, w1.M, w1.N) || !w1.db) return hipErrorInvalidValue;
+  GemmParams p1, p2;
+  SlabReduce r1, r2;
+  make_wgrad(w1, p1, r1);
+  set_extents<XMAJ, XMAJ>(p1);
+  const int gx1 = (w1.N + 255) / 256, gy1 = (w1.M + 255) / 256;
+  int gx2, gy2;
+  if (w2) {
+    if (!wide_pair_wgrad_ok(w2->K, w2->M, w2->N) || !w2->db) return hipErrorInvalidValue;
+    make_wgrad(*w2, p2, r2);
+    set_extents<XMAJ, XMAJ>(p2);
+    gx2 = (w2->N + 255) / 256; gy2 = (w2->M + 255) / 256;
+  } else {
+    // dZ[M rows][K out] x W[K out][N in] -> dX[M][N], times act'(Aprev)
+    if (!wide_pair_dgrad_ok(dg->M, dg->K, dg->N)) return hipErrorInvalidValue;
+    p2 = GemmParams{};
+    p2.A = dg->dZ; p2.lda = dg->lddz; p2.B = dg->W; p2.ldb = dg->ldw;
+    p2.M = dg->M; p2.N = dg->N; p2.K = dg->K;
+    p2.k_per_split = ((dg->K + GEMM_BK - 1) / GEMM_BK) * GEMM_BK;
+    p2.C = dg->dX; p2.ldc = dg->lddx; p2.aux = dg->Aprev; p2.ldaux = dg->lda_prev;
+    set_extents<KMAJ, XMAJ>(p2);
+    gx2 = (dg->N + 255) / 256; gy2 = (dg->M + 255) / 256;
+  }
+  const dim3 grid(gx1 * gy1 + gx2 * gy2), blk(PP_THREADS);
+#define NNMPI_PAIR_LAUNCH(...)                                                                     \
+  {                                                                                                \
+    auto kfn = gemm_bf16_pp256_pair_kernel<XMAJ, XMAJ, EPI_F32, ACT_NONE, true, 1, __VA_ARGS__>;   \
+    pp_attr_once(kfn);                                                                             \
+    hipLaunchKernelGGL(kfn, grid, blk, PP_SMEM, s, p1, p2, gx1, gy1, gx2, gy2);                   \
+    return hipGetLastError();                                                                      \
+  }
+  if (w2) NNMPI_PAIR_LAUNCH(XMAJ, XMAJ, EPI_F32, ACT_NONE, true, 1)
+  switch (dg->act) {
+    case ACT_RELU: NNMPI_PAIR_LAUNCH(KMAJ, XMAJ, EPI_DACT, ACT_RELU, false, 4)
+    case ACT_TANH: NNMPI_PAIR_LAUNCH(KMAJ, XMAJ, EPI_DACT, ACT_TANH, false, 4)
+    default: NNMPI_PAIR_LAUNCH(KMAJ, XMAJ, EPI_DACT, ACT_NONE, false, 4)
+  }
+#undef NNMPI_PAIR_LAUNCH
 }
 
 }  // namespace nnmpi

@@ -39,6 +39,7 @@ struct SlabReduce {
   float loss_scale;
   float* loss_out;
   SgdFuse sg;               // sg.g_base != null: apply the optimizer update instead of storing
+  int sgd_serial = 0;       // 1: optimizer operands loaded after the sums (A/B, NNMPI_SGD_SERIAL)
 };
 
 enum Epi : int { EPI_BIAS_ACT = 0, EPI_DACT = 1, EPI_F32 = 2 };
@@ -111,6 +112,15 @@ void set_bwd_group(int on);   // 1 = grouped kernel (default), 0 = separate laun
 bool bwd_group_supported(int rows, int out_f, int in_f);   // this layer shape runs grouped
 hipError_t bwd_group(const DgradArgs* dg, const WgradArgs* wg, const SlabReduce* red,
                      SlabReduce* wg_pending, hipStream_t s);
+// Wide-model backward pair: the un-split 256x256 weight gradient w1 (with its SGD epilogue when
+// w1.sg.g_base is set) and EITHER the dgrad dg OR a second weight gradient w2, in ONE launch
+// whose blocks interleave the two jobs (memory-bound SGD epilogues beside compute-bound main
+// loops).  Bitwise identical to the separate launches.  hipErrorInvalidValue when a job is not
+// eligible (the *_ok predicates): the caller launches them separately then.
+bool wide_pair_wgrad_ok(int rows, int out_f, int in_f);
+bool wide_pair_dgrad_ok(int rows, int out_f, int in_f);
+hipError_t wide_pair(const WgradArgs& w1, const DgradArgs* dg, const WgradArgs* w2, hipStream_t s);
+void set_wide_pair(int on);
 
 // ---- fp32 GEMM (gemm_f32.hip) ----
 hipError_t linear_fwd_f32(const float* X, int ldx, const float* W, int ldw, const float* bias,

@@ -400,21 +400,56 @@ class MLPEngine:
             self._head(h, dz)
             unfused.append(last)
         self._mark("head")
-        for i in range(L - 2, -1, -1):
-            x_in = self.acts[i - 1][:rows] if i > 0 else x
-            dz_i = dz
-            if i > 0:
-                dz_next = self._dzl(i - 1, rows)
-                ops.linear_dgrad(dz_i, ar.compute_weight(i), self.acts[i - 1][:rows], self.act, dz_next)
-                dz = dz_next
+        # Wide layers (256x256-tile, un-split weight gradients): wgrad_i + its SGD epilogue runs
+        # in ONE launch with dgrad_{i-1} (or, last, with wgrad_0) -- ops.wide_pair -- so the
+        # memory-bound SGD epilogues overlap compute-bound main loops.  `pend` is the weight
+        # gradient waiting for its partner; every hazard is as in the sequential order: W_i's
+        # last reader dgrad_i ran in an earlier launch, dgrad_{i-1} reads only W_{i-1}.
+        pairs = hasattr(ops, "wide_pair")
+        pend = None
+
+        def wg_of(i, dz_i, x_in):
+            return (dz_i, x_in, ar.grad_weight(i), ar.grad_bias(i))
+
+        def pair_wg_ok(i, dz_i):
             out_f, in_f = self.spec.layer_shape(i)
-            # dgrad_i was issued above: nothing reads W_i any more, so even an un-split wgrad
+            return pairs and ops.wide_pair_wgrad_ok(dz_i.shape[0], out_f, in_f)
+
+        def issue_wgrad(i, dz_i, x_in):
+            out_f, in_f = self.spec.layer_shape(i)
+            # dgrad_i was issued before: nothing reads W_i any more, so even an un-split wgrad
             # may update it in its epilogue
             if ops.wgrad_can_fuse_sgd(rows, out_f, in_f, self.dtype, epilogue=True):
                 ops.linear_wgrad(dz_i, x_in, ar.grad_weight(i), ar.grad_bias(i), ws=self.ws, sgd=fz)
             else:
                 ops.linear_wgrad(dz_i, x_in, ar.grad_weight(i), ar.grad_bias(i), ws=self.ws)
                 unfused.append(i)
+
+        for i in range(L - 2, -1, -1):
+            x_in = self.acts[i - 1][:rows] if i > 0 else x
+            dz_i = dz
+            if i > 0:
+                dz_next = self._dzl(i - 1, rows)
+                dg = (dz_i, ar.compute_weight(i), self.acts[i - 1][:rows], self.act, dz_next)
+                out_f, in_f = self.spec.layer_shape(i)
+                if pend is not None and pair_wg_ok(pend[0], pend[1]) and \
+                        ops.wide_pair_dgrad_ok(rows, out_f, in_f):
+                    ops.wide_pair(wg_of(*pend), fz, dgrad=dg)
+                else:
+                    if pend is not None:
+                        issue_wgrad(*pend)
+                    ops.linear_dgrad(*dg)
+                pend = None
+                dz = dz_next
+            if pend is not None:            # i == 0: the last two weight gradients
+                if pair_wg_ok(pend[0], pend[1]) and pair_wg_ok(i, dz_i):
+                    ops.wide_pair(wg_of(*pend), fz, wgrad2=wg_of(i, dz_i, x_in), sgd2=fz)
+                    pend = None
+                    continue
+                issue_wgrad(*pend)
+            pend = (i, dz_i, x_in)
+        if pend is not None:
+            issue_wgrad(*pend)
         self._mark("bwd")
         for i in unfused:
             s, e = ar.layer_range[i]

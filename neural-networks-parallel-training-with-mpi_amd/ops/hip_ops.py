@@ -204,6 +204,43 @@ class HipOps:
     def bwd_group_supported(self, rows, out_f, in_f) -> bool:
         return bool(self.lib.bwd_group_supported(rows, out_f, in_f))
 
+    # ---- wide-model backward pairs (one launch: weight gradient + SGD beside a dgrad) -------
+    def wide_pair_wgrad_ok(self, rows, out_f, in_f) -> bool:
+        return bool(self.lib.wide_pair_wgrad_ok(rows, out_f, in_f))
+
+    def wide_pair_dgrad_ok(self, rows, out_f, in_f) -> bool:
+        return bool(self.lib.wide_pair_dgrad_ok(rows, out_f, in_f))
+
+    def wide_pair(self, wgrad, sgd, dgrad=None, wgrad2=None, sgd2=None):
+        """``wgrad = (dz, x, gW, gb)`` (un-split, SGD epilogue ``sgd``) in one launch with EITHER
+        ``dgrad = (dz, W, a_prev, act, out)`` OR ``wgrad2`` (same form as wgrad, ``sgd2``)."""
+        dz, x, gW, gb = wgrad
+        rows, M = dz.shape
+        N = x.shape[1]
+        _check(dz.dtype == torch.bfloat16 and gb is not None and
+               self.wide_pair_wgrad_ok(rows, M, N), "wide pair: weight gradient not eligible")
+        _check(tuple(gW.shape) == (M, N) and gW.stride(0) == N, "wide pair: dense dW")
+        w = (_p(dz), dz.stride(0), _p(x), x.stride(0), _p(gW), _p(gb), M, N, rows, sgd)
+        if dgrad is not None:
+            dz2, W, a_prev, act, out = dgrad
+            r2, K2 = dz2.shape
+            N2 = W.shape[1]
+            _check(self.wide_pair_dgrad_ok(r2, K2, N2) and tuple(out.shape) == (r2, N2),
+                   "wide pair: dgrad not eligible")
+            self.lib.wide_pair_wgrad_dgrad_bf16(*w, _p(dz2), dz2.stride(0), _p(W), W.stride(0),
+                                                _p(a_prev), a_prev.stride(0), _p(out),
+                                                out.stride(0), r2, N2, K2, ACT_CODES[act],
+                                                self.stream)
+            return
+        dz2, x2, gW2, gb2 = wgrad2
+        r2, M2 = dz2.shape
+        N2 = x2.shape[1]
+        _check(gb2 is not None and self.wide_pair_wgrad_ok(r2, M2, N2) and
+               tuple(gW2.shape) == (M2, N2) and gW2.stride(0) == N2,
+               "wide pair: second weight gradient not eligible")
+        self.lib.wide_pair_wgrad_wgrad_bf16(*w, _p(dz2), dz2.stride(0), _p(x2), x2.stride(0),
+                                            _p(gW2), _p(gb2), M2, N2, r2, sgd2, self.stream)
+
     def bwd_group(self, dgrad, wgrad, sgd, pending):
         """One grouped launch: dgrad of layer i (``(dz, W, a_prev, act, out)`` or None), wgrad of
         layer i (``(dz, x, gW, gb, ws)`` or None, optional optimizer fusion ``sgd``) and the

@@ -426,6 +426,27 @@ def _wide_cfg(**kw):
     return TrainConfig(**base)
 
 
+@pytest.mark.parametrize("width,rows", [(4096, 4096), (8192, 512)])
+def test_wide_pair_launches_bitwise_equal(width, rows):
+    """Single rank, 256x256-tile layers: wgrad_i + SGD epilogue beside dgrad_{i-1} (and the last
+    two weight gradients together) in one interleaved launch each == the separate launches.
+    4096 rows: both pair kinds; 512 rows: the dgrads are too small to pair (fallback) and only
+    the last two weight gradients share a launch."""
+    from nnmpi_amd import native
+    lib = native.lib()
+    cfg = _wide_cfg(widths=[width] * 4 + [1], n_features=width, n_samples=rows)
+    try:
+        lib.set_wide_pair(1)
+        a = trainer.run_worker(cfg)
+        lib.set_wide_pair(0)
+        b = trainer.run_worker(cfg)
+    finally:
+        lib.set_wide_pair(-1)
+    assert a.losses == b.losses
+    assert torch.equal(a.final_params, b.final_params)
+    assert a.losses[-1] == a.losses[-1]
+
+
 def test_wide_chunked_buckets_overlap_bitwise_equal():
     """8192-wide layers cut into 4 output-row chunk buckets: each chunk's weight gradient is
     its own launch, its all-reduce starts behind it on the comm stream, its SGD runs on the
