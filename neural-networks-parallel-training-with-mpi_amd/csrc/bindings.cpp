@@ -101,6 +101,7 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
   m.def("wide_pair_wgrad_ok", &wide_pair_wgrad_ok);
   m.def("wide_pair_dgrad_ok", &wide_pair_dgrad_ok);
   m.def("set_wide_pair", &set_wide_pair);
+  m.def("set_sgd_epilogue", &set_sgd_epilogue);
   m.def("wide_pair_wgrad_dgrad_bf16", [](uptr dZ, int lddz, uptr X, int ldx, uptr dW, uptr db, int M,
                                          int N, int K, py::object sgd, uptr dZ2, int lddz2, uptr W2,
                                          int ldw2, uptr Ap2, int ldap2, uptr dX2, int lddx2, int M2,

@@ -54,13 +54,15 @@ struct GemmParams {
   int store_pol;              // epilogue output stores: 0 plain, 1 nt, 2 sc1 (write-through)
   bf16* c16;                  // EPI_F32 without split-K: store the gradient as bf16 here instead
   bf16* bg16;                 // (same ldc as C) and the bias gradient here -- the bf16 payload
-  int sgd_serial;             // 1: the per-fragment SGD epilogue (A/B of sgd_epilogue_batched)
+  int sgd_serial;             // SGD epilogue form (A/B): 0 LDS-staged rows (256x256 tiles,
+                              // default), 1 per fragment, 2 fragment rows batched
 };
-static int g_sgd_serial = -1;   // NNMPI_SGD_SERIAL=1: per-fragment SGD epilogue (experiments)
+static int g_sgd_serial = -1;   // NNMPI_SGD_SERIAL=<form> (experiments)
+void set_sgd_epilogue(int form) { g_sgd_serial = form; }   // -1: re-read the environment
 static int sgd_serial() {
   if (g_sgd_serial < 0) {
     const char* e = std::getenv("NNMPI_SGD_SERIAL");
-    g_sgd_serial = (e && e[0] == '1') ? 1 : 0;
+    g_sgd_serial = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 0;
   }
   return g_sgd_serial;
 }
@@ -268,7 +270,8 @@ template <int MI, int NJ, int EPI, int ACT, bool BIASGRAD>
 __device__ __forceinline__ void epilogue_store(const GemmParams& p, f32x4 (&acc)[MI][NJ],
                                                f32x4 (&accb)[MI], bool do_bg, const int (&mrow)[MI],
                                                const int (&ncol)[NJ], int lane, int split,
-                                               const f32x4* bias_pre = nullptr) {
+                                               const f32x4* bias_pre = nullptr,
+                                               bool main_done = false) {
   if constexpr (EPI == EPI_BIAS_ACT) {
     f32x4 bias[NJ];
     // unconditional (clamped) loads: no per-element branch -> no vmcnt(0) per element
@@ -326,9 +329,9 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& p, f32x4 (&acc)
     // a final (un-split) weight gradient on a single rank: the optimizer update is applied
     // here, in the epilogue -- no gradient store and no separate optimizer pass over it
     const bool fuse = p.sg.g_base != nullptr;
-    bool batched = false;
-    {
-      if (fuse && !p.c16 && !p.sgd_serial) {
+    bool batched = main_done;   // (the caller already applied the LDS-staged form)
+    if (!batched) {
+      if (fuse && !p.c16 && p.sgd_serial != 1) {
         sgd_epilogue_batched<MI, NJ>(p.sg, acc, mrow, ncol, cbase, p.ldc, p.M, p.N);
         batched = true;
       }
@@ -893,6 +896,70 @@ constexpr int PP_THREADS = 512;
 // barrier later stays inside it.
 // GM: grouped tile order (grouped_tile) -- 32 blocks resident per XCD read 4 A + 8 B panels per
 // K-tile instead of 1 A + 32 B at the 8192-wide shape.
+// SGD epilogue of a full 256x256 weight-gradient tile, staged through the (then idle) 128 KiB LDS
+// ring: each 128-row half of the fp32 tile is written to LDS ([128 rows][64 float4], float4 index
+// XOR (row & 15): conflict-free for the fragment writes and the row reads), then every wave
+// updates whole rows -- each memory instruction moves 1 KiB contiguous of master / momentum
+// (512 B of the bf16 shadow) instead of 16 row pieces of 64 B, and each lane keeps 8 rows of
+// master + momentum loads in flight (2 round trips per half instead of 4 fragment rows).  Same
+// arithmetic as sgd_fused_store4: bitwise identical.
+__device__ __forceinline__ void sgd_epilogue_lds_256(const GemmParams& p, const f32x4 (&acc)[8][4],
+                                                     char* smem, int m0, int n0, int wm, int wn,
+                                                     int w, int lane, int split) {
+  const SgdFuse& f = p.sg;
+  const float lr = f.hp[0], mom = f.hp[1], damp = f.hp[2], wd = f.hp[3], gs = f.hp[4];
+  const bool nest = f.nesterov != 0, first = f.first != 0;
+  const float* cbase = reinterpret_cast<const float*>(p.C) + split * p.c_split_stride;
+  const long long base = cbase - f.g_base;
+  f32x4* img = reinterpret_cast<f32x4*>(smem);
+#pragma unroll
+  for (int h = 0; h < 2; ++h) {
+    __syncthreads();   // the ring (h 0) / the previous half's rows (h 1) are no longer read
+#pragma unroll
+    for (int ii = 0; ii < 4; ++ii) {
+      const int r = wm * 64 + ii * 16 + (lane & 15);
+#pragma unroll
+      for (int j = 0; j < 4; ++j) {
+        const int cv = ((j >> 1) * 128 + wn * 32 + (j & 1) * 16) / 4 + (lane >> 4);
+        img[r * 64 + (cv ^ (r & 15))] = acc[h * 4 + ii][j];
+      }
+    }
+    __syncthreads();
+#pragma unroll
+    for (int sb = 0; sb < 2; ++sb) {
+      f32x4 pv[8], bv[8];
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int r = w * 16 + sb * 8 + k;
+        const long long o = base + (long long)(m0 + h * 128 + r) * p.ldc + n0 + lane * 4;
+        pv[k] = *reinterpret_cast<const f32x4*>(f.p_base + o);
+        bv[k] = *reinterpret_cast<const f32x4*>(f.m_base + o);
+      }
+#pragma unroll
+      for (int k = 0; k < 8; ++k) {
+        const int r = w * 16 + sb * 8 + k;
+        const long long o = base + (long long)(m0 + h * 128 + r) * p.ldc + n0 + lane * 4;
+        const f32x4 g = img[r * 64 + (lane ^ (r & 15))];
+        f32x4 q = pv[k], b = bv[k];
+#pragma unroll
+        for (int e = 0; e < 4; ++e) {
+          float bb = b[e];
+          q[e] = sgd_elem(q[e], g[e], bb, lr, mom, damp, wd, gs, nest, first);
+          b[e] = bb;
+        }
+        *reinterpret_cast<f32x4*>(f.p_base + o) = q;
+        if (mom != 0.f) *reinterpret_cast<f32x4*>(f.m_base + o) = b;
+        if (f.s_base) {
+          bf16x4 sv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) sv[e] = (bf16)q[e];
+          *reinterpret_cast<bf16x4*>(f.s_base + o) = sv;
+        }
+      }
+    }
+  }
+}
+
 // One 256x256 output tile: `bid` is the tile's XCD-remapped id in a gx x gy grid (the standalone
 // launch below, or one job of gemm_bf16_pp256_pair_kernel).
 template <int LA, int LB, int EPI, int ACT, bool BIASGRAD, bool LATE_LGKM = true, int GM = 4>
@@ -1053,7 +1120,16 @@ __device__ __forceinline__ void pp256_tile(const GemmParams& p, char* smem, int 
   for (int i = 0; i < 8; ++i) mrow[i] = m0 + (i >> 2) * 128 + wm * 64 + (i & 3) * 16 + (lane & 15);
 #pragma unroll
   for (int j = 0; j < 4; ++j) ncol[j] = n0 + (j >> 1) * 128 + wn * 32 + (j & 1) * 16 + (lane >> 4) * 4;
-  epilogue_store<8, 4, EPI, ACT, BIASGRAD>(p, acc, accb, do_bg, mrow, ncol, lane, split);
+  bool main_done = false;
+  if constexpr (EPI == EPI_F32) {
+    // block-uniform condition (full tile, fused SGD): the LDS-staged row form
+    if (p.sg.g_base && !p.c16 && p.sgd_serial == 0 && m0 + 256 <= p.M && n0 + 256 <= p.N) {
+      sgd_epilogue_lds_256(p, acc, smem, m0, n0, wm, wn, w, lane, split);
+      main_done = true;
+    }
+  }
+  epilogue_store<8, 4, EPI, ACT, BIASGRAD>(p, acc, accb, do_bg, mrow, ncol, lane, split, nullptr,
+                                           main_done);
 }
 
 template <int LA, int LB, int EPI, int ACT, bool BIASGRAD, bool LATE_LGKM = true, int GM = 4>
@@ -1303,7 +1379,7 @@ __device__ __forceinline__ void slab_reduce_block(const SlabReduce& r, int b, in
     const float* p = r.ws + m * N + n;
     float* o = r.out + m * r.ldo + n;
     // the combiner's optimizer operands are loaded first, beside the slab loads
-    const bool upd = combiner && v < nvec && r.sg.g_base && !r.sgd_serial;
+    const bool upd = combiner && v < nvec && r.sg.g_base && r.sgd_serial != 1;
     SgdPre4 pre{};
     if (upd) pre = sgd_pre4(r.sg, o);
 #pragma unroll

@@ -447,6 +447,27 @@ def test_wide_pair_launches_bitwise_equal(width, rows):
     assert a.losses[-1] == a.losses[-1]
 
 
+@pytest.mark.parametrize("rows", [4096, 600])
+def test_wide_sgd_epilogue_forms_bitwise_equal(rows):
+    """Single rank, 256x256 weight-gradient tiles with the SGD update in the epilogue: the
+    LDS-staged row form (default), the per-fragment form and the batched-fragment form give
+    identical parameters.  600 rows: partial dgrad/forward tiles; the 4096-wide weight tiles are
+    full either way (the LDS form needs a full tile and falls back per tile otherwise)."""
+    from nnmpi_amd import native
+    lib = native.lib()
+    cfg = _wide_cfg(widths=[4096] * 4 + [1], n_features=4096, n_samples=rows)
+    out = []
+    try:
+        for form in (0, 1, 2):
+            lib.set_sgd_epilogue(form)
+            out.append(trainer.run_worker(cfg))
+    finally:
+        lib.set_sgd_epilogue(-1)
+    for r in out[1:]:
+        assert r.losses == out[0].losses
+        assert torch.equal(r.final_params, out[0].final_params)
+
+
 def test_wide_chunked_buckets_overlap_bitwise_equal():
     """8192-wide layers cut into 4 output-row chunk buckets: each chunk's weight gradient is
     its own launch, its all-reduce starts behind it on the comm stream, its SGD runs on the
