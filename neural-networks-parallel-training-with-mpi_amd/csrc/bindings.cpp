@@ -102,6 +102,15 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
   m.def("wide_pair_dgrad_ok", &wide_pair_dgrad_ok);
   m.def("set_wide_pair", &set_wide_pair);
   m.def("set_sgd_epilogue", &set_sgd_epilogue);
+  m.def("wgrad_defer_ok", &wgrad_defer_ok);
+  m.def("linear_wgrad_bf16_out16_defer", [](uptr dZ, int lddz, uptr X, int ldx, uptr dW16, uptr db16,
+                                            int M, int N, int K, py::object other, uptr g16o, uptr s) {
+    SgdFuse f{};
+    if (!to_sgd(other, f)) throw std::runtime_error("deferred update needs its SGD operands");
+    check(linear_wgrad_bf16_out16_defer(P<const bf16>(dZ), lddz, P<const bf16>(X), ldx, P<bf16>(dW16),
+                                        P<bf16>(db16), M, N, K, f, P<const bf16>(g16o), S(s)),
+          "linear_wgrad_bf16_out16_defer");
+  });
   m.def("wide_pair_wgrad_dgrad_bf16", [](uptr dZ, int lddz, uptr X, int ldx, uptr dW, uptr db, int M,
                                          int N, int K, py::object sgd, uptr dZ2, int lddz2, uptr W2,
                                          int ldw2, uptr Ap2, int ldap2, uptr dX2, int lddx2, int M2,

@@ -54,6 +54,12 @@ struct GemmParams {
   int store_pol;              // epilogue output stores: 0 plain, 1 nt, 2 sc1 (write-through)
   bf16* c16;                  // EPI_F32 without split-K: store the gradient as bf16 here instead
   bf16* bg16;                 // (same ldc as C) and the bias gradient here -- the bf16 payload
+  // Deferred update of ANOTHER arena region with the same [M][N] shape (several ranks, bf16
+  // payload): this tile stores its own gradient as bf16 into c16 and applies SGD-momentum to the
+  // other region's element (m, n) with the reduced bf16 gradient g16o[m * ldc + n]; sg2's bases
+  // point at the other region's first element.  256x256 tiles, full tiles only.
+  SgdFuse sg2;
+  const bf16* g16o;
   int sgd_serial;             // SGD epilogue form (A/B): 0 LDS-staged rows (256x256 tiles,
                               // default), 1 per fragment, 2 fragment rows batched
 };
@@ -903,14 +909,17 @@ constexpr int PP_THREADS = 512;
 // (512 B of the bf16 shadow) instead of 16 row pieces of 64 B, and each lane keeps 8 rows of
 // master + momentum loads in flight (2 round trips per half instead of 4 fragment rows).  Same
 // arithmetic as sgd_fused_store4: bitwise identical.
+// OTHER: the tile's own gradient goes to the bf16 payload c16 (row stores from the same staged
+// image) and the update applies to the region sg2 / g16o (see GemmParams).
+template <bool OTHER = false>
 __device__ __forceinline__ void sgd_epilogue_lds_256(const GemmParams& p, const f32x4 (&acc)[8][4],
                                                      char* smem, int m0, int n0, int wm, int wn,
                                                      int w, int lane, int split) {
-  const SgdFuse& f = p.sg;
+  const SgdFuse& f = OTHER ? p.sg2 : p.sg;
   const float lr = f.hp[0], mom = f.hp[1], damp = f.hp[2], wd = f.hp[3], gs = f.hp[4];
   const bool nest = f.nesterov != 0, first = f.first != 0;
   const float* cbase = reinterpret_cast<const float*>(p.C) + split * p.c_split_stride;
-  const long long base = cbase - f.g_base;
+  const long long base = OTHER ? 0 : cbase - f.g_base;
   f32x4* img = reinterpret_cast<f32x4*>(smem);
 #pragma unroll
   for (int h = 0; h < 2; ++h) {
@@ -928,18 +937,31 @@ __device__ __forceinline__ void sgd_epilogue_lds_256(const GemmParams& p, const 
 #pragma unroll
     for (int sb = 0; sb < 2; ++sb) {
       f32x4 pv[8], bv[8];
+      f32x4 gov[OTHER ? 8 : 1];
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int r = w * 16 + sb * 8 + k;
         const long long o = base + (long long)(m0 + h * 128 + r) * p.ldc + n0 + lane * 4;
         pv[k] = *reinterpret_cast<const f32x4*>(f.p_base + o);
         bv[k] = *reinterpret_cast<const f32x4*>(f.m_base + o);
+        if constexpr (OTHER) {
+          const bf16x4 gq = *reinterpret_cast<const bf16x4*>(p.g16o + o);
+          gov[k] = f32x4{(float)gq[0], (float)gq[1], (float)gq[2], (float)gq[3]};
+        }
       }
 #pragma unroll
       for (int k = 0; k < 8; ++k) {
         const int r = w * 16 + sb * 8 + k;
         const long long o = base + (long long)(m0 + h * 128 + r) * p.ldc + n0 + lane * 4;
-        const f32x4 g = img[r * 64 + (lane ^ (r & 15))];
+        const f32x4 a = img[r * 64 + (lane ^ (r & 15))];
+        f32x4 g = a;
+        if constexpr (OTHER) {
+          g = gov[k];
+          bf16x4 o16;   // own gradient -> bf16 payload, rounded as cast_f32_bf16 rounds
+#pragma unroll
+          for (int e = 0; e < 4; ++e) o16[e] = (bf16)a[e];
+          *reinterpret_cast<bf16x4*>(p.c16 + (long long)(m0 + h * 128 + r) * p.ldc + n0 + lane * 4) = o16;
+        }
         f32x4 q = pv[k], b = bv[k];
 #pragma unroll
         for (int e = 0; e < 4; ++e) {
@@ -1125,6 +1147,9 @@ __device__ __forceinline__ void pp256_tile(const GemmParams& p, char* smem, int 
     // block-uniform condition (full tile, fused SGD): the LDS-staged row form
     if (p.sg.g_base && !p.c16 && p.sgd_serial == 0 && m0 + 256 <= p.M && n0 + 256 <= p.N) {
       sgd_epilogue_lds_256(p, acc, smem, m0, n0, wm, wn, w, lane, split);
+      main_done = true;
+    } else if (p.g16o && p.c16) {   // (the host admits full tiles only)
+      sgd_epilogue_lds_256<true>(p, acc, smem, m0, n0, wm, wn, w, lane, split);
       main_done = true;
     }
   }
@@ -1780,6 +1805,24 @@ hipError_t linear_wgrad_bf16_ex(const bf16* dZ, int lddz, const bf16* X, int ldx
     return hipSuccess;
   }
   return r.S > 0 ? slab_reduce(r, s) : hipSuccess;
+}
+
+bool wgrad_defer_ok(int M, int N, int K) {
+  return gemm_impl() == 2 && g_force_tile == 0 && g_variant == 0 && sgd_serial() == 0 &&
+         wgrad_tile(M, N) == 256 && M % 256 == 0 && N % 256 == 0 && wgrad_splits(M, N, K) == 1;
+}
+
+hipError_t linear_wgrad_bf16_out16_defer(const bf16* dZ, int lddz, const bf16* X, int ldx, bf16* dW16,
+                                         bf16* db16, int M, int N, int K, const SgdFuse& other,
+                                         const bf16* g16o, hipStream_t s) {
+  if (!wgrad_defer_ok(M, N, K) || !dW16 || !db16 || !g16o || !other.p_base) return hipErrorInvalidValue;
+  WgradArgs a{dZ, lddz, X, ldx, nullptr, nullptr, M, N, K, nullptr, SgdFuse{}, dW16, db16};
+  GemmParams p;
+  SlabReduce r;
+  make_wgrad(a, p, r);
+  p.sg2 = other;
+  p.g16o = g16o;
+  return launch_t<256, 256, XMAJ, XMAJ, EPI_F32, ACT_NONE, true>(p, 1, s);
 }
 
 hipError_t linear_wgrad_bf16(const bf16* dZ, int lddz, const bf16* X, int ldx, float* dW,

@@ -125,6 +125,15 @@ void set_wide_pair(int on);
 // 0 LDS-staged rows (256x256 tiles), 1 per fragment (operands loaded after the sums), 2 fragment
 // rows batched
 void set_sgd_epilogue(int form);
+// Deferred update fused into a weight-gradient epilogue (several ranks, bf16 payload): the
+// un-split 256x256 weight gradient [M][N] stores its own gradient as bf16 (dW16 / db16, the
+// all-reduce payload) and applies SGD-momentum to ANOTHER [M][N] region whose all-reduce has
+// completed: `other` holds that region's master / momentum / shadow bases (g_base unused) and
+// g16o its reduced bf16 gradient.  hipErrorInvalidValue unless wgrad_defer_ok.
+bool wgrad_defer_ok(int M, int N, int K);
+hipError_t linear_wgrad_bf16_out16_defer(const bf16* dZ, int lddz, const bf16* X, int ldx, bf16* dW16,
+                                         bf16* db16, int M, int N, int K, const SgdFuse& other,
+                                         const bf16* g16o, hipStream_t s);
 
 // ---- fp32 GEMM (gemm_f32.hip) ----
 hipError_t linear_fwd_f32(const float* X, int ldx, const float* W, int ldw, const float* bias,

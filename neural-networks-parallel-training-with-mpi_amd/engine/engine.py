@@ -22,6 +22,7 @@ on the CPU (gloo) — that is the reference-semantics path and the test oracle.
 from __future__ import annotations
 
 import math
+import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
@@ -120,6 +121,25 @@ class MLPEngine:
         self._w16 = (self._upd_grad is not None and dtype == torch.bfloat16
                      and hasattr(ops, "wgrad_can_write_bf16"))
         self._written16: List[Tuple[int, int]] = []
+        # Deferred updates (several ranks, bf16 payload written by the chunk weight gradients):
+        # the SGD of chunk bucket (layer i+1, rows r0:r1) runs in the epilogue of the weight
+        # gradient of chunk (layer i, rows r0:r1) -- same [rows, in] shape -- once its all-reduce
+        # has completed (the compute stream waits for that collective's event), instead of as a
+        # separate memory-bound pass next to compute-bound GEMMs.  _defer_plan: chunk bucket
+        # index -> the partner bucket it updates.
+        self._defer_plan: Dict[int, object] = {}
+        if (self._w16 and hasattr(ops, "linear_wgrad_defer") and not self.sharded
+                and os.environ.get("NNMPI_DEFER", "1") != "0"):
+            for i in range(L - 2):
+                if spec.layer_shape(i) != spec.layer_shape(i + 1):
+                    continue
+                nxt = {b.rows: b for b in arena.chunk_buckets(i + 1)}
+                for b in arena.chunk_buckets(i):
+                    if b.rows in nxt:
+                        self._defer_plan[b.index] = nxt[b.rows]
+        self._defer_targets = {b.index for b in self._defer_plan.values()}
+        self.ev_ar = ({b.index: torch.cuda.Event(enable_timing=False)
+                       for b in self._defer_plan.values()} if self._defer_plan else {})
         self.rows = 0
         self.steps_done = 0
         self._graphs: Dict[tuple, object] = {}
@@ -283,11 +303,37 @@ class MLPEngine:
         for b in chunks:
             r0, r1 = b.rows
             if g16 is not None:
-                self.ops.linear_wgrad(dz[:, r0:r1], x_in, None, None, out_bf16=(
-                    ar.weight(i, g16)[r0:r1], ar.bias(i, g16)[r0:r1]))
+                if not self._defer_update(b, i, dz[:, r0:r1], x_in, g16):
+                    self.ops.linear_wgrad(dz[:, r0:r1], x_in, None, None, out_bf16=(
+                        ar.weight(i, g16)[r0:r1], ar.bias(i, g16)[r0:r1]))
             else:
                 self.ops.linear_wgrad(dz[:, r0:r1], x_in, gW[r0:r1], gb[r0:r1], ws=self.ws)
             yield b
+
+    def _defer_update(self, b, i: int, dz, x_in, g16) -> bool:
+        """Launch chunk bucket b's weight gradient (layer i, bf16 payload) with the pending SGD
+        of its partner bucket fused into the epilogue; False when there is nothing to fuse."""
+        part = self._defer_plan.get(b.index)
+        if part is None:
+            return False
+        k = next((n for n, (pb, _) in enumerate(self._pending_sgd) if pb.index == part.index), None)
+        out_f, in_f = self.spec.layer_shape(i)
+        r0, r1 = b.rows
+        if k is None or not self.ops.wgrad_defer_ok(dz.shape[0], r1 - r0, in_f):
+            return False
+        self._pending_sgd.pop(k)
+        ar, main = self.arena, self.stream
+        main.wait_event(self.ev_ar[part.index])      # the partner's all-reduce has completed
+        woff = ar.by_name[f"layers.{2 * (i + 1)}.weight"].offset + part.rows[0] * in_f
+        self.ops.linear_wgrad_defer(dz, x_in, ar.weight(i, g16)[r0:r1], ar.bias(i, g16)[r0:r1],
+                                    ar, self.hp, self.nesterov, self._first, woff, g16)
+        # the rest of the partner bucket (its layer's bias and padding, in the last chunk)
+        wend = woff + (r1 - r0) * in_f
+        rest = part.offset + part.numel - wend
+        if rest > 0:
+            self.ops.sgd(ar, self.hp, self.nesterov, self._first, offset=wend, numel=rest,
+                         **self._upd_kw())
+        return True
 
     def _forward(self, x):
         h = x
@@ -556,6 +602,8 @@ class MLPEngine:
                     b, stream, cast_back=False, written=self._written16)
             else:
                 self._reduced[b.index] = self.sync.launch_bucket(b, stream)
+            if b.index in self.ev_ar and self._reduced[b.index] is not None:
+                self._reduced[b.index].record_event(self.ev_ar[b.index])
             self._flush_sgd(1)
         return self._reduced[b.index]
 
@@ -573,8 +621,14 @@ class MLPEngine:
             self._sgd_done.add(b.index)
 
     def _flush_sgd(self, n: Optional[int] = None):
-        while self._pending_sgd and (n is None or n > 0):
-            b, rs = self._pending_sgd.pop(0)
+        # (updates planned into a later weight-gradient epilogue stay queued for it;
+        # _join_comm runs whatever is left)
+        while n is None or n > 0:
+            k = next((k for k, (pb, _) in enumerate(self._pending_sgd)
+                      if pb.index not in self._defer_targets), None)
+            if k is None:
+                break
+            b, rs = self._pending_sgd.pop(k)
             with torch.cuda.stream(rs):
                 for l in b.layers:
                     rs.wait_event(self.ev_wfree[l])

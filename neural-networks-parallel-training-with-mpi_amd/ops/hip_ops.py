@@ -204,6 +204,30 @@ class HipOps:
     def bwd_group_supported(self, rows, out_f, in_f) -> bool:
         return bool(self.lib.bwd_group_supported(rows, out_f, in_f))
 
+    # ---- deferred update fused into a weight-gradient epilogue (several ranks, bf16 payload) ---
+    def wgrad_defer_ok(self, rows, out_f, in_f) -> bool:
+        return bool(self.lib.wgrad_defer_ok(out_f, in_f, rows))
+
+    def linear_wgrad_defer(self, dz, x, gW16, gb16, arena, hp, nesterov: bool, first: bool,
+                           other_offset: int, g16):
+        """Weight gradient ``dz^T x`` stored as bf16 into (gW16, gb16) -- the all-reduce payload --
+        while its epilogue applies SGD-momentum to the arena weights at ``other_offset`` (a region
+        of the same [out, in] shape whose reduced bf16 gradient is in ``g16`` at that offset)."""
+        rows, M = dz.shape
+        N = x.shape[1]
+        _check(self.wgrad_defer_ok(rows, M, N), "deferred update: weight gradient not eligible")
+        _check(tuple(gW16.shape) == (M, N) and gW16.stride(0) == N and gb16.numel() == M,
+               "deferred update: dense bf16 outputs")
+        _check(other_offset + M * N <= arena.numel and g16.numel() >= other_offset + M * N,
+               "deferred update: region out of range")
+        e, o = 4, other_offset
+        sh = _p(arena.shadow) + 2 * o if arena.shadow is not None else 0
+        other = (_p(arena.grad) + e * o, _p(arena.master) + e * o, _p(arena.momentum) + e * o, sh,
+                 _p(hp), int(nesterov), int(first))
+        self.lib.linear_wgrad_bf16_out16_defer(_p(dz), dz.stride(0), _p(x), x.stride(0), _p(gW16),
+                                               _p(gb16), M, N, rows, other, _p(g16) + 2 * o,
+                                               self.stream)
+
     # ---- wide-model backward pairs (one launch: weight gradient + SGD beside a dgrad) -------
     def wide_pair_wgrad_ok(self, rows, out_f, in_f) -> bool:
         return bool(self.lib.wide_pair_wgrad_ok(rows, out_f, in_f))
