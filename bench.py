@@ -47,6 +47,7 @@ from __future__ import annotations
 
 import argparse
 import json
+import math
 import os
 import socket
 import subprocess
@@ -62,6 +63,9 @@ BASELINE_SAMPLES_PER_S = {1: 32190.0, 2: 61546.0, 4: 88657.0, 8: 105377.0}
 # below this gradient volume the all-reduce is latency-bound: issue it inline (see parallel/sync.py)
 INLINE_MAX_GRAD_BYTES = 64 << 20
 EXTRA_STEPS = 50
+# untimed warm-up tops up to this much continuous step work on the GPU (DVFS ramp; see warm())
+MIN_WARM_MS = 30.0
+WARM_CHUNK = 16
 
 CONFIGS = {
     "proxy512": dict(widths=[512, 512, 512, 512, 1], loss="mse", rows=8192,
@@ -374,18 +378,42 @@ def run(a, job):
         mode = "none"
     elif native_comm is None and mode == "tune":
         mode = "inline"
+    warm_run = {"steps": 0}
+
     def warm(e, n):
-        """n untimed steps.  The timed region's graphs are captured FIRST (after the eager first
-        step), so the warm-up steps run right before the timed region: capturing is host-only
-        work, and a GPU left idle meanwhile drops its clocks, which a 20-step timed region
-        (2 ms) would otherwise start with (measured: within noise either way,
-        profiles/r2_experiments.md section 9)."""
+        """n untimed steps, then (GPU) a top-up to at least MIN_WARM_MS of continuous step work.
+        The timed region's graphs are captured FIRST (after the eager first step): capturing is
+        host-only work, and a GPU left idle meanwhile drops its clocks.  Measured on MI355X
+        (profiles/r2s2_short_region_warmup_ab.txt): after setup + capture the first ~10-20 ms of
+        steady work run at lower clocks -- the driver's 20-step region measured 0.1015-0.1017
+        ms/step after 5 warm-up steps (0.5 ms of work) and 0.0953-0.0970 after 200, 50 steps
+        0.0992-0.0995 vs 0.0938-0.0942 -- so a short region after W = 5 steps times the DVFS ramp,
+        not the step, and a 1-GPU run (no tuning phase) would be timed colder than an N-GPU run
+        (whose tuning keeps the GPU busy), skewing the scaling efficiency.  The top-up count is
+        derived from the slowest rank's warm-up step time, so every rank runs the same steps
+        (collectives); the JSON reports it (warmup_steps_run)."""
+        ran = 0
         if n > 0 and e.steps_done == 0:
             e.run_steps(1, 1)
             n -= 1
+            ran += 1
         e.prepare_steps(a.steps, chunk)
         e.prepare_steps(n, chunk_for(n))
+        if gpu:
+            e.prepare_steps(WARM_CHUNK, WARM_CHUNK)
+            torch.cuda.synchronize()
+        t0 = time.perf_counter()
         e.run_steps(n, chunk_for(n))
+        ran += n
+        if gpu and MIN_WARM_MS > 0 and n > 0:
+            e.synchronize()
+            per = max_over_ranks((time.perf_counter() - t0) / max(n, 1))
+            extra = max(0, math.ceil(MIN_WARM_MS * 1e-3 / max(per, 1e-6)) - n)
+            extra = -(-extra // WARM_CHUNK) * WARM_CHUNK
+            for _ in range(extra // WARM_CHUNK):
+                e.run_steps(WARM_CHUNK, WARM_CHUNK)
+            ran += extra
+        warm_run["steps"] += ran
 
     tune = None
     bucket_mb = a.bucket_mb
@@ -519,6 +547,7 @@ def run(a, job):
             "n_gpus": world,
             "steps": a.steps,
             "warmup": a.warmup,
+            "warmup_steps_run": warm_run["steps"],
             "ms_per_step": round(ms, 5),
             "higher_is_better": True,
             "scaling": a.scaling,
