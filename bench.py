@@ -49,7 +49,6 @@ import argparse
 import json
 import math
 import os
-import socket
 import subprocess
 import sys
 import time
@@ -138,9 +137,8 @@ def parse(argv=None):
 
 
 def _free_port() -> int:
-    with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from nnmpi_amd.parallel.dist import free_port
+    return free_port()
 
 
 def _fail(msg: str, code: int = 2):

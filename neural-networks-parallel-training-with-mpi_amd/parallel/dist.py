@@ -54,10 +54,26 @@ def detect_job() -> JobInfo:
     return JobInfo(0, 1, 0, 1, "single")
 
 
-def _free_port() -> int:
+def free_port() -> int:
+    """A free TCP port for a rendezvous store, BELOW the kernel's ephemeral range (32768+ by
+    default): an ephemeral port from bind(0) can be handed to another socket (an earlier job's
+    RCCL / gloo bootstrap, a connection in TIME_WAIT) before rank 0's store binds it -- seen as
+    EADDRINUSE in a multi-rank GPU test."""
+    import random
+    for _ in range(200):
+        port = random.randint(20000, 32000)
+        with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
+            try:
+                s.bind(("127.0.0.1", port))
+            except OSError:
+                continue
+            return port
     with socket.socket(socket.AF_INET, socket.SOCK_STREAM) as s:
         s.bind(("127.0.0.1", 0))
         return s.getsockname()[1]
+
+
+_free_port = free_port
 
 
 class _stdout_to_stderr:

@@ -1,7 +1,6 @@
 """Multi-process helpers for CPU (gloo) tests: run ``run_worker(cfg)`` on N spawned ranks and
 collect each rank's TrainResult through files (no shared state, separate RNGs)."""
 import os
-import socket
 import tempfile
 
 import torch
@@ -9,9 +8,8 @@ import torch.multiprocessing as mp
 
 
 def _free_port():
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        return s.getsockname()[1]
+    from nnmpi_amd.parallel.dist import free_port
+    return free_port()
 
 
 def _entry(rank, world, port, cfg, outdir, fn_name):
