@@ -447,15 +447,16 @@ def test_wide_pair_launches_bitwise_equal(width, rows):
     assert a.losses[-1] == a.losses[-1]
 
 
-@pytest.mark.parametrize("rows", [4096, 600])
-def test_wide_sgd_epilogue_forms_bitwise_equal(rows):
+@pytest.mark.parametrize("width,rows", [(4096, 4096), (4096, 600), (4000, 1000)])
+def test_wide_sgd_epilogue_forms_bitwise_equal(width, rows):
     """Single rank, 256x256 weight-gradient tiles with the SGD update in the epilogue: the
     LDS-staged row form (default), the per-fragment form and the batched-fragment form give
-    identical parameters.  600 rows: partial dgrad/forward tiles; the 4096-wide weight tiles are
-    full either way (the LDS form needs a full tile and falls back per tile otherwise)."""
+    identical parameters.  600 rows: partial dgrad/forward tiles; 4000 wide: the edge weight
+    tiles are partial, so interior tiles take the LDS form and edge tiles fall back to the
+    fragment form inside the same launch."""
     from nnmpi_amd import native
     lib = native.lib()
-    cfg = _wide_cfg(widths=[4096] * 4 + [1], n_features=4096, n_samples=rows)
+    cfg = _wide_cfg(widths=[width] * 4 + [1], n_features=width, n_samples=rows)
     out = []
     try:
         for form in (0, 1, 2):
