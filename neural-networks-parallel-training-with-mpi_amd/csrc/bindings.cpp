@@ -102,6 +102,7 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
   m.def("wide_pair_dgrad_ok", &wide_pair_dgrad_ok);
   m.def("set_wide_pair", &set_wide_pair);
   m.def("set_sgd_epilogue", &set_sgd_epilogue);
+  m.def("set_stage_epi", &set_stage_epi);
   m.def("wgrad_defer_ok", &wgrad_defer_ok);
   m.def("linear_wgrad_bf16_out16_defer", [](uptr dZ, int lddz, uptr X, int ldx, uptr dW16, uptr db16,
                                             int M, int N, int K, py::object other, uptr g16o, uptr s) {

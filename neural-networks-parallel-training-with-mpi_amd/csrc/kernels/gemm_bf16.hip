@@ -60,9 +60,19 @@ struct GemmParams {
   // point at the other region's first element.  256x256 tiles, full tiles only.
   SgdFuse sg2;
   const bf16* g16o;
+  int stage_epi;              // 256x256 forward: bias+act tile staged through LDS, row stores
   int sgd_serial;             // SGD epilogue form (A/B): 0 LDS-staged rows (256x256 tiles,
                               // default), 1 per fragment, 2 fragment rows batched
 };
+static int g_stage_epi = -1;   // NNMPI_STAGE_EPI=1: LDS-staged 256x256 forward epilogue (A/B)
+void set_stage_epi(int on) { g_stage_epi = on; }   // -1: re-read the environment
+static int stage_epi() {
+  if (g_stage_epi < 0) {
+    const char* e = std::getenv("NNMPI_STAGE_EPI");
+    g_stage_epi = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_stage_epi;
+}
 static int g_sgd_serial = -1;   // NNMPI_SGD_SERIAL=<form> (experiments)
 void set_sgd_epilogue(int form) { g_sgd_serial = form; }   // -1: re-read the environment
 static int sgd_serial() {
@@ -279,6 +289,7 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& p, f32x4 (&acc)
                                                const f32x4* bias_pre = nullptr,
                                                bool main_done = false) {
   if constexpr (EPI == EPI_BIAS_ACT) {
+   if (!main_done) {
     f32x4 bias[NJ];
     // unconditional (clamped) loads: no per-element branch -> no vmcnt(0) per element
     if (bias_pre) {
@@ -309,6 +320,7 @@ __device__ __forceinline__ void epilogue_store(const GemmParams& p, f32x4 (&acc)
         *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(p.C) + (long long)mrow[i] * p.ldc + ncol[j]) = o;
       }
     }
+   }
   } else if constexpr (EPI == EPI_DACT) {
     bf16x4 aux[MI][NJ];
 #pragma unroll
@@ -982,6 +994,44 @@ __device__ __forceinline__ void sgd_epilogue_lds_256(const GemmParams& p, const 
   }
 }
 
+// Forward epilogue of a full 256x256 tile staged through the idle 128 KiB LDS ring (A/B,
+// NNMPI_STAGE_EPI=1): act(acc + bias) as bf16 into a [256 rows][64 x 8 B] image (8-byte unit
+// index XOR 2*(row & 15): conflict-free fragment writes and row reads), then every wave stores
+// whole rows -- 512 B contiguous per instruction instead of 16 row pieces of 32 B.
+template <int ACT>
+__device__ __forceinline__ void bias_act_lds_256(const GemmParams& p, const f32x4 (&acc)[8][4],
+                                                 char* smem, int m0, int n0, int wm, int wn, int w,
+                                                 int lane) {
+  bf16x4* img = reinterpret_cast<bf16x4*>(smem);
+  f32x4 bias[4];
+#pragma unroll
+  for (int j = 0; j < 4; ++j) {
+    const int c = n0 + (j >> 1) * 128 + wn * 32 + (j & 1) * 16 + (lane >> 4) * 4;
+    bias[j] = p.bias ? *reinterpret_cast<const f32x4*>(p.bias + c) : f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  __syncthreads();   // the ring is no longer read
+#pragma unroll
+  for (int i = 0; i < 8; ++i) {
+    const int r = (i >> 2) * 128 + wm * 64 + (i & 3) * 16 + (lane & 15);
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      const int u = ((j >> 1) * 128 + wn * 32 + (j & 1) * 16) / 4 + (lane >> 4);
+      const f32x4 v = acc[i][j] + bias[j];
+      bf16x4 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) o[e] = (bf16)act_fwd_t<ACT>(v[e]);
+      img[r * 64 + (u ^ ((r & 15) << 1))] = o;
+    }
+  }
+  __syncthreads();
+#pragma unroll 4
+  for (int k = 0; k < 32; ++k) {
+    const int r = w * 32 + k;
+    *reinterpret_cast<bf16x4*>(reinterpret_cast<bf16*>(p.C) + (long long)(m0 + r) * p.ldc + n0 + lane * 4) =
+        img[r * 64 + (lane ^ ((r & 15) << 1))];
+  }
+}
+
 // One 256x256 output tile: `bid` is the tile's XCD-remapped id in a gx x gy grid (the standalone
 // launch below, or one job of gemm_bf16_pp256_pair_kernel).
 template <int LA, int LB, int EPI, int ACT, bool BIASGRAD, bool LATE_LGKM = true, int GM = 4>
@@ -1143,6 +1193,12 @@ __device__ __forceinline__ void pp256_tile(const GemmParams& p, char* smem, int 
 #pragma unroll
   for (int j = 0; j < 4; ++j) ncol[j] = n0 + (j >> 1) * 128 + wn * 32 + (j & 1) * 16 + (lane >> 4) * 4;
   bool main_done = false;
+  if constexpr (EPI == EPI_BIAS_ACT) {
+    if (p.stage_epi && m0 + 256 <= p.M && n0 + 256 <= p.N) {
+      bias_act_lds_256<ACT>(p, acc, smem, m0, n0, wm, wn, w, lane);
+      main_done = true;
+    }
+  }
   if constexpr (EPI == EPI_F32) {
     // block-uniform condition (full tile, fused SGD): the LDS-staged row form
     if (p.sg.g_base && !p.c16 && p.sgd_serial == 0 && m0 + 256 <= p.M && n0 + 256 <= p.N) {
@@ -1699,6 +1755,7 @@ hipError_t linear_fwd_bf16(const bf16* X, int ldx, const bf16* W, int ldw, const
   p.k_per_split = ((K + GEMM_BK - 1) / GEMM_BK) * GEMM_BK;
   p.C = Y; p.ldc = ldy; p.bias = bias;
   const int t = pick_tile(M, N);
+  p.stage_epi = stage_epi();
   if (t == 256) return launch_act<256, 256, KMAJ, KMAJ, EPI_BIAS_ACT, false>(p, act, 1, s);
   if (t == 128) {
     const int v = g_variant != 0 ? g_variant : g_fwd_variant >= 0 ? g_fwd_variant : FWD_VARIANT_DEFAULT;

@@ -125,6 +125,7 @@ void set_wide_pair(int on);
 // 0 LDS-staged rows (256x256 tiles), 1 per fragment (operands loaded after the sums), 2 fragment
 // rows batched
 void set_sgd_epilogue(int form);
+void set_stage_epi(int on);   // 1: LDS-staged 256x256 forward epilogue (A/B)
 // Deferred update fused into a weight-gradient epilogue (several ranks, bf16 payload): the
 // un-split 256x256 weight gradient [M][N] stores its own gradient as bf16 (dW16 / db16, the
 // all-reduce payload) and applies SGD-momentum to ANOTHER [M][N] region whose all-reduce has

@@ -469,6 +469,24 @@ def test_wide_sgd_epilogue_forms_bitwise_equal(width, rows):
         assert torch.equal(r.final_params, out[0].final_params)
 
 
+@pytest.mark.parametrize("width,rows", [(4096, 4096), (4000, 1000)])
+def test_wide_staged_forward_epilogue_bitwise_equal(width, rows):
+    """256x256 forward tiles: bias + activation staged through LDS with row stores == the
+    fragment stores (4000 wide / 1000 rows: partial edge tiles keep the fragment form)."""
+    from nnmpi_amd import native
+    lib = native.lib()
+    cfg = _wide_cfg(widths=[width] * 4 + [1], n_features=width, n_samples=rows)
+    out = []
+    try:
+        for on in (1, 0):
+            lib.set_stage_epi(on)
+            out.append(trainer.run_worker(cfg))
+    finally:
+        lib.set_stage_epi(-1)
+    assert out[0].losses == out[1].losses
+    assert torch.equal(out[0].final_params, out[1].final_params)
+
+
 def test_wide_chunked_buckets_overlap_bitwise_equal():
     """8192-wide layers cut into 4 output-row chunk buckets: each chunk's weight gradient is
     its own launch, its all-reduce starts behind it on the comm stream, its SGD runs on the
