@@ -217,7 +217,41 @@ def main(argv=None):
         if have < job.local_world and not isolated and not a.shared_gpu_rehearsal:
             _fail(f"{job.local_world} local ranks need as many GPUs; {have} visible "
                   "(one rank per GPU: RCCL refuses two ranks on one device)")
+    from nnmpi_amd.parallel import supervisor as sup
+    if job.world > 1 and not sup.supervised() and os.environ.get("NNMPI_BENCH_SUPERVISE", "1") != "0":
+        # this process never touches the GPU: it runs the rank as a child and retries the whole
+        # job in fresh processes with a more conservative schedule if any rank dies or hangs
+        sys.exit(supervise(a, argv, job))
     run(a, job)
+
+
+def fallback_ladder(a, argv):
+    """The argv of every attempt: as launched, then the origin-stream inline all-reduce (one
+    collective on the compute stream, the capture form measured to work at P = 2..8), then the
+    same without hipGraphs."""
+    ladder = [("as launched", [])]
+    if a.comm_mode != "inline":
+        ladder.append(("--comm_mode inline", ["--comm_mode", "inline"]))
+    if a.device != "cpu" and not a.no_graph:
+        ladder.append(("--comm_mode inline --no_graph", ["--comm_mode", "inline", "--no_graph"]))
+    n = int(os.environ.get("NNMPI_BENCH_ATTEMPTS", len(ladder)))
+    return [(d, [sys.executable, os.path.abspath(__file__)] + list(argv) + extra)
+            for d, extra in ladder[:max(1, n)]]
+
+
+def supervise(a, argv, job) -> int:
+    from nnmpi_amd.parallel.supervisor import Supervisor
+    ladder = fallback_ladder(a, argv)
+    s = Supervisor(job.rank, job.world, stall_s=float(os.environ.get("NNMPI_BENCH_STALL_S", 300)))
+
+    def annotate(line, log):
+        first_fail = next((f for e in log for f in (e["failures"] or [])), None)
+        # set when the measurement comes from a retry: why the first attempt was abandoned
+        line["fallback"] = first_fail if len(log) > 1 else None
+        line["attempts"] = log
+        line["measured_mode"] = log[-1]["mode"]
+        return line
+    return s.run([cmd for _, cmd in ladder], lambda k: ladder[k][0], annotate)
 
 
 def run(a, job):
@@ -231,10 +265,12 @@ def run(a, job):
     from nnmpi_amd.models.mlp import MLPSpec, reference_init
     from nnmpi_amd.parallel import dist as pdist
     from nnmpi_amd.parallel.sync import NativeRcclSync, NoSync, ShardedSync, TorchDistSync
+    from nnmpi_amd.parallel.supervisor import supervised, write_result
     from nnmpi_amd.utils.config import TrainConfig
     from nnmpi_amd.utils.metrics import comm_volume, scaling_report
 
     rank, world = job.rank, job.world
+    milestone = _milestones(rank)
     gpu = a.device == "cuda"
     if gpu:
         from nnmpi_amd import native
@@ -255,6 +291,7 @@ def run(a, job):
         make_ops = lambda: TorchOps(dev)  # noqa: E731
         a.comm = "torch"
     pg = pdist.ProcessGroupContext(job, 600.0, want_nccl=(gpu and a.comm == "torch" and world > 1))
+    milestone("rendezvous")
     c = CONFIGS[a.config]
     widths = c["widths"]
     spec = MLPSpec(tuple(widths), "relu", c["loss"])
@@ -275,6 +312,7 @@ def run(a, job):
         lib = native.lib()
         uid = pg.broadcast_object(lib.rccl_unique_id() if rank == 0 else None, 0)
         native_comm = native.make_comm(uid, world, rank, dev.index)
+    milestone("communicator")
     comm_group = pg.nccl if (gpu and pg.nccl is not None) else pg.gloo
 
     def shard(n_global):
@@ -390,6 +428,7 @@ def run(a, job):
         (whose tuning keeps the GPU busy), skewing the scaling efficiency.  The top-up count is
         derived from the slowest rank's warm-up step time, so every rank runs the same steps
         (collectives); the JSON reports it (warmup_steps_run)."""
+        milestone("warm-up")
         ran = 0
         if n > 0 and e.steps_done == 0:
             e.run_steps(1, 1)
@@ -428,6 +467,7 @@ def run(a, job):
             if half_mb > a.bucket_mb:
                 cands.append(("overlap", half_mb))
         for m, bmb in cands:
+            milestone(f"tune {m}")
             e = build(m, data, bucket_mb=bmb)
             e.run_steps(a.warmup, chunk_for(a.warmup))
             tm = min(timed(e, a.tune_steps, chunk_for(a.tune_steps)) for _ in range(2))
@@ -451,6 +491,7 @@ def run(a, job):
     # replay's fixed cost per chunk); every graph is captured before the timed region
     eng.prepare_steps(a.steps, chunk)
     loss0 = eng.loss()
+    milestone("timed")
     barrier()
     t0 = time.perf_counter()
     eng.run_steps(a.steps, chunk)
@@ -467,50 +508,76 @@ def run(a, job):
     n_buckets = len(eng.arena.buckets)
     wire = comm_volume(eng.arena.numel, world, grad_dtype, sharded=sharded,
                        shadow=eng.arena.shadow is not None)["wire_bytes_per_rank"]
+    milestone("measured")
+    # every replica must hold the same parameters and optimizer state, bit for bit: a hash of
+    # the fp32 master, the momentum and the bf16 shadow on every rank, all-gathered over gloo
+    digests = pg.allgather_object(replica_digest(eng, gpu))
+    replicas_equal = len(set(digests)) == 1
 
     # ---------------- after the timed region: what the BASELINE metric derives from it ----------
     extras = {}
     strong = None
     extras_error = None
 
+    def agree(ok: bool) -> bool:
+        """Every rank's verdict on an extras phase (MIN over gloo): one rank failing outside a
+        collective makes every rank skip the remaining phases together instead of leaving its
+        peers blocked in the next collective (a rank stuck INSIDE one is the supervisor's
+        stall detector's job)."""
+        if world == 1:
+            return ok
+        t = torch.tensor([1.0 if ok else 0.0], dtype=torch.float64)
+        pg.allreduce_cpu(t, op=dist.ReduceOp.MIN)
+        return bool(t.item() > 0.5)
+
+    def phase(name, fn):
+        nonlocal extras_error
+        milestone(f"extras {name}")
+        err = None
+        try:
+            fn()
+        except Exception as exc:   # noqa: BLE001
+            err = f"{name}: {type(exc).__name__}: {exc}"[:300]
+            print(f"[bench] extras failed on rank {rank}: {err}", file=sys.stderr, flush=True)
+        if not agree(err is None):
+            extras_error = err or f"{name} failed on another rank"
+            return False
+        return True
+
     def run_extras():
-        nonlocal eng, data
-        ex, st = {}, None
+        """Efficiency / comm-only / strong-scaling measurements, one agreed phase at a time."""
+        nonlocal eng, data, extras, strong
         n_ex = max(1, min(a.steps, EXTRA_STEPS))
-        comm_ms = None
-        if use_comm:
+        res = {"comm_ms": None, "comp_ms": ms}
+
+        def comm_only():
             # the step's collectives alone (same buckets / dtype / order), replayed like the step
             sync = eng.sync
             with torch.no_grad():
                 eng.arena.grad.zero_()
             if gpu:
                 torch.cuda.synchronize()
-            comm_ms = _time_comm_only(sync, n_ex, chunk_for(n_ex), gpu and not a.no_graph, barrier,
-                                      max_over_ranks) * 1e3
+            use_graph = gpu and not a.no_graph and not isinstance(sync, TorchDistSync)
+            res["comm_ms"] = _time_comm_only(sync, n_ex, chunk_for(n_ex), use_graph, barrier,
+                                             max_over_ranks) * 1e3
             with torch.no_grad():
                 eng.arena.grad.zero_()
-        eng = None
-        if gpu:
-            torch.cuda.empty_cache()
-        if use_comm:
+
+        def single():
             # the same per-rank work with the gradient sync off: every rank alone (1-GPU step)
             e = build("none", data, comm=False)
             e.run_steps(min(a.warmup, 10) + 1, chunk_for(min(a.warmup, 10)))
-            comp_ms = timed(e, n_ex, chunk_for(n_ex)) / n_ex * 1e3
-            del e
-        else:
-            comp_ms = ms
-        ex = scaling_report(world, max(data[0].counts), n_global, ms, comp_ms, comm_ms, wire)
-        ex["single_gpu_ms_per_step"] = comp_ms
-        data = None
-        if world > 1 and a.scaling == "weak":
+            res["comp_ms"] = timed(e, n_ex, chunk_for(n_ex)) / n_ex * 1e3
+
+        def strong_scaling():
             # strong scaling: the reference's fixed dataset (the 1-GPU shard, 8192 rows for the
             # proxy) split over the N ranks
+            nonlocal strong
             sdata = shard(rows_pg)
             e = build(mode if mode != "none" else "inline", sdata, bucket_mb=bucket_mb)
             e.run_steps(min(a.warmup, 10) + 1, chunk_for(min(a.warmup, 10)))
             s_ms = timed(e, n_ex, chunk_for(n_ex)) / n_ex * 1e3
-            del e, sdata
+            comp_ms = res["comp_ms"]
             # S(1): the single-GPU step of the whole dataset = the compute-only step above
             # (weak scaling gives every rank rows_pg rows, the last one rows_pg - 1)
             st = {"global_batch": rows_pg, "ms_per_step": round(s_ms, 5),
@@ -518,27 +585,36 @@ def run(a, job):
                   "parallel_efficiency": round(comp_ms / (world * s_ms), 4)}
             base = BASELINE_SAMPLES_PER_S.get(world) if a.config == "proxy512" else None
             st["vs_baseline"] = round(st["samples_per_s"] / base, 2) if base else None
+            strong = st
+
+        ok = True
+        if use_comm:
+            ok = phase("comm_only", comm_only)
+        eng = None
         if gpu:
             torch.cuda.empty_cache()
-        return ex, st
-
-    if not a.no_extras:
-        # the timed result above stands on its own: a failure in these extra measurements is
-        # reported in the JSON line instead of losing the line
-        try:
-            extras, strong = run_extras()
-        except Exception as exc:   # noqa: BLE001
-            extras_error = f"{type(exc).__name__}: {exc}"[:300]
-            print(f"[bench] extras failed on rank {rank}: {extras_error}", file=sys.stderr,
-                  flush=True)
+        if ok and use_comm:
+            ok = phase("single_gpu", single)
+        if ok and (res["comp_ms"] is not None):
+            extras = scaling_report(world, max(data[0].counts), n_global, ms, res["comp_ms"],
+                                    res["comm_ms"], wire)
+            extras["single_gpu_ms_per_step"] = res["comp_ms"]
+        data = None
+        if gpu:
+            torch.cuda.empty_cache()
+        if ok and world > 1 and a.scaling == "weak":
+            phase("strong_scaling", strong_scaling)
+        if gpu:
+            torch.cuda.empty_cache()
 
     base = BASELINE_SAMPLES_PER_S.get(world) if a.config == "proxy512" else None
     tflops = spec.flops_per_sample() * n_global / (ms * 1e-3) / 1e12
 
     def rnd(x, k=4):
         return None if x is None else round(float(x), k)
-    if rank == 0:
-        out = {
+
+    def line():
+        return {
             "metric": "samples_per_sec_whole_node",
             "value": round(value, 1),
             "unit": "samples/s",
@@ -568,6 +644,8 @@ def run(a, job):
                        "bucket_mb": bucket_mb,
                        "n_buckets": n_buckets},
             "rccl_ranks": (native_comm.size if native_comm is not None else None),
+            "replicas_bitwise_equal": replicas_equal,
+            "replica_hash": digests[0],
             "shared_gpu_rehearsal": bool(a.shared_gpu_rehearsal),
             "model_tflops_per_s": round(tflops, 2),
             "parallel_efficiency": rnd(extras.get("parallel_efficiency")),
@@ -582,12 +660,23 @@ def run(a, job):
             "loss_after_warmup": loss0,
             "final_loss": loss,
         }
-        print(json.dumps(out), flush=True)
+
+    if rank == 0 and supervised():
+        # the measurement so far, in case the extras never come back (the supervisor prints it)
+        write_result(dict(line(), extras_error="extras did not finish", complete=False))
+    if not a.no_extras:
+        run_extras()
+    milestone("done")
+    if rank == 0:
+        if supervised():
+            write_result(dict(line(), complete=True))
+        else:
+            print(json.dumps(line()), flush=True)
     # Teardown, in order, each step timed on stderr (NNMPI_TEARDOWN_TRACE=1): the graphs (which
     # hold captured RCCL kernels) and engines first, then the communicator, then the process
-    # group.  The result is already printed: a teardown that stalls (a communicator destroy
+    # group.  The result is already out: a teardown that stalls (a communicator destroy
     # waiting on a peer that has gone) must not keep the job alive, so a watchdog ends the
-    # process after TEARDOWN_S seconds.
+    # process after TEARDOWN_S seconds -- with a non-zero code, since a stall is still a defect.
     _exit_watchdog(TEARDOWN_S)
     if gpu:
         torch.cuda.synchronize()
@@ -604,6 +693,64 @@ def run(a, job):
 
 
 TEARDOWN_S = 60.0
+RC_TEARDOWN_STALL = 4     # = parallel.supervisor.RC_TEARDOWN_STALL (3: the step watchdog)
+
+
+def _milestones(rank: int):
+    """progress(phase) for the supervisor's stall detector, plus TESTING-only fault hooks:
+    NNMPI_BENCH_CRASH / NNMPI_BENCH_HANG = "rank:attempt[:phase]" make that rank die by SIGSEGV
+    / stop making progress when it reaches the phase (default: "timed") in that attempt ("*":
+    every attempt)."""
+    from nnmpi_amd.parallel.supervisor import progress
+
+    def hook(var):
+        spec = os.environ.get(var, "")
+        if not spec:
+            return None
+        parts = spec.split(":")
+        if int(parts[0]) != rank or parts[1] not in ("*", os.environ.get("NNMPI_ATTEMPT", "0")):
+            return None
+        return parts[2] if len(parts) > 2 else "timed"
+    crash_at, hang_at = hook("NNMPI_BENCH_CRASH"), hook("NNMPI_BENCH_HANG")
+
+    def milestone(phase: str):
+        progress(phase)
+        if crash_at == phase:
+            import signal
+            print(f"[bench] rank {rank}: injected SIGSEGV at '{phase}'", file=sys.stderr, flush=True)
+            os.kill(os.getpid(), signal.SIGSEGV)
+        if hang_at == phase:
+            print(f"[bench] rank {rank}: injected hang at '{phase}'", file=sys.stderr, flush=True)
+            while True:
+                time.sleep(60)
+    return milestone
+
+
+def replica_digest(eng, gpu: bool) -> str:
+    """Bitwise hash of this rank's replica: fp32 master, momentum and bf16 shadow (HIP kernel
+    hash_u32 on the GPU; sha256 of the bytes on the CPU).  A sharded optimizer (ZeRO-1) first
+    re-assembles the full master and momentum (a collective: every rank calls this)."""
+    import torch
+    ar = eng.arena
+    eng.synchronize()
+    if getattr(eng.sync, "sharded", False):
+        eng.sync.gather_state()
+    bufs = [ar.master, ar.momentum] + ([ar.shadow] if ar.shadow is not None else [])
+    if gpu:
+        from nnmpi_amd import native
+        torch.cuda.synchronize()
+        out = torch.zeros(len(bufs), 257, dtype=torch.int64, device=ar.master.device)
+        s = torch.cuda.current_stream()
+        for k, b in enumerate(bufs):
+            nbytes = b.numel() * b.element_size()
+            native.lib().hash_u32(b.data_ptr(), nbytes // 4, out[k].data_ptr(), int(s.cuda_stream))
+        vals = out[:, 256].cpu().tolist()
+        return "-".join(f"{v & 0xFFFFFFFFFFFFFFFF:016x}" for v in vals)
+    import hashlib
+    h = hashlib.sha256()
+    for b in bufs:
+        h.update(b.detach().cpu().contiguous().view(torch.uint8).numpy().tobytes())
+    return h.hexdigest()[:48]
 
 
 def _trace(msg: str):
@@ -616,9 +763,9 @@ def _exit_watchdog(seconds: float):
     import threading
 
     def fire():
-        print(f"[bench] teardown did not finish in {seconds:.0f} s: exiting (result already "
-              "printed)", file=sys.stderr, flush=True)
-        os._exit(0)
+        print(f"[bench] teardown did not finish in {seconds:.0f} s: exiting with code "
+              f"{RC_TEARDOWN_STALL} (result already out)", file=sys.stderr, flush=True)
+        os._exit(RC_TEARDOWN_STALL)
     t = threading.Timer(seconds, fire)
     t.daemon = True
     t.start()

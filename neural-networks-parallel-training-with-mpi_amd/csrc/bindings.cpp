@@ -340,6 +340,9 @@ PYBIND11_MODULE(_nnmpi_hip, m) {
   m.def("checksum_f32", [](uptr x, long long n, uptr out, uptr s) {
     check(checksum_f32(P<const float>(x), n, P<double>(out), S(s)), "checksum_f32");
   });
+  m.def("hash_u32", [](uptr x, long long n, uptr out, uptr s) {
+    check(hash_u32(P<const unsigned>(x), n, P<unsigned long long>(out), S(s)), "hash_u32");
+  });
 
   // ---- data ----
   m.def("gather_rows", [](uptr src, uptr dst, uptr idx, int n, long long row_bytes, long long n_src,

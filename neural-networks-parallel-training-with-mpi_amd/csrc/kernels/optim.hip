@@ -174,4 +174,52 @@ hipError_t checksum_f32(const float* x, long long n, double* out, hipStream_t s)
   return hipGetLastError();
 }
 
+// Bitwise replica hash: sum over i of mix64((i << 32) | word_i) mod 2^64 (splitmix64 finaliser).
+// A value sum (checksum_f32) can coincide for different bits (-0.0 vs 0.0, compensating
+// errors); this one changes with any flipped bit of any word, and integer addition makes the
+// result independent of the reduction order.  HASH_BLOCKS partials, then one block sums them.
+constexpr int HASH_BLOCKS = 256;
+
+__device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
+  z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
+  z = (z ^ (z >> 27)) * 0x94d049bb133111ebull;
+  return z ^ (z >> 31);
+}
+
+__global__ void __launch_bounds__(256) hash_u32_kernel(const unsigned* __restrict__ x, long long n,
+                                                       unsigned long long* __restrict__ part) {
+  __shared__ unsigned long long red[256];
+  unsigned long long h = 0;
+  const long long stride = (long long)gridDim.x * blockDim.x;
+  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+    h += mix64(((unsigned long long)i << 32) | x[i]);
+  red[threadIdx.x] = h;
+  __syncthreads();
+  for (int o = 128; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) part[blockIdx.x] = red[0];
+}
+
+__global__ void __launch_bounds__(256) hash_final_kernel(const unsigned long long* __restrict__ part,
+                                                         unsigned long long* __restrict__ out) {
+  __shared__ unsigned long long red[HASH_BLOCKS];
+  red[threadIdx.x] = part[threadIdx.x];
+  __syncthreads();
+  for (int o = HASH_BLOCKS / 2; o > 0; o >>= 1) {
+    if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) *out = red[0];
+}
+
+// out must hold HASH_BLOCKS + 1 uint64 (partials + the result at out[HASH_BLOCKS]).
+hipError_t hash_u32(const unsigned* x, long long n, unsigned long long* out, hipStream_t s) {
+  if (n < 0) return hipErrorInvalidValue;
+  hipLaunchKernelGGL(hash_u32_kernel, dim3(HASH_BLOCKS), dim3(256), 0, s, x, n, out);
+  hipLaunchKernelGGL(hash_final_kernel, dim3(1), dim3(HASH_BLOCKS), 0, s, out, out + HASH_BLOCKS);
+  return hipGetLastError();
+}
+
 }  // namespace nnmpi

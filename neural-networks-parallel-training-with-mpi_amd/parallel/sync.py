@@ -133,6 +133,8 @@ class TorchDistSync(GradSync):
     def comm_only(self):
         for b in self.arena.buckets:
             view = self.arena.grad[b.offset:b.offset + b.numel]
+            if self.bf16:   # the payload the step sends (the wire-byte count assumes it)
+                view = view.to(torch.bfloat16)
             if self.mode == "root":
                 dist.reduce(view, dst=0, group=self.group)
                 dist.broadcast(view, src=0, group=self.group)

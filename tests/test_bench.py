@@ -64,6 +64,44 @@ def test_bench_rank_failure_fails_the_job():
     assert r.returncode != 0
 
 
+def test_bench_rank_sigsegv_relaunches_fresh_ranks():
+    """A rank dying by a signal (what a crash inside a HIP/RCCL call looks like) does not cost the
+    result: the supervisors kill the attempt's survivors and re-run the job in fresh processes
+    with the inline schedule; the line says why (fallback) and which mode produced it."""
+    d = _line(_run(["--gpus", "2", "--device", "cpu", "--config", "ref", "--steps", "6",
+                    "--warmup", "2"], env={"NNMPI_BENCH_CRASH": "1:0"}))
+    assert "SIGSEGV" in d["fallback"] and d["measured_mode"] == "--comm_mode inline"
+    assert [e["result"] for e in d["attempts"]] == ["none", "full"]
+    assert d["replicas_bitwise_equal"] is True and d["extras_error"] is None
+
+
+def test_bench_rank_hang_is_detected_and_retried():
+    """A rank that stops making progress (a peer blocked forever in a collective) is killed after
+    the stall limit, and so is the rest of the attempt."""
+    d = _line(_run(["--gpus", "3", "--device", "cpu", "--config", "ref", "--steps", "6",
+                    "--warmup", "2"], env={"NNMPI_BENCH_HANG": "2:0", "NNMPI_BENCH_STALL_S": "8"}))
+    assert "no progress" in d["fallback"] and d["attempts"][-1]["result"] == "full"
+    assert d["n_gpus"] == 3 and d["replicas_bitwise_equal"] is True
+
+
+def test_bench_crash_in_extras_keeps_the_measurement_under_torchrun():
+    """Rank 0 dying after the timed region (inside the efficiency extras), under the driver's
+    torchrun form: the timed measurement is still printed, with extras_error, and rc 0."""
+    r = _torchrun(["--steps", "6", "--warmup", "2"],
+                  env={"NNMPI_BENCH_CRASH": "0:0:extras single_gpu"})
+    d = _line(r)
+    assert d["extras_error"] and d["parallel_efficiency"] is None
+    assert d["attempts"][0]["result"] == "core" and d["fallback"] is None
+    assert d["value"] > 0 and d["replicas_bitwise_equal"] is True
+
+
+def test_bench_every_attempt_failing_fails_the_job():
+    r = _run(["--gpus", "2", "--device", "cpu", "--config", "ref", "--steps", "4", "--warmup",
+              "1"], env={"NNMPI_BENCH_CRASH": "0:*"})
+    assert r.returncode != 0 and r.stdout.strip() == ""
+    assert r.stderr.count("injected SIGSEGV") == 2      # as launched, then inline
+
+
 def test_scaling_report_arithmetic():
     from nnmpi_amd.utils.metrics import scaling_report
     # 4 ranks x 1000 rows; step 2.0 ms, compute-only 1.5 ms, collectives alone 1.0 ms
@@ -106,22 +144,43 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
     assert d["parallel_efficiency"] is not None and d["comm_bus_gbps"] is not None
     assert d["strong_scaling"]["global_batch"] == 8192
     assert d["final_loss"] == d["final_loss"]
+    assert d["replicas_bitwise_equal"] is True and d["fallback"] is None
+
+
+@pytest.mark.gpu
+def test_bench_gpu_rank_sigsegv_falls_back_to_inline():
+    """The fallback with real GPU processes: RCCL rank 1 dies by SIGSEGV before the timed region
+    (its peer holds an RCCL communicator and captured graphs); fresh ranks re-run the job with
+    the inline schedule, and the replicas they leave are bitwise equal."""
+    r = _run(["--gpus", "2", "--shared_gpu_rehearsal", "--steps", "8", "--warmup", "2",
+              "--tune_steps", "4", "--no_extras"], env={"NNMPI_BENCH_CRASH": "1:0"}, timeout=300)
+    d = _line(r)
+    assert "SIGSEGV" in d["fallback"] and d["config"]["comm_mode"] == "inline"
+    assert d["rccl_ranks"] == 2 and d["replicas_bitwise_equal"] is True
+
+
+def _torchrun(args, n=2, env=None):
+    from nnmpi_amd.parallel.dist import free_port
+    e = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    e.update(env or {})
+    return subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                           "--nproc-per-node", str(n), "--master-addr", "127.0.0.1",
+                           "--master-port", str(free_port()), BENCH, "--gpus", str(n), "--device",
+                           "cpu", "--config", "ref"] + args, capture_output=True, text=True,
+                          timeout=300, env=e)
 
 
 def test_bench_under_torchrun_driver_command():
     """The driver's exact launch form: torch.distributed.run --nnodes=1 --nproc-per-node N
     --master-addr 127.0.0.1 --master-port P bench.py --gpus N (CPU plumbing here)."""
-    import socket
-    with socket.socket() as s:
-        s.bind(("127.0.0.1", 0))
-        port = s.getsockname()[1]
-    e = dict(os.environ)
-    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
-        e.pop(k, None)
-    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
-                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
-                        str(port), BENCH, "--gpus", "2", "--device", "cpu", "--config", "ref",
-                        "--steps", "6", "--warmup", "2"], capture_output=True, text=True,
-                       timeout=300, env=e)
-    d = _line(r)
+    d = _line(_torchrun(["--steps", "6", "--warmup", "2"]))
     assert d["n_gpus"] == 2 and d["steps"] == 6 and d["config"]["parallelism"] == "dp2"
+    assert d["replicas_bitwise_equal"] is True and d["fallback"] is None
+
+
+def test_bench_under_torchrun_sigsegv_falls_back():
+    d = _line(_torchrun(["--steps", "6", "--warmup", "2"], n=3,
+                        env={"NNMPI_BENCH_CRASH": "2:0:warm-up"}))
+    assert "rank 2 killed by SIGSEGV" == d["fallback"] and d["n_gpus"] == 3
