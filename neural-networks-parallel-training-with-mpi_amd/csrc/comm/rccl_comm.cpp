@@ -1,6 +1,8 @@
 #include <cstdlib>
 #include "rccl_comm.h"
+#include "kernels/kernels.h"
 
+#include <algorithm>
 #include <cstring>
 #include <stdexcept>
 
@@ -120,6 +122,41 @@ void RcclComm::scatterv(const void* sendbuf, const std::vector<long long>& count
   NCCL_THROW(ncclGroupEnd());
 }
 
+size_t RcclComm::acc32_slice(size_t count) const {
+  const size_t per = (count + nranks_ - 1) / nranks_;
+  return (per + 63) / 64 * 64;
+}
+
+void RcclComm::allreduce_bf16_acc32(void* buf, void* scratch, size_t count, hipStream_t s) {
+  if (nranks_ == 1) return;
+  const size_t c = acc32_slice(count);
+  auto off = [&](int r) { return std::min(count, (size_t)r * c); };
+  auto cnt = [&](int r) { return std::min(count, (size_t)(r + 1) * c) - off(r); };
+  bf16* b = static_cast<bf16*>(buf);
+  bf16* sc = static_cast<bf16*>(scratch);
+  // 1) all-to-all: slice q of my buffer to its owner q; every peer's copy of my slice into
+  //    scratch slot [peer]
+  NCCL_THROW(ncclGroupStart());
+  for (int q = 0; q < nranks_; ++q) {
+    if (q == rank_) continue;
+    if (cnt(q) > 0) NCCL_THROW(ncclSend(b + off(q), cnt(q), ncclBfloat16, q, comm_, s));
+    if (cnt(rank_) > 0) NCCL_THROW(ncclRecv(sc + (size_t)q * c, cnt(rank_), ncclBfloat16, q, comm_, s));
+  }
+  NCCL_THROW(ncclGroupEnd());
+  // 2) the owner's fp32 sum in rank order, one rounding, in place in its slice
+  if (cnt(rank_) > 0)
+    HIP_THROW(sum_slices_bf16(b + off(rank_), sc, nranks_, rank_, (long long)c,
+                              (long long)cnt(rank_), s));
+  // 3) all-gather of the reduced slices (grouped send/recv: uneven last slices)
+  NCCL_THROW(ncclGroupStart());
+  for (int q = 0; q < nranks_; ++q) {
+    if (q == rank_) continue;
+    if (cnt(rank_) > 0) NCCL_THROW(ncclSend(b + off(rank_), cnt(rank_), ncclBfloat16, q, comm_, s));
+    if (cnt(q) > 0) NCCL_THROW(ncclRecv(b + off(q), cnt(q), ncclBfloat16, q, comm_, s));
+  }
+  NCCL_THROW(ncclGroupEnd());
+}
+
 int RcclComm::poll_error(bool abort_on_error) {
   if (aborted_) return (int)ncclInvalidUsage;
   ncclResult_t r = ncclSuccess;
@@ -174,7 +211,10 @@ void GradSync::bucket_ready(int b, void* ptr, size_t count, int dtype, hipStream
   if (b < 0 || b >= (int)ready_.size()) throw std::runtime_error("bucket index out of range");
   HIP_THROW(hipEventRecord(ready_[b], compute));
   HIP_THROW(hipStreamWaitEvent(comm_stream_, ready_[b], 0));
-  comm_->allreduce(ptr, count, dtype, 0, comm_stream_);
+  if (dtype == 1 && acc32_scratch_)
+    comm_->allreduce_bf16_acc32(ptr, acc32_scratch_, count, comm_stream_);
+  else
+    comm_->allreduce(ptr, count, dtype, 0, comm_stream_);
 }
 
 void GradSync::join(hipStream_t compute) {

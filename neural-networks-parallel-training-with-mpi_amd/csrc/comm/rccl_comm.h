@@ -49,6 +49,15 @@ class RcclComm {
   void broadcast_pieces(void* base, const std::vector<long long>& offsets,
                         const std::vector<long long>& counts, const std::vector<int>& roots,
                         int dtype, hipStream_t s);
+  // bf16 sum all-reduce with ONE rounding: [buf, buf + count) is cut into 64-aligned owner
+  // slices; a grouped send/recv all-to-all delivers every rank's copy of slice r to rank r
+  // (scratch: at least acc32_scratch_elems(count) bf16), the owner adds the P copies in fp32 in
+  // rank order and rounds once, and a grouped all-gather returns the slices.  The same wire bytes
+  // as a ring all-reduce in bf16 -- which rounds the partial sum at every hop, so its error grows
+  // with P -- and every transfer takes the direct xGMI link between the two GPUs.
+  void allreduce_bf16_acc32(void* buf, void* scratch, size_t count, hipStream_t s);
+  size_t acc32_slice(size_t count) const;
+  size_t acc32_scratch_elems(size_t count) const { return acc32_slice(count) * nranks_; }
   // Returns the RCCL async error code (0 = ok); aborts the communicator on error if asked.
   int poll_error(bool abort_on_error);
   void abort();
@@ -66,12 +75,15 @@ class GradSync {
   ~GradSync();
   // compute stream -> (event) -> comm stream: all-reduce [ptr, ptr+count) of bucket b.
   void bucket_ready(int b, void* ptr, size_t count, int dtype, hipStream_t compute);
+  // bf16 buckets use RcclComm::allreduce_bf16_acc32 with this scratch (nullptr: ncclAllReduce)
+  void set_acc32_scratch(void* scratch) { acc32_scratch_ = scratch; }
   // comm stream -> (event) -> compute stream: everything launched so far is complete.
   void join(hipStream_t compute);
   hipStream_t comm_stream() const { return comm_stream_; }
 
  private:
   RcclComm* comm_;
+  void* acc32_scratch_ = nullptr;
   hipStream_t comm_stream_ = nullptr;
   std::vector<hipEvent_t> ready_;
   hipEvent_t done_ = nullptr;

@@ -211,6 +211,10 @@ hipError_t cast_f32_bf16(const float* x, bf16* y, long long n, hipStream_t s);
 hipError_t scale_f32(float* x, long long n, float a, hipStream_t s);
 hipError_t cast_bf16_f32(const bf16* x, float* y, long long n, hipStream_t s);
 hipError_t checksum_f32(const float* x, long long n, double* out, hipStream_t s);
+// out[j] = bf16(sum over q = 0..P-1, in order, of (q == me ? out[j] : scratch[q * stride + j]))
+// for j < n, accumulated in fp32 (the owner step of RcclComm::allreduce_bf16_acc32)
+hipError_t sum_slices_bf16(bf16* out, const bf16* scratch, int P, int me, long long stride,
+                           long long n, hipStream_t s);
 // bitwise replica hash of n 32-bit words; out: 257 uint64, result at out[256]
 hipError_t hash_u32(const unsigned* x, long long n, unsigned long long* out, hipStream_t s);
 

@@ -174,6 +174,53 @@ hipError_t checksum_f32(const float* x, long long n, double* out, hipStream_t s)
   return hipGetLastError();
 }
 
+// Owner step of the one-rounding bf16 all-reduce (rccl_comm.cpp): P bf16 copies of a slice,
+// summed in fp32 in rank order (the same order on every owner, so the result is a pure function
+// of the inputs), rounded once.  8 elements (16 B) per lane when the slice allows it.
+__global__ void __launch_bounds__(256) sum_slices_bf16_kernel(bf16* __restrict__ out,
+                                                              const bf16* __restrict__ sc, int P,
+                                                              int me, long long stride,
+                                                              long long n) {
+  const long long t0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long step = (long long)gridDim.x * blockDim.x;
+  const bool vec = ((((uintptr_t)out) | ((uintptr_t)sc)) & 15) == 0 && (stride % 8) == 0;
+  const long long n8 = vec ? n / 8 : 0;
+  for (long long i = t0; i < n8; i += step) {
+    float acc[8];
+#pragma unroll
+    for (int e = 0; e < 8; ++e) acc[e] = 0.f;
+    for (int q = 0; q < P; ++q) {
+      const bf16* src = (q == me) ? out : sc + (long long)q * stride;
+      const uint4 w = reinterpret_cast<const uint4*>(src)[i];
+      const unsigned ws[4] = {w.x, w.y, w.z, w.w};
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        acc[2 * e] += __uint_as_float(ws[e] << 16);
+        acc[2 * e + 1] += __uint_as_float(ws[e] & 0xffff0000u);
+      }
+    }
+    bf16x4 lo, hi;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) { lo[e] = (bf16)acc[e]; hi[e] = (bf16)acc[4 + e]; }
+    reinterpret_cast<bf16x4*>(out)[2 * i] = lo;
+    reinterpret_cast<bf16x4*>(out)[2 * i + 1] = hi;
+  }
+  for (long long j = n8 * 8 + t0; j < n; j += step) {
+    float acc = 0.f;
+    for (int q = 0; q < P; ++q) acc += (float)((q == me) ? out[j] : sc[(long long)q * stride + j]);
+    out[j] = (bf16)acc;
+  }
+}
+
+hipError_t sum_slices_bf16(bf16* out, const bf16* scratch, int P, int me, long long stride,
+                           long long n, hipStream_t s) {
+  if (P < 1 || me < 0 || me >= P || n < 0 || stride < n) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(sum_slices_bf16_kernel, dim3(grid_for((n + 7) / 8)), dim3(256), 0, s, out,
+                     scratch, P, me, stride, n);
+  return hipGetLastError();
+}
+
 // Bitwise replica hash: sum over i of mix64((i << 32) | word_i) mod 2^64 (splitmix64 finaliser).
 // A value sum (checksum_f32) can coincide for different bits (-0.0 vs 0.0, compensating
 // errors); this one changes with any flipped bit of any word, and integer addition makes the

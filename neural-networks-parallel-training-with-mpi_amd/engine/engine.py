@@ -573,7 +573,8 @@ class MLPEngine:
             self._mark("comm")
             for b in ar.buckets:
                 if b.index not in self._sgd_done:
-                    ops.sgd(ar, self.hp, self.nesterov, first, offset=b.offset, numel=b.numel)
+                    ops.sgd(ar, self.hp, self.nesterov, first, offset=b.offset, numel=b.numel,
+                            **self._upd_kw())
             return
         if fz is not None:
             for i in unfused:
@@ -819,6 +820,7 @@ class MLPEngine:
         if origin is None:
             origin = self.stream
         g.begin(int(origin.cuda_stream))
+        self.sync.record(True)
         try:
             if origin is not self.stream:
                 # collectives live on the comm stream: it is the capture origin, the compute
@@ -828,10 +830,15 @@ class MLPEngine:
             if origin is not self.stream:
                 origin.wait_stream(self.stream)
         except Exception:
+            self.sync.record(False)
             g.cancel()    # leave the stream out of capture mode, drop the partial graph
             raise
+        notes = self.sync.record(False)
         g.end()
-        return g
+        # the capture issued these collectives once, but every launch runs them: the launch
+        # adds them to the collective signature (utils/seqcheck.py), the capture does not
+        self.sync.seq -= len(notes)
+        return _Graph(g, self.sync, notes)
 
     # ---------------- gradient accumulation ----------------------------------------------------
     # Not in the reference (one backward per step, SURVEY.md §2.3 "optional").  A step over more
@@ -944,6 +951,17 @@ class MLPEngine:
     @property
     def flops_per_step(self) -> float:
         return float(self.spec.flops_per_sample()) * self.rows
+
+
+class _Graph:
+    """A captured graph plus the collectives it issues per launch (for the signature)."""
+
+    def __init__(self, runner, sync, notes):
+        self.runner, self.sync, self.notes = runner, sync, notes
+
+    def launch(self, stream_handle: int):
+        self.runner.launch(stream_handle)
+        self.sync.replay(self.notes)
 
 
 class _SilentSync:

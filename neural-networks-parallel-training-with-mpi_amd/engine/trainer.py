@@ -61,6 +61,7 @@ class TrainResult:
     epoch_times: List[float] = field(default_factory=list)
     steps: int = 0
     phase_ms: Optional[dict] = None   # --profile_steps: mean ms per step per phase
+    schedule: Optional[dict] = None   # what the engine chose: payload, sync, grouped/deferred
 
 
 def dist_train(args) -> Optional[TrainResult]:
@@ -84,7 +85,7 @@ class Job:
         self.job = pdist.detect_job()
         self.rank, self.world = self.job.rank, self.job.world
         self.device = torch.device("cpu")
-        if resolve_device(cfg.device) == "cuda":
+        if resolve_device(cfg.device, self.job.local_world) == "cuda":
             if not torch.cuda.is_available():
                 raise RuntimeError("--device cuda requested but no GPU is visible")
             ndev = torch.cuda.device_count()
@@ -231,12 +232,22 @@ def broadcast_params(j: Job, arena: Arena):
     arena.sync_shadow()
 
 
+def grad_payload(cfg: TrainConfig, device_type: str, numel: int) -> str:
+    """The all-reduce payload dtype: ``auto`` is bf16 on the GPU above INLINE_MAX_GRAD_BYTES of
+    fp32 gradient (the bandwidth-bound regime; same rule as bench.py), fp32 otherwise."""
+    if cfg.grad_dtype != "auto":
+        return cfg.grad_dtype
+    return "bf16" if (device_type == "cuda" and numel * 4 > INLINE_MAX_GRAD_BYTES
+                      and not cfg.shard_optimizer) else "fp32"
+
+
 def make_sync(j: Job, arena: Arena):
     cfg = j.cfg
     if j.comm_kind == "none":
         return NoSync(arena)
+    grad_dtype = grad_payload(cfg, j.device.type, arena.numel)
     if cfg.shard_optimizer:
-        if cfg.sync == "root" or cfg.grad_dtype != "fp32":
+        if cfg.sync == "root" or grad_dtype != "fp32":
             raise ValueError("--shard_optimizer reduce-scatters fp32 gradients "
                              "(no --sync root / --grad_dtype bf16)")
         if j.comm_kind == "native":
@@ -247,11 +258,11 @@ def make_sync(j: Job, arena: Arena):
         inline = (cfg.comm_mode == "inline" or
                   (cfg.comm_mode == "auto" and arena.numel * 4 <= INLINE_MAX_GRAD_BYTES))
         return NativeRcclSync(arena, j.native_comm, j.world, inline=inline,
-                              grad_dtype=cfg.grad_dtype, mode=cfg.sync)
+                              grad_dtype=grad_dtype, mode=cfg.sync)
     group = (j.pg.nccl if (j.device.type == "cuda" and j.pg.nccl is not None
                            and j.comm_kind != "gloo") else j.pg.gloo)
     return TorchDistSync(arena, group, j.world, mode=cfg.sync, overlap=cfg.overlap,
-                         grad_dtype=cfg.grad_dtype)
+                         grad_dtype=grad_dtype)
 
 
 def make_ops(j: Job):
@@ -373,11 +384,19 @@ def _run(j: Job) -> TrainResult:
         eng.timer = EventTimer(j.device.type)
     Xc = X.to(dtype)
     metrics = MetricsWriter(cfg.metrics_json if rank == 0 else None)
-    cvol = comm_volume(arena.numel, world, cfg.grad_dtype, sharded=getattr(sync, "sharded", False),
+    cvol = comm_volume(arena.numel, world, grad_payload(cfg, j.device.type, arena.numel),
+                       sharded=getattr(sync, "sharded", False),
                        shadow=arena.shadow is not None)
     seqchk = SequenceChecker(j.pg) if cfg.seqcheck else None
+    if seqchk is not None:
+        seqchk.check_plan(sync)      # before any gradient collective
     wd = Watchdog(cfg.timeout_s, j.native_comm) if world > 1 else None
     res = TrainResult(rank, world, rows=rows_local)
+    res.schedule = {"device": j.device.type, "comm": j.comm_kind, "sync": type(sync).__name__,
+                    "grad_dtype": grad_payload(cfg, j.device.type, arena.numel),
+                    "inline": bool(getattr(sync, "inline", False)),
+                    "grouped": bool(eng.grouped), "deferred_updates": len(eng._defer_plan),
+                    "graph": bool(eng.use_graph)}
     n_micro = max(1, math.ceil(max_rows / mb)) if mb else 1
     steps_per_epoch = math.ceil(n_micro / K) if K > 1 else (1 if not bs else n_micro)
 
@@ -403,8 +422,12 @@ def _run(j: Job) -> TrainResult:
             eng.set_scales(*loss_scales(cfg, eng.rows, list(train_counts), cfg.widths[-1]))
             hist = torch.zeros(FAST_EPOCHS, dtype=torch.float32, device=j.device)
             epoch = start_epoch
+            # epochs per replay: the watchdog is kicked once per replay, so with several ranks a
+            # replay must stay well inside timeout_s -- start small, then size it (a power of two,
+            # so only a few graphs are ever captured) from the measured epoch time
+            per_replay = 4 if wd else FAST_EPOCHS
             while epoch < cfg.nepochs:
-                c = min(FAST_EPOCHS, cfg.nepochs - epoch)
+                c = min(per_replay, cfg.nepochs - epoch)
                 t0 = time.perf_counter()
                 eng.run_steps(c, c, losses=hist)
                 eng.synchronize()            # the losses are written on the engine's stream
@@ -412,6 +435,8 @@ def _run(j: Job) -> TrainResult:
                 dt = (time.perf_counter() - t0) / c
                 if wd:
                     wd.kick()
+                    fit = int(0.25 * cfg.timeout_s / max(dt, 1e-9))
+                    per_replay = max(1, min(FAST_EPOCHS, 1 << max(0, fit.bit_length() - 1)))
                 for k in range(c):
                     _print(cfg, rank, "[ = = = = = Epoch {} = = = = = ]".format(epoch + k))
                     res.losses.append(vals[k])
@@ -508,7 +533,7 @@ def _run(j: Job) -> TrainResult:
                 res.val_losses.append(vl)
                 _print(cfg, rank, f"validation loss: {vl}") if rank == 0 else None
             if seqchk:
-                seqchk.check(epoch, sync.seq)
+                seqchk.check(epoch, sync.seq, sync.sig)
             sps = sum(train_counts) / dt if dt > 0 else None
             metrics.write(epoch=epoch, loss=loss, epoch_s=dt, steps=steps_per_epoch,
                           samples_per_s=sps, world=world,

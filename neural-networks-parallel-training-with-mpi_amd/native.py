@@ -23,8 +23,19 @@ _lib = None
 
 def _load():
     path = _build.ext_path()
-    if not os.path.exists(path):
+    want = _build.source_hash()
+    have = _build.built_hash(path) if os.path.exists(path) else ""
+    if have != want:
+        # a missing or STALE library (built from other csrc sources than these): rebuild it
+        # (hipcc, in-tree) rather than run kernels that are not the ones in the tree; without
+        # a toolchain this raises
+        print(f"[nnmpi_amd] native library {'missing' if not have else 'stale'} "
+              f"(built from {have or '-'}, sources are {want}): rebuilding", file=sys.stderr,
+              flush=True)
         _build.build(verbose=True)
+        have = _build.built_hash(path)
+        if have != want:
+            raise RuntimeError(f"rebuilt {path} but it carries source hash {have!r}, not {want!r}")
     name = __package__ + "._nnmpi_hip"
     if name in sys.modules:
         return sys.modules[name]

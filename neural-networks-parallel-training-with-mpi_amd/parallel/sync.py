@@ -55,6 +55,37 @@ class GradSync:
         self._pending_layers = set()
         self._done_buckets = set()
         self.seq = 0  # collective sequence number (for the sequence checker)
+        self.sig = 0  # running signature of every collective issued (kind, bucket, offset, size)
+        self._recording: Optional[list] = None
+
+    # -- collective signature (utils/seqcheck.py) --------------------------------------------
+    # kinds: 1 all-reduce, 2 root reduce+broadcast, 3 reduce-scatter/owner-update/all-gather;
+    # dtype codes: 0 fp32, 1 bf16.  Python hashes tuples of ints identically in every process.
+    def note(self, kind: int, index: int, offset: int, numel: int, dtype: int):
+        rec = (kind, index, offset, numel, dtype)
+        self.seq += 1
+        self.sig = (self.sig * 1000003 ^ hash(rec)) & 0xFFFFFFFFFFFFFFFF
+        if self._recording is not None:
+            self._recording.append(rec)
+
+    def record(self, on: bool):
+        """Start (on) / stop (returns the notes) recording the collectives issued meanwhile: the
+        engine records a graph capture's collectives and replays them into the signature at
+        every launch of that graph."""
+        if on:
+            self._recording = []
+            return None
+        out, self._recording = self._recording or [], None
+        return out
+
+    def replay(self, notes):
+        for rec in notes:
+            self.note(*rec)
+
+    def plan(self):
+        """What this rank will issue every step: sync kind, payload dtype, buckets."""
+        return (type(self).__name__, getattr(self, "bf16", False),
+                tuple((b.index, b.offset, b.numel) for b in self.arena.buckets))
 
     def begin(self):
         self._done_buckets = set()
@@ -101,8 +132,9 @@ class NoSync(GradSync):
 
 
 class TorchDistSync(GradSync):
-    """``grad_dtype="bf16"``: the payload is rounded to bf16 before and after the reduction
-    (the gloo/CPU rendition of the compressed all-reduce; the native path reduces in bf16)."""
+    """``grad_dtype="bf16"``: the payload is rounded to bf16 before and after an fp32 reduction
+    -- the numeric contract of the native path's one-rounding bf16 all-reduce
+    (NativeRcclSync ``bf16_reduce="acc32"``), up to gloo's summation order at P > 2."""
 
     def __init__(self, arena, group, world: int, mode: str = "allreduce", overlap: bool = True,
                  grad_dtype: str = "fp32"):
@@ -117,7 +149,8 @@ class TorchDistSync(GradSync):
 
     def _launch(self, bucket):
         view = self.arena.grad[bucket.offset:bucket.offset + bucket.numel]
-        self.seq += 1
+        self.note(2 if self.mode == "root" else 1, bucket.index, bucket.offset, bucket.numel,
+                  int(self.bf16))
         if self.bf16:
             view.copy_(view.to(torch.bfloat16))
             self._rounded.append(view)
@@ -158,7 +191,13 @@ class NativeRcclSync(GradSync):
     faster than overlap; large volumes use the overlapped comm stream."""
 
     def __init__(self, arena, native_comm, world: int, priority: int = -1, inline: bool = False,
-                 grad_dtype: str = "fp32", mode: str = "allreduce"):
+                 grad_dtype: str = "fp32", mode: str = "allreduce", bf16_reduce: str = ""):
+        """``bf16_reduce`` (bf16 payload): ``acc32`` (default) sums the P bf16 copies of every
+        element in fp32 on its owner and rounds ONCE (all-to-all + owner sum + all-gather,
+        RcclComm::allreduce_bf16_acc32) -- the result is bf16(sum_r bf16(g_r)) whatever P is,
+        the same contract as the CPU path's round / fp32-sum / round; ``rccl`` is ncclAllReduce
+        in bf16, whose ring rounds the partial sum at every one of its P-1 hops (the error
+        grows with P: tests/test_multirank_gpu.py::test_rccl_bf16_reduction_error_vs_p)."""
         super().__init__(arena)
         self.mode = mode
         # the root pattern is a serial reduce + broadcast: always on the compute stream
@@ -181,10 +220,28 @@ class NativeRcclSync(GradSync):
         self.gbuf = (torch.zeros(arena.numel, dtype=torch.bfloat16, device=arena.grad.device)
                      if self.bf16 else None)
         self._comm_stream = torch.cuda.ExternalStream(self.gs.comm_stream)
+        import os
+        self.bf16_reduce = bf16_reduce or os.environ.get("NNMPI_BF16_REDUCE", "acc32")
+        if self.bf16_reduce not in ("acc32", "rccl"):
+            raise ValueError(f"bf16_reduce must be acc32 or rccl, not {self.bf16_reduce!r}")
+        self.scratch = None
+        if self.bf16 and self.bf16_reduce == "acc32" and mode != "root":
+            # one bucket reduces at a time on its stream: scratch for the largest
+            n = max(b.numel for b in arena.buckets)
+            self.scratch = torch.empty(max(1, native_comm.acc32_scratch_elems(n)),
+                                       dtype=torch.bfloat16, device=arena.grad.device)
+            self.gs.set_acc32_scratch(self.scratch.data_ptr())
+
+    def _allreduce(self, ptr: int, n: int, dt: int, h: int):
+        if dt == 1 and self.scratch is not None:
+            self.comm.allreduce_bf16_acc32(ptr, self.scratch.data_ptr(), n, h)
+        else:
+            self.comm.allreduce(ptr, n, dt, 0, h)
 
     def _launch(self, bucket, stream=None, cast_back: bool = True, written=()):
         view = self.arena.grad[bucket.offset:bucket.offset + bucket.numel]
-        self.seq += 1
+        self.note(2 if self.mode == "root" else 1, bucket.index, bucket.offset, bucket.numel,
+                  int(self.bf16))
         h = int(stream.cuda_stream) if stream is not None else self.native.stream_handle()
         lib = self.native.lib()
         ptr, dt = view.data_ptr(), 0
@@ -201,7 +258,7 @@ class NativeRcclSync(GradSync):
                 self.comm.reduce(ptr, bucket.numel, dt, 0, 0, h)
                 self.comm.broadcast(ptr, bucket.numel, dt, 0, h)
             else:
-                self.comm.allreduce(ptr, bucket.numel, dt, 0, h)
+                self._allreduce(ptr, bucket.numel, dt, h)
             if self.bf16:
                 lib.cast_bf16_f32(ptr, view.data_ptr(), bucket.numel, h)
             return
@@ -241,7 +298,7 @@ class NativeRcclSync(GradSync):
                 self.comm.reduce(ptr, b.numel, dt, 0, 0, h)
                 self.comm.broadcast(ptr, b.numel, dt, 0, h)
             else:
-                self.comm.allreduce(ptr, b.numel, dt, 0, h)
+                self._allreduce(ptr, b.numel, dt, h)
             if self.bf16:
                 lib.cast_bf16_f32(ptr, view.data_ptr(), b.numel, h)
 
@@ -325,7 +382,7 @@ class ShardedSync(GradSync):
     def update(self, ops, hp, nesterov: bool, first: bool):
         """Reduce-scatter -> owner SGD -> all-gather, on the current (compute) stream."""
         ar = self.arena
-        self.seq += 1
+        self.note(3, 0, 0, self.shard, 0)
         if self.comm is not None:
             h = self.native.stream_handle()
             g = ar.grad.data_ptr()

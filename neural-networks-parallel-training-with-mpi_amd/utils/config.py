@@ -75,7 +75,8 @@ class TrainConfig:
     overlap: bool = True
     graph: bool = True                # capture the steady-state step in a HIP graph
     fast_epochs: bool = True          # full-batch GPU epochs replayed 64 per graph (same output)
-    grad_dtype: str = "fp32"          # fp32 | bf16 (all-reduce payload dtype)
+    grad_dtype: str = "auto"          # auto | fp32 | bf16 (all-reduce payload dtype; auto: bf16
+                                      # above 64 MB of fp32 gradient on the GPU, as bench.py)
     shard_optimizer: bool = False     # ZeRO-1: reduce-scatter grads, SGD on own 1/P, all-gather
     deterministic: bool = True
     # --- IO / observability ---
@@ -161,7 +162,9 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--no_fast_epochs", dest="fast_epochs", action="store_false",
                    help="one graph replay + loss readback per epoch (default: 64 epochs per "
                         "replay, losses recorded on the device; identical output)")
-    p.add_argument("--grad_dtype", choices=["fp32", "bf16"], default="fp32")
+    p.add_argument("--grad_dtype", choices=["auto", "fp32", "bf16"], default="auto",
+                   help="all-reduce payload: auto = bf16 above 64 MB of fp32 gradient on the GPU "
+                        "(one-rounding reduction, see parallel/sync.py), fp32 otherwise")
     p.add_argument("--shard_optimizer", "--zero1", dest="shard_optimizer", action="store_true",
                    help="sharded optimizer state (ZeRO-1): reduce-scatter gradients, SGD on this "
                         "rank's 1/P of the parameters, all-gather the updated parameters")
@@ -220,17 +223,22 @@ def config_from_args(args) -> TrainConfig:
     return cfg
 
 
-def resolve_device(device: str) -> str:
-    """``auto`` -> ``cuda`` when a GPU is visible.  ``device_count()`` does not initialise the
-    HIP runtime, so a launcher process may call this before it spawns its ranks."""
+def resolve_device(device: str, local_world: int = 1) -> str:
+    """``auto`` -> ``cuda`` when every local rank can have a GPU of its own (RCCL refuses two
+    ranks on one device), else ``cpu``: ``mpiexec -n 4`` on a 1-GPU node runs the CPU/gloo path
+    as the reference does.  ``device_count()`` does not initialise the HIP runtime, so a
+    launcher process may call this before it spawns its ranks."""
     if device != "auto":
         return device
     import torch
-    return "cuda" if torch.cuda.device_count() > 0 else "cpu"
+    n = torch.cuda.device_count()
+    return "cuda" if n > 0 and local_world <= n else "cpu"
 
 
 def validate(cfg: TrainConfig) -> None:
     """Fail fast before any collective."""
+    if cfg.grad_dtype not in ("auto", "fp32", "bf16"):
+        raise ValueError(f"grad_dtype must be auto, fp32 or bf16, got {cfg.grad_dtype!r}")
     if cfg.device not in ("auto", "cpu", "cuda"):
         raise ValueError(f"device must be auto, cpu or cuda, got {cfg.device!r}")
     if len(cfg.widths) < 2:

@@ -14,6 +14,9 @@ import threading
 import time
 
 
+ABORT_GRACE_S = 15.0
+
+
 class Watchdog:
     def __init__(self, timeout_s: float, native_comm=None, poll_s: float = 1.0, on_fail=None):
         self.timeout_s = float(timeout_s)
@@ -49,12 +52,25 @@ class Watchdog:
 
     def _fail(self, why: str):
         self.failed = why
+        # a backstop first: if ncclCommAbort itself never returns (a peer's kernel that ignores
+        # the abort flag), the process still ends, non-zero, ABORT_GRACE_S later
+        backstop = threading.Timer(ABORT_GRACE_S, self._backstop, args=(why,))
+        backstop.daemon = True
+        backstop.start()
         if self.comm is not None:
+            print(f"[nnmpi watchdog] rank {os.environ.get('RANK', '?')}: {why}; aborting the "
+                  "RCCL communicator", file=sys.stderr, flush=True)
             try:
                 self.comm.abort()
             except Exception:
                 pass
         self.on_fail(why)
+
+    @staticmethod
+    def _backstop(why: str):
+        print(f"[nnmpi watchdog] rank {os.environ.get('RANK', '?')}: abort did not return in "
+              f"{ABORT_GRACE_S:.0f} s after '{why}'; exiting", file=sys.stderr, flush=True)
+        os._exit(3)
 
     @staticmethod
     def _default_fail(why: str):

@@ -32,7 +32,8 @@ def run_ranks(cfg, world, fn_name="run_worker"):
         return [torch.load(os.path.join(d, f"r{r}.pt"), weights_only=True) for r in range(world)]
 
 
-def run_ranks_proc(cfg: dict, world: int, env_per_rank=None, timeout: float = 150.0):
+def run_ranks_proc(cfg: dict, world: int, env_per_rank=None, timeout: float = 150.0,
+                   entry: str = "_rank_entry.py"):
     """Like :func:`run_ranks`, but every rank is an independent ``subprocess`` (as mpiexec /
     torchrun start them) with a hard time limit: on a hang or a failing rank every process is
     killed and the test fails with the ranks' stderr.  ``env_per_rank(rank) -> dict`` adds
@@ -41,7 +42,7 @@ def run_ranks_proc(cfg: dict, world: int, env_per_rank=None, timeout: float = 15
     import subprocess
     import sys
     import time
-    entry = os.path.join(os.path.dirname(os.path.abspath(__file__)), "_rank_entry.py")
+    entry = os.path.join(os.path.dirname(os.path.abspath(__file__)), entry)
     port = _free_port()
     with tempfile.TemporaryDirectory() as d:
         procs, logs = [], []

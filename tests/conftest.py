@@ -13,6 +13,18 @@ def pytest_configure(config):
     config.addinivalue_line("markers", "slow: longer multi-process runs")
 
 
+def pytest_report_header(config):
+    """The provenance of the native library under test: the hash of the csrc tree and the hash
+    the built .so carries (they must match; nnmpi_amd.native rebuilds a stale library)."""
+    try:
+        import nnmpi_amd  # noqa: F401
+        from nnmpi_amd import _build
+        return (f"nnmpi_amd csrc source hash {_build.source_hash()}, built library "
+                f"{_build.built_hash() or 'missing'} ({os.path.basename(_build.ext_path())})")
+    except Exception as e:  # pragma: no cover
+        return f"nnmpi_amd source hash unavailable: {e}"
+
+
 def gpu_available():
     try:
         import torch

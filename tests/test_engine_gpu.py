@@ -672,3 +672,39 @@ def test_minibatch_epoch_graph_same_as_per_step(comm):
     b = trainer.run_worker(_cfg(fast_epochs=False, **kw))
     assert a.losses == b.losses and a.steps == b.steps == 20
     assert torch.equal(a.final_params, b.final_params)
+
+
+def test_compat_cli_wide_preset_takes_the_bench_schedule():
+    """``--preset wide8192 --comm native`` through the compat trainer picks what bench.py picks:
+    the bf16 payload (auto: > 64 MB of fp32 gradient) and the overlapped chunk buckets whose
+    updates ride in the next weight-gradient epilogue (deferred updates)."""
+    from nnmpi_amd.utils.config import build_parser, config_from_args
+    cfg = config_from_args(build_parser().parse_args(
+        ["--preset", "wide8192", "--comm", "native", "--nepochs", "2", "--print_rank", "none",
+         "--data_gen", "device", "--data_dist", "local", "--scaling", "none", "--lr", "1e-5"]))
+    res = trainer.run_worker(cfg)
+    sch = res.schedule
+    assert sch["grad_dtype"] == "bf16" and sch["sync"] == "NativeRcclSync" and not sch["inline"]
+    assert sch["deferred_updates"] > 0, sch
+    assert all(l == l for l in res.losses)
+
+
+def test_mpiexec_default_device_on_a_one_gpu_node_matches_golden():
+    """`mpiexec -n 2 python dataParallelTraining_NN_MPI.py` with no flags on a node with fewer
+    GPUs than ranks: --device auto resolves to the CPU/gloo path (RCCL cannot put two ranks on
+    one device) and the reference's P=2 losses come out."""
+    import os
+    import subprocess
+    import sys
+    import torch as _t
+    if _t.cuda.device_count() >= 2:
+        pytest.skip("the node has a GPU per rank")
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = dict(os.environ)
+    env.pop("MASTER_ADDR", None)
+    env.pop("MASTER_PORT", None)
+    r = subprocess.run(["/opt/conda/bin/mpiexec", "-n", "2", sys.executable,
+                        os.path.join(root, "dataParallelTraining_NN_MPI.py")],
+                       capture_output=True, text=True, timeout=300, env=env)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "loss in worker 1: 2835.11" in r.stdout

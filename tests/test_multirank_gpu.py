@@ -161,7 +161,9 @@ def test_rccl_grouped_overlap_two_ranks_bitwise():
     """512-wide (grouped backward kernels) at P=2: per-bucket all-reduce overlapped on the comm
     stream == one inline all-reduce == the gloo all-reduce, bit for bit."""
     kw = dict(widths=[512, 512, 512, 1], n_features=512, n_samples=4096, lr=1e-4)
-    a = run_ranks_proc(_cfg(comm="native", comm_mode="overlap", **kw), 2, env_per_rank=rccl_env)
+    # (--seqcheck: the per-epoch collective signature, replayed graphs included, agrees)
+    a = run_ranks_proc(_cfg(comm="native", comm_mode="overlap", seqcheck=True, **kw), 2,
+                       env_per_rank=rccl_env)
     b = run_ranks_proc(_cfg(comm="native", comm_mode="inline", **kw), 2, env_per_rank=rccl_env)
     c = run_ranks_proc(_cfg(comm="gloo", graph=False, **kw), 2)
     _replicas_equal(a)
@@ -184,3 +186,126 @@ def test_rccl_chunked_buckets_two_ranks_bitwise(grad_dtype):
     b = run_ranks_proc(_cfg(comm="native", comm_mode="inline", **kw), 2, env_per_rank=env)
     _replicas_equal(a)
     assert torch.equal(a[0]["final"], b[0]["final"])
+
+
+# ---------------------------------------------------------------- bf16 payload numerics, P > 2
+def _bf16_reduce_job(world, n=300_007):
+    return run_ranks_proc({"n": n}, world, env_per_rank=rccl_env, timeout=240,
+                          entry="_rccl_reduce_entry.py")
+
+
+def _rel(x, exact):
+    return float((x.double() - exact).norm() / exact.norm())
+
+
+@pytest.mark.parametrize("world", [3, 4, 8])
+def test_rccl_bf16_reduction_error_vs_p(world):
+    """The bf16 gradient payload's reduction at P = 3 / 4 / 8 (ranks sharing the GPU).
+
+    * acc32 (the default): bitwise equal on every rank to bf16(sum over ranks, in rank order, in
+      fp32, of bf16(g_r)) -- one rounding of the inputs, one of the sum, whatever P is -- so its
+      error against the exact sum of the fp32 gradients stays at the bf16 half-ulp level
+      (<= 2^-8 relative per element).
+    * ncclAllReduce in bf16 is measured next to it (its ring rounds the partial sum at every
+      hop) and both errors are written to gpurun_out/ for the record; only acc32 is pinned.
+    The reference averages fp32 gradients exactly (ref.py:190-197)."""
+    out = _bf16_reduce_job(world)
+    g = [o["g"] for o in out]
+    exact = torch.stack([x.double() for x in g]).sum(0)
+    emul = torch.zeros_like(g[0])
+    for x in g:                                  # fp32 accumulation in rank order
+        emul += x.to(torch.bfloat16).float()
+    emul = emul.to(torch.bfloat16)
+    for r, o in enumerate(out):
+        assert torch.equal(o["acc32"], emul), f"rank {r}: acc32 differs from its contract"
+        assert torch.equal(o["acc32"], out[0]["acc32"]) and torch.equal(o["ring_bf16"], out[0]["ring_bf16"])
+    e_acc, e_ring = _rel(out[0]["acc32"], exact), _rel(out[0]["ring_bf16"], exact)
+    e_f32 = _rel(out[0]["fp32"], exact)
+    # elementwise: bf16 inputs (2^-9 relative each, summed) + one output rounding (2^-9)
+    bound = (torch.stack([x.double().abs() for x in g]).sum(0) * 2.0 ** -9 +
+             exact.abs() * 2.0 ** -8 + 1e-30)
+    assert bool(((out[0]["acc32"].double() - exact).abs() <= bound).all())
+    assert e_acc < 8e-3 and e_f32 < 1e-6
+    import json
+    import os
+    os.makedirs("gpurun_out", exist_ok=True)
+    with open("gpurun_out/bf16_reduce_error.jsonl", "a") as f:
+        f.write(json.dumps({"world": world, "n": int(exact.numel()), "rel_err_acc32": e_acc,
+                            "rel_err_rccl_bf16_ring": e_ring, "rel_err_fp32": e_f32}) + "\n")
+
+
+@pytest.mark.parametrize("world", [3, 4])
+def test_rccl_bf16_payload_training_close_to_fp32(world):
+    """~20 steps of a 1024x3 model with chunk buckets forced, bf16 payload (acc32 reduction,
+    overlapped chunk all-reduces, deferred updates) vs the fp32 payload at P = 3 / 4:
+    replicas bitwise equal, and the parameter UPDATE within 1e-2 relative (L2) of the fp32
+    run's.  Justification: each step's reduced gradient differs from the fp32 one by at most
+    the two bf16 roundings (2^-9 relative each per element, ~0.4 % worst case, ~0.2 % typical);
+    the update is a momentum average of such gradients times lr, so its relative error stays
+    at that level over 20 small steps -- 1e-2 leaves a 2.5x margin over the worst case."""
+    kw = dict(widths=[1024, 1024, 1024, 1], n_features=1024, lr=1e-4, bucket_mb=1.0,
+              n_samples=256 * world, nepochs=20, comm_mode="overlap")
+
+    def env(r):
+        return dict(rccl_env(r), NNMPI_CHUNK_MIN_TILES="4")
+    init = run_ranks_proc(_cfg(comm="none", nepochs=0, **{k: v for k, v in kw.items()
+                                                          if k != "nepochs"}), 1)[0]["final"]
+    b16 = run_ranks_proc(_cfg(comm="native", grad_dtype="bf16", **kw), world, env_per_rank=env,
+                         timeout=300)
+    f32 = run_ranks_proc(_cfg(comm="native", grad_dtype="fp32", **kw), world, env_per_rank=env,
+                         timeout=300)
+    _replicas_equal(b16)
+    _replicas_equal(f32)
+    du16, du32 = b16[0]["final"] - init, f32[0]["final"] - init
+    assert float(du32.norm()) > 0
+    rel = float((du16 - du32).norm() / du32.norm())
+    assert rel < 1e-2, rel
+
+
+# ---------------------------------------------------------------- failure path over RCCL
+def test_rccl_one_rank_failure_ends_every_rank():
+    """The GPU twin of test_parallel_cpu.py::test_one_rank_failure_ends_every_rank: 3 RCCL ranks
+    (graph-replayed steps, the all-reduce captured in the step's hipGraph), rank 1 raising at
+    epoch 1 while ranks 0 and 2 wait inside the captured collective.  The reference hangs here
+    (ref.py:185,203).  Every rank must exit non-zero within timeout_s + 30 s
+    (after start-up), the survivors through the watchdog, which aborts the communicator
+    (ncclCommAbort) so the spinning collective kernels return."""
+    import os
+    import subprocess
+    import sys
+    import time
+    from _mp import _free_port
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    timeout_s, world, fail = 20, 3, 1
+    port = _free_port()
+    procs = []
+    for r in range(world):
+        env = dict(os.environ, RANK=str(r), WORLD_SIZE=str(world), LOCAL_RANK=str(r),
+                   LOCAL_WORLD_SIZE=str(world), MASTER_ADDR="127.0.0.1", MASTER_PORT=str(port),
+                   NNMPI_FAULT_INJECT=f"{fail}:1", OMP_NUM_THREADS="1", **rccl_env(r))
+        procs.append(subprocess.Popen(
+            [sys.executable, os.path.join(root, "dataParallelTraining_NN_MPI.py"), "--device",
+             "cuda", "--comm", "native", "--nepochs", "40", "--timeout_s", str(timeout_s),
+             "--print_rank", "none"], env=env, stdout=subprocess.PIPE, stderr=subprocess.PIPE,
+            text=True))
+    t_fail = None
+    deadline = time.monotonic() + 240
+    try:
+        while any(p.poll() is None for p in procs) and time.monotonic() < deadline:
+            if t_fail is None and procs[fail].poll() is not None:
+                t_fail = time.monotonic()
+            time.sleep(0.2)
+        t_end = time.monotonic()
+    finally:
+        for p in procs:
+            if p.poll() is None:
+                p.kill()
+                p.wait()
+    errs = [p.stderr.read() for p in procs]
+    codes = [p.returncode for p in procs]
+    assert all(c not in (None, 0) for c in codes), (codes, [e[-2000:] for e in errs])
+    assert "injected fault" in errs[fail]
+    assert t_fail is not None and t_end - t_fail < timeout_s + 30, (t_end - t_fail, codes)
+    for r in range(world):
+        if r != fail:
+            assert "nnmpi watchdog" in errs[r] or "RCCL" in errs[r], errs[r][-2000:]

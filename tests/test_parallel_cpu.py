@@ -67,6 +67,21 @@ def test_sequence_checker_passes():
     assert len(out) == 2
 
 
+def test_sequence_checker_catches_bucket_layout_mismatch():
+    """Two ranks with different bucket layouts (rank 1 chunks the 512x512 layer into row
+    buckets, rank 0 does not) issue the same number of collectives with different sizes -- a
+    hang or silent corruption over RCCL.  --seqcheck compares the plans before the first
+    collective and every rank raises instead."""
+    from _mp import run_ranks_proc
+    cfg = dict(device="cpu", print_rank="none", widths=[512, 512, 1], n_features=512,
+               n_samples=64, bucket_mb=0.1, seqcheck=True, nepochs=2, data_gen="device",
+               data_dist="local")
+    with pytest.raises(AssertionError, match="CollectiveMismatch"):
+        run_ranks_proc(cfg, 2, env_per_rank=lambda r: {"NNMPI_CHUNK_MIN_TILES": "1"} if r else {})
+    out = run_ranks_proc(cfg, 2)             # same layout everywhere: passes
+    assert torch.equal(out[0]["final"], out[1]["final"])
+
+
 def test_bf16_cpu_path_trains():
     cfg = TrainConfig(device="cpu", print_rank="none", widths=[64, 64, 64, 1], n_features=64, n_samples=512,
                       dtype="bf16", nepochs=4, lr=1e-4)
@@ -143,7 +158,7 @@ def test_mpiexec_launch_matches_golden():
     env.pop("MASTER_ADDR", None)
     env.pop("MASTER_PORT", None)
     r = subprocess.run(["/opt/conda/bin/mpiexec", "-n", "2", sys.executable,
-                        os.path.join(ROOT, "dataParallelTraining_NN_MPI.py")],
+                        os.path.join(ROOT, "dataParallelTraining_NN_MPI.py"), "--device", "cpu"],
                        capture_output=True, text=True, timeout=300, env=env)
     assert r.returncode == 0, r.stderr[-2000:]
     got = {}
@@ -157,8 +172,8 @@ def test_mpiexec_launch_matches_golden():
 
 def test_self_spawn_cli():
     r = subprocess.run([sys.executable, os.path.join(ROOT, "dataParallelTraining_NN_MPI.py"),
-                        "--nprocs", "2", "--nepochs", "1"], capture_output=True, text=True,
-                       timeout=300)
+                        "--nprocs", "2", "--nepochs", "1", "--device", "cpu"],
+                       capture_output=True, text=True, timeout=300)
     assert r.returncode == 0, r.stderr[-2000:]
     assert "loss in worker 1: 2835.11" in r.stdout
 
@@ -209,6 +224,39 @@ def test_sharded_optimizer_checkpoint_resume_is_exact(tmp_path):
     run_ranks(TrainConfig(device="cpu", nepochs=3, checkpoint=ck, **cfg), 2)
     res = run_ranks(TrainConfig(device="cpu", nepochs=5, resume=ck, **cfg), 2)
     assert torch.equal(res[0]["final"], full[0]["final"])
+
+
+def test_zero1_checkpoint_resumes_at_another_world_size(tmp_path):
+    """A ZeRO-1 checkpoint written at P=2 (arena padded to 2*64) resumes at P=3 -- with ZeRO-1
+    (padded to 3*64) and without it: the momentum is stored per parameter name, unpadded, and
+    re-laid into the new arena, so both resumed runs start from the saved state bit for bit and
+    continue identically."""
+    import torch as _t
+    ck, ck2, ck3 = (str(tmp_path / n) for n in ("z.pt", "z3.pt", "a3.pt"))
+    base = dict(print_rank="none", n_samples=48, scaling="global", averaging="weighted")
+    run_ranks(TrainConfig(device="cpu", nepochs=3, checkpoint=ck, shard_optimizer=True, **base), 2)
+    saved = _t.load(ck + ".train", weights_only=True)
+    # resumed with nothing left to train: the re-saved state is the saved one
+    run_ranks(TrainConfig(device="cpu", nepochs=3, resume=ck, checkpoint=ck2,
+                          shard_optimizer=True, **base), 3)
+    again = _t.load(ck2 + ".train", weights_only=True)
+    for k, v in saved["momentum_by_name"].items():
+        assert _t.equal(again["momentum_by_name"][k], v), k
+        assert float(v.abs().sum()) > 0, k                  # a real (non-restarted) momentum
+    a = run_ranks(TrainConfig(device="cpu", nepochs=5, resume=ck, shard_optimizer=True, **base), 3)
+    b = run_ranks(TrainConfig(device="cpu", nepochs=5, resume=ck, checkpoint=ck3, **base), 3)
+    assert _t.equal(a[0]["final"], b[0]["final"])
+
+
+def test_resume_with_mismatched_optimizer_state_raises(tmp_path):
+    ck = str(tmp_path / "m.pt")
+    trainer.run_worker(TrainConfig(device="cpu", print_rank="none", nepochs=1, checkpoint=ck))
+    import torch as _t
+    st = _t.load(ck + ".train", weights_only=True)
+    st["momentum_by_name"]["layers.0.weight"] = _t.zeros(4, 2)
+    _t.save(st, ck + ".train")
+    with pytest.raises(ValueError, match="layers.0.weight"):
+        trainer.run_worker(TrainConfig(device="cpu", print_rank="none", nepochs=2, resume=ck))
 
 
 def _reference_val_loss(res, n_val):

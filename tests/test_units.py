@@ -228,3 +228,28 @@ def test_subtract_ranges():
     assert _subtract((0, 10), [(2, 4), (6, 8)]) == [(0, 2), (4, 6), (8, 10)]
     assert _subtract((5, 10), [(0, 6), (9, 20)]) == [(6, 9)]
     assert _subtract((5, 10), [(10, 12), (0, 5)]) == [(5, 10)]
+
+
+def test_stale_native_library_is_rebuilt(monkeypatch):
+    """A library whose embedded source hash differs from the csrc tree's (sources edited without
+    a rebuild) is rebuilt before it is loaded, never run stale."""
+    from nnmpi_amd import _build, native
+    calls = []
+    state = {"built": "0" * 32}
+    monkeypatch.setattr(_build, "source_hash", lambda: "f" * 32)
+    monkeypatch.setattr(_build, "built_hash", lambda path="": state["built"])
+
+    def fake_build(**kw):
+        calls.append(kw)
+        state["built"] = "f" * 32
+        return _build.ext_path()
+    monkeypatch.setattr(_build, "build", fake_build)
+    native._load()
+    assert len(calls) == 1
+    native._load()          # now current: no second build
+    assert len(calls) == 1
+
+
+def test_built_library_carries_the_source_hash():
+    from nnmpi_amd import _build
+    assert _build.built_hash() == _build.source_hash()
