@@ -491,7 +491,8 @@ def test_wide_chunked_buckets_overlap_bitwise_equal():
     """8192-wide layers cut into 4 output-row chunk buckets: each chunk's weight gradient is
     its own launch, its all-reduce starts behind it on the comm stream, its SGD runs on the
     update stream -- bitwise equal to the communication-free run (SGD fused in the epilogue)."""
-    a = trainer.run_worker(_wide_cfg(comm="native", comm_mode="overlap", bucket_mb=16))
+    a = trainer.run_worker(_wide_cfg(comm="native", comm_mode="overlap", bucket_mb=16,
+                                     grad_dtype="fp32"))
     b = trainer.run_worker(_wide_cfg(comm="none"))
     assert a.losses == b.losses
     assert torch.equal(a.final_params, b.final_params)
