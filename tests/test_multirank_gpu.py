@@ -221,9 +221,11 @@ def test_rccl_bf16_reduction_error_vs_p(world):
         assert torch.equal(o["acc32"], out[0]["acc32"]) and torch.equal(o["ring_bf16"], out[0]["ring_bf16"])
     e_acc, e_ring = _rel(out[0]["acc32"], exact), _rel(out[0]["ring_bf16"], exact)
     e_f32 = _rel(out[0]["fp32"], exact)
-    # elementwise: bf16 inputs (2^-9 relative each, summed) + one output rounding (2^-9)
-    bound = (torch.stack([x.double().abs() for x in g]).sum(0) * 2.0 ** -9 +
-             exact.abs() * 2.0 ** -8 + 1e-30)
+    # elementwise: every bf16 rounding (8 significant bits) is within u = 2^-8 relative: the
+    # inputs' roundings add up to u * sum|g_r|, the output's to u * |sum| (+ second order)
+    u = 2.0 ** -8
+    bound = (torch.stack([x.double().abs() for x in g]).sum(0) * u * (1 + 2 * u) +
+             exact.abs() * u * (1 + 2 * u) + 1e-30)
     assert bool(((out[0]["acc32"].double() - exact).abs() <= bound).all())
     assert e_acc < 8e-3 and e_f32 < 1e-6
     import json
