@@ -124,9 +124,11 @@ def parse(argv=None):
                         "a 1-GPU box; the JSON line says so and its numbers are not a measurement")
     p.add_argument("--fwd_variant", type=int, default=-1, help="forward GEMM variant (experiments)")
     p.add_argument("--gemm_variant", type=int, default=0,
-                   help="GEMM main-loop variant of every launch (experiments; 19 = deep-ring 256x256)")
+                   help="GEMM main-loop variant of every launch (experiments; 19..24 = deep-ring "
+                        "256x256, needs an NNMPI_EXPERIMENTS=1 build)")
     p.add_argument("--pp_order", default="",
-                   help="256x256 GEMM tile order for fwd,dgrad,wgrad (0 GM4, 2 GM1, 3 GM8; experiments)")
+                   help="256x256 GEMM kernel for fwd,dgrad,wgrad (0 GM4, 1 row-major, 2 GM4 + one "
+                        "DMA half per phase, 3 row-major + one half per phase; experiments)")
     p.add_argument("--head_xcd_rows", type=int, default=0,
                    help="head kernels take XCD-remapped row blocks (experiments)")
     p.add_argument("--store_policy", type=int, default=0,

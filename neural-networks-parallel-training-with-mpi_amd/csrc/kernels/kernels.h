@@ -121,6 +121,8 @@ bool wide_pair_wgrad_ok(int rows, int out_f, int in_f);
 bool wide_pair_dgrad_ok(int rows, int out_f, int in_f);
 hipError_t wide_pair(const WgradArgs& w1, const DgradArgs* dg, const WgradArgs* w2, hipStream_t s);
 void set_wide_pair(int on);
+// the experiment kernels (csrc/experiments: deep ring, wide pairs, stamps) are linked in
+bool experiments_built();
 // SGD epilogue form of the un-split weight gradients and split-K combines (A/B; 0 default):
 // 0 LDS-staged rows (256x256 tiles), 1 per fragment (operands loaded after the sums), 2 fragment
 // rows batched

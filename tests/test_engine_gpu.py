@@ -434,6 +434,10 @@ def test_wide_pair_launches_bitwise_equal(width, rows):
     the last two weight gradients share a launch."""
     from nnmpi_amd import native
     lib = native.lib()
+    if not lib.experiments_built():
+        # production build: the pair kernel is not linked and every pair is refused
+        assert not lib.wide_pair_wgrad_ok(rows, width, width)
+        pytest.skip("experiment kernels not built (NNMPI_EXPERIMENTS=1)")
     cfg = _wide_cfg(widths=[width] * 4 + [1], n_features=width, n_samples=rows)
     try:
         lib.set_wide_pair(1)
@@ -445,6 +449,27 @@ def test_wide_pair_launches_bitwise_equal(width, rows):
     assert a.losses == b.losses
     assert torch.equal(a.final_params, b.final_params)
     assert a.losses[-1] == a.losses[-1]
+
+
+@pytest.mark.parametrize("width,rows", [(4096, 4096), (4000, 1000)])
+def test_pp256_one_half_per_phase_bitwise_equal(width, rows):
+    """The 256x256 kernel with one DMA half per phase (set_pp256_order 2 / 3) gives the same bits
+    as the default 1/0/2/1 placement for the forward, dgrad and weight gradient (full and ragged
+    tiles): only the issue point of B0(t+2) and the counted waits move."""
+    from nnmpi_amd import native
+    lib = native.lib()
+    cfg = _wide_cfg(widths=[width] * 4 + [1], n_features=width, n_samples=rows)
+    out = []
+    try:
+        for orders in ((0, 0, 1), (2, 2, 3)):
+            for epi, idx in enumerate(orders):
+                lib.set_pp256_order(epi, idx)
+            out.append(trainer.run_worker(cfg))
+    finally:
+        for epi, idx in enumerate((0, 0, 1)):
+            lib.set_pp256_order(epi, idx)
+    assert out[0].losses == out[1].losses
+    assert torch.equal(out[0].final_params, out[1].final_params)
 
 
 @pytest.mark.parametrize("width,rows", [(4096, 4096), (4096, 600), (4000, 1000)])
