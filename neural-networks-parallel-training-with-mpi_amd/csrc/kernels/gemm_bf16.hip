@@ -261,6 +261,20 @@ void set_fwd_variant(int v) { g_fwd_variant = v; }
 void set_group_async(int m) { g_group_async = m; }
 void set_wgrad_splits(int s) { g_wgrad_splits = s; }
 void set_store_policy(int p) { g_store_pol = p; }
+// Store policy of the split-K weight-gradient slabs alone in the grouped backward (A/B,
+// NNMPI_SLAB_STORE=<0|1|2>; -1 = the general policy above).  The slabs are read back by the NEXT
+// launch's combine from every XCD, so their dirty lines are written back at the launch boundary
+// ("boundary" row, MI355X_MICROARCH.md: + B / 6 TB/s); write-through (2 = sc1) moves that
+// traffic into the epilogue, where other CUs' main loops may hide it.
+static int g_slab_store_pol = -2;
+void set_slab_store_policy(int p) { g_slab_store_pol = p; }
+static int slab_store_pol() {
+  if (g_slab_store_pol == -2) {
+    const char* e = std::getenv("NNMPI_SLAB_STORE");
+    g_slab_store_pol = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : -1;
+  }
+  return g_slab_store_pol >= 0 ? g_slab_store_pol : g_store_pol;
+}
 
 template <int BM, int BN, int LA, int LB, int EPI, int ACT, bool BG>
 static hipError_t launch_t(GemmParams p, int splits, hipStream_t s, int variant = -1) {
@@ -654,7 +668,7 @@ hipError_t bwd_group(const DgradArgs* dg, const WgradArgs* wg, const SlabReduce*
     g.nb_bias = nb_bias;
   }
   g.dg.store_pol = g_store_pol;
-  g.wg.store_pol = g_store_pol;
+  g.wg.store_pol = splits > 1 ? slab_store_pol() : g_store_pol;
   const int nb = g.dg_blocks + g.wg_blocks + nbr;
   if (nb == 0) return hipSuccess;
   const int act = dg ? dg->act : ACT_NONE;

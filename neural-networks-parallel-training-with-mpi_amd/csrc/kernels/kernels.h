@@ -59,7 +59,8 @@ void set_gemm_variant(int v);  // DMA-path main-loop variant (experiments), 0 = 
 // step-level kernel-selection knobs (-1 / 0 = built-in default; scripts/step_ab.py)
 void set_fwd_variant(int v);   // forward GEMM (128x128 tiles) main-loop variant
 void set_pp256_order(int epi, int idx);   // 256x256 kernel tile order per epilogue (A/B)
-void set_store_policy(int p);  // LDS-epilogue output stores: 0 plain, 1 nt, 2 sc1 (experiments)
+void set_store_policy(int p);
+void set_slab_store_policy(int p);   // split-K slab stores of the grouped backward (-2: env)  // LDS-epilogue output stores: 0 plain, 1 nt, 2 sc1 (experiments)
 void set_head_xcd_rows(int v);  // head kernels: rows of XCD-remapped logical blocks (experiment)
 // diagnostic: the default 128x128 forward kernel with per-block entry/exit real-time stamps
 // (stamps: 2 * grid uint64, 100 MHz counter)

@@ -16,6 +16,10 @@ for r in 1 2; do
     step "wide $o" $?
   done
 done
+timeout -k 10 400 python scripts/step_ab.py --config proxy512 --rounds 7 --steps 128 --configs '[{}, {"slab": 2}, {"slab": 1}, {}]' > $O/proxy_slab_ab.jsonl 2> $O/proxy_slab_ab.err
+step proxy_slab_ab $?
+timeout -k 10 400 python scripts/step_ab.py --config wide8192 --rounds 3 --steps 20 --chunk 10 --configs '[{}, {"pp": "2,2,3"}, {"pp": "0,0,3"}, {"pp": "2,2,1"}]' > $O/wide_pp_ab.jsonl 2> $O/wide_pp_ab.err
+step wide_pp_ab $?
 timeout -k 10 300 python scripts/head_bench.py > $O/head.jsonl 2> $O/head.err
 step head $?
 rm -rf $O/trace_fc

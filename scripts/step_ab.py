@@ -48,6 +48,9 @@ def apply(lib, knobs):
     lib.set_fwd_variant(int(knobs.get("fwd", -1)))
     lib.set_group_async(int(knobs.get("gasync", -1)))
     lib.set_wgrad_splits(int(knobs.get("wsplit", 0)))
+    lib.set_slab_store_policy(int(knobs.get("slab", -1)))     # split-K slab stores (2 = sc1)
+    for epi, idx in enumerate(str(knobs.get("pp", "0,0,1")).split(",")):
+        lib.set_pp256_order(epi, int(idx))                    # 256x256 kernel per epilogue
 
 
 def main():
