@@ -6,6 +6,7 @@ export TMPDIR=/tmp
 O=gpurun_out/r3g
 mkdir -p $O
 step() { echo "[r3g] $1 rc=$2" | tee -a $O/summary.txt; if [ "$2" -ne 0 ]; then exit "$2"; fi; }
+if [ -z "$ONLY_TAIL" ]; then
 timeout -k 10 400 python -u -m pytest tests/test_engine_gpu.py -m gpu -v --timeout 200 --timeout-method thread -k "pp256_one_half or wide_pair or wide_sgd or test_reference_config_on_gpu" > $O/pytest.log 2>&1
 step pytest $?
 timeout -k 10 300 python scripts/gemm_bench.py --rows 4096 --inf 8192 --outf 8192 --rounds 5 --iters 5 --impls 0,2 --tiles 0 --variants 15,16,17,18 > $O/gemm_wide.jsonl 2> $O/gemm_wide.err
@@ -20,6 +21,7 @@ timeout -k 10 400 python scripts/step_ab.py --config proxy512 --rounds 7 --steps
 step proxy_slab_ab $?
 timeout -k 10 400 python scripts/step_ab.py --config wide8192 --rounds 3 --steps 20 --chunk 10 --configs '[{}, {"pp": "2,2,3"}, {"pp": "0,0,3"}, {"pp": "2,2,1"}]' > $O/wide_pp_ab.jsonl 2> $O/wide_pp_ab.err
 step wide_pp_ab $?
+fi
 timeout -k 10 300 python scripts/head_bench.py > $O/head.jsonl 2> $O/head.err
 step head $?
 rm -rf $O/trace_fc
