@@ -253,7 +253,13 @@ def supervise(a, argv, job) -> int:
         line["attempts"] = log
         line["measured_mode"] = log[-1]["mode"]
         return line
-    return s.run([cmd for _, cmd in ladder], lambda k: ladder[k][0], annotate)
+    env = {}
+    if a.shared_gpu_rehearsal:
+        # (as launch_ranks does for its own ranks: RCCL accepts two ranks on one device only if
+        # they look like different hosts)
+        env = dict(NCCL_HOSTID=f"nnmpi-rehearsal-{job.rank}", NCCL_SOCKET_IFNAME="lo",
+                   NCCL_IB_DISABLE="1")
+    return s.run([cmd for _, cmd in ladder], lambda k: ladder[k][0], annotate, env_extra=env)
 
 
 def run(a, job):

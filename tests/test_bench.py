@@ -148,6 +148,25 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
 
 
 @pytest.mark.gpu
+def test_bench_driver_torchrun_form_on_one_gpu():
+    """The driver's exact N-GPU launch (torch.distributed.run ... bench.py --gpus N) with the GPU
+    ranks sharing the one device: per-rank supervisors under torchrun's agent store, RCCL ranks,
+    one JSON line with replicas_bitwise_equal."""
+    from nnmpi_amd.parallel.dist import free_port
+    e = dict(os.environ)
+    for k in ("RANK", "WORLD_SIZE", "LOCAL_RANK", "MASTER_ADDR", "MASTER_PORT"):
+        e.pop(k, None)
+    r = subprocess.run([sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+                        "--nproc-per-node", "2", "--master-addr", "127.0.0.1", "--master-port",
+                        str(free_port()), BENCH, "--gpus", "2", "--steps", "8", "--warmup", "2",
+                        "--tune_steps", "4", "--shared_gpu_rehearsal"], capture_output=True,
+                       text=True, timeout=300, env=e)
+    d = _line(r)
+    assert d["n_gpus"] == 2 and d["rccl_ranks"] == 2 and d["replicas_bitwise_equal"] is True
+    assert d["fallback"] is None and d["attempts"][0]["result"] == "full"
+
+
+@pytest.mark.gpu
 def test_bench_gpu_rank_sigsegv_falls_back_to_inline():
     """The fallback with real GPU processes: RCCL rank 1 dies by SIGSEGV before the timed region
     (its peer holds an RCCL communicator and captured graphs); fresh ranks re-run the job with
