@@ -96,6 +96,9 @@ def parse(argv=None):
     p.add_argument("--grad_dtype", choices=["auto", "fp32", "bf16"], default="auto",
                    help="all-reduce payload (auto: bf16 above 64 MB of fp32 gradients)")
     p.add_argument("--bucket_mb", type=float, default=1.0)
+    p.add_argument("--chunk_tiles", type=int, default=0,
+                   help="256x256 weight-gradient tiles per output-row chunk bucket at least "
+                        "(0: 256 = 4 chunks per 8192-wide layer; 512: 2 chunks)")
     p.add_argument("--no_graph", action="store_true")
     p.add_argument("--no_overlap", action="store_true")
     p.add_argument("--no_group", action="store_true",
@@ -335,9 +338,10 @@ def run(a, job):
             labels = None
         return part, X.to(dtype), Y, labels
 
-    def build(mode, data, comm=True, bucket_mb=None):
+    def build(mode, data, comm=True, bucket_mb=None, chunk_tiles=0):
         """One arena + gradient-sync strategy + engine over ``data`` (a shard()).
-        mode: inline | overlap | zero1 | none (no gradient synchronisation at all)."""
+        mode: inline | overlap | zero1 | none (no gradient synchronisation at all);
+        chunk_tiles: 256x256 tiles per output-row chunk bucket at least (0: the default)."""
         part, X, Y, labels = data
         rows = part.rows(rank)
         model = reference_init(widths, "relu", seed=0, device=dev if (big and gpu) else None)
@@ -345,7 +349,7 @@ def run(a, job):
         arena = Arena([spec.layer_shape(i) for i in range(spec.n_layers)], dev,
                       shadow_dtype=torch.bfloat16 if dtype == torch.bfloat16 else None,
                       bucket_bytes=(bucket_mb or a.bucket_mb) * 2 ** 20,
-                      pad_to=64 * world if zero1 else 64)
+                      pad_to=64 * world if zero1 else 64, chunk_min_tiles=chunk_tiles)
         arena.bind_model(model)
         del model
         if not comm or not use_comm:
@@ -462,6 +466,7 @@ def run(a, job):
 
     tune = None
     bucket_mb = a.bucket_mb
+    chunk_tiles = a.chunk_tiles
     if mode == "tune":
         tune = {}
         eng = None
@@ -469,14 +474,18 @@ def run(a, job):
         # larger, the exposed last one smaller than the whole gradient)
         half_mb = round(grad_bytes / 2 ** 20 * 0.6, 3)
         if grad_bytes > INLINE_MAX_GRAD_BYTES:
-            cands = [("overlap", a.bucket_mb), ("inline", None), ("zero1", None)]
+            # overlap with 4 chunk buckets per 8192-wide layer (one 256-tile wave each: the
+            # earliest collective start) and with 2 (half the launches and cross-queue waits,
+            # twice the exposed last collective); measured at one rank: docs/PERF.md
+            cands = [("overlap", a.bucket_mb), ("overlap_c2", a.bucket_mb), ("inline", None),
+                     ("zero1", None)]
         else:
             cands = [("inline", None), ("zero1", None), ("overlap", a.bucket_mb)]
             if half_mb > a.bucket_mb:
                 cands.append(("overlap", half_mb))
         for m, bmb in cands:
             milestone(f"tune {m}")
-            e = build(m, data, bucket_mb=bmb)
+            e = build(m.split("_c")[0], data, bucket_mb=bmb, chunk_tiles=512 if m.endswith("_c2") else 0)
             e.run_steps(a.warmup, chunk_for(a.warmup))
             tm = min(timed(e, a.tune_steps, chunk_for(a.tune_steps)) for _ in range(2))
             key = m if bmb in (None, a.bucket_mb) else f"{m}_{bmb}mb"
@@ -484,6 +493,7 @@ def run(a, job):
             # every rank sees the same max-over-ranks times, so every rank keeps the same mode
             if eng is None or tm < best_t:
                 eng, best_t, mode, bucket_mb = e, tm, m, (bmb or a.bucket_mb)
+                chunk_tiles = 512 if m.endswith("_c2") else 0
             del e
         if gpu:
             torch.cuda.empty_cache()
@@ -491,7 +501,7 @@ def run(a, job):
         # the tuning runs themselves)
         warm(eng, a.warmup)
     else:
-        eng = build(mode, data)
+        eng = build(mode, data, chunk_tiles=a.chunk_tiles)
         warm(eng, a.warmup)
 
     # ---------------- the timed region: exactly K steps -------------------------------------
@@ -513,6 +523,8 @@ def run(a, job):
     ms = elapsed / a.steps * 1e3
     value = n_global * a.steps / elapsed
     sharded = mode == "zero1"
+    mode_name = mode
+    mode = mode.split("_c")[0]
     n_buckets = len(eng.arena.buckets)
     wire = comm_volume(eng.arena.numel, world, grad_dtype, sharded=sharded,
                        shadow=eng.arena.shadow is not None)["wire_bytes_per_rank"]
@@ -582,7 +594,8 @@ def run(a, job):
             # proxy) split over the N ranks
             nonlocal strong
             sdata = shard(rows_pg)
-            e = build(mode if mode != "none" else "inline", sdata, bucket_mb=bucket_mb)
+            e = build(mode if mode != "none" else "inline", sdata, bucket_mb=bucket_mb,
+                      chunk_tiles=chunk_tiles)
             e.run_steps(min(a.warmup, 10) + 1, chunk_for(min(a.warmup, 10)))
             s_ms = timed(e, n_ex, chunk_for(n_ex)) / n_ex * 1e3
             comp_ms = res["comp_ms"]
@@ -645,7 +658,7 @@ def run(a, job):
                                 if use_comm else "none"),
                        "graph": gpu and not a.no_graph, "graph_chunk": chunk,
                        "overlap": not a.no_overlap, "grouped": not a.no_group,
-                       "comm_mode": mode if use_comm else None,
+                       "comm_mode": mode_name if use_comm else None,
                        "comm_tune_ms_per_step": tune,
                        "grad_dtype": grad_dtype if use_comm else None,
                        "grad_wire_bytes_per_rank": wire,
@@ -747,12 +760,12 @@ def replica_digest(eng, gpu: bool) -> str:
     if gpu:
         from nnmpi_amd import native
         torch.cuda.synchronize()
-        out = torch.zeros(len(bufs), 257, dtype=torch.int64, device=ar.master.device)
+        out = torch.zeros(len(bufs), 1025, dtype=torch.int64, device=ar.master.device)
         s = torch.cuda.current_stream()
         for k, b in enumerate(bufs):
             nbytes = b.numel() * b.element_size()
             native.lib().hash_u32(b.data_ptr(), nbytes // 4, out[k].data_ptr(), int(s.cuda_stream))
-        vals = out[:, 256].cpu().tolist()
+        vals = out[:, 1024].cpu().tolist()
         return "-".join(f"{v & 0xFFFFFFFFFFFFFFFF:016x}" for v in vals)
     import hashlib
     h = hashlib.sha256()

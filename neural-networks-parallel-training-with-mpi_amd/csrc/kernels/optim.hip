@@ -225,7 +225,7 @@ hipError_t sum_slices_bf16(bf16* out, const bf16* scratch, int P, int me, long l
 // A value sum (checksum_f32) can coincide for different bits (-0.0 vs 0.0, compensating
 // errors); this one changes with any flipped bit of any word, and integer addition makes the
 // result independent of the reduction order.  HASH_BLOCKS partials, then one block sums them.
-constexpr int HASH_BLOCKS = 256;
+constexpr int HASH_BLOCKS = 1024;
 
 __device__ __forceinline__ unsigned long long mix64(unsigned long long z) {
   z = (z ^ (z >> 30)) * 0xbf58476d1ce4e5b9ull;
@@ -238,7 +238,28 @@ __global__ void __launch_bounds__(256) hash_u32_kernel(const unsigned* __restric
   __shared__ unsigned long long red[256];
   unsigned long long h = 0;
   const long long stride = (long long)gridDim.x * blockDim.x;
-  for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n; i += stride)
+  const long long t0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  // 16-byte loads, two in flight per lane (the callers' buffers are 16-byte aligned), then the
+  // scalar tail
+  const bool vec = (((uintptr_t)x) & 15) == 0;
+  const long long n4 = vec ? n / 4 : 0;
+  long long q = t0;
+  for (; q + stride < n4; q += 2 * stride) {
+    const uint4 a = reinterpret_cast<const uint4*>(x)[q];
+    const uint4 b = reinterpret_cast<const uint4*>(x)[q + stride];
+    const unsigned long long i = (unsigned long long)(4 * q), j = (unsigned long long)(4 * (q + stride));
+    h += mix64((i << 32) | a.x) + mix64(((i + 1) << 32) | a.y) + mix64(((i + 2) << 32) | a.z) +
+         mix64(((i + 3) << 32) | a.w);
+    h += mix64((j << 32) | b.x) + mix64(((j + 1) << 32) | b.y) + mix64(((j + 2) << 32) | b.z) +
+         mix64(((j + 3) << 32) | b.w);
+  }
+  for (; q < n4; q += stride) {
+    const uint4 a = reinterpret_cast<const uint4*>(x)[q];
+    const unsigned long long i = (unsigned long long)(4 * q);
+    h += mix64((i << 32) | a.x) + mix64(((i + 1) << 32) | a.y) + mix64(((i + 2) << 32) | a.z) +
+         mix64(((i + 3) << 32) | a.w);
+  }
+  for (long long i = n4 * 4 + t0; i < n; i += stride)
     h += mix64(((unsigned long long)i << 32) | x[i]);
   red[threadIdx.x] = h;
   __syncthreads();
@@ -251,21 +272,23 @@ __global__ void __launch_bounds__(256) hash_u32_kernel(const unsigned* __restric
 
 __global__ void __launch_bounds__(256) hash_final_kernel(const unsigned long long* __restrict__ part,
                                                          unsigned long long* __restrict__ out) {
-  __shared__ unsigned long long red[HASH_BLOCKS];
-  red[threadIdx.x] = part[threadIdx.x];
+  __shared__ unsigned long long red[256];
+  unsigned long long h = 0;
+  for (int i = threadIdx.x; i < HASH_BLOCKS; i += 256) h += part[i];
+  red[threadIdx.x] = h;
   __syncthreads();
-  for (int o = HASH_BLOCKS / 2; o > 0; o >>= 1) {
+  for (int o = 128; o > 0; o >>= 1) {
     if ((int)threadIdx.x < o) red[threadIdx.x] += red[threadIdx.x + o];
     __syncthreads();
   }
   if (threadIdx.x == 0) *out = red[0];
 }
 
-// out must hold HASH_BLOCKS + 1 uint64 (partials + the result at out[HASH_BLOCKS]).
+// out must hold HASH_BLOCKS + 1 = 1025 uint64 (partials + the result at out[HASH_BLOCKS]).
 hipError_t hash_u32(const unsigned* x, long long n, unsigned long long* out, hipStream_t s) {
   if (n < 0) return hipErrorInvalidValue;
   hipLaunchKernelGGL(hash_u32_kernel, dim3(HASH_BLOCKS), dim3(256), 0, s, x, n, out);
-  hipLaunchKernelGGL(hash_final_kernel, dim3(1), dim3(HASH_BLOCKS), 0, s, out, out + HASH_BLOCKS);
+  hipLaunchKernelGGL(hash_final_kernel, dim3(1), dim3(256), 0, s, out, out + HASH_BLOCKS);
   return hipGetLastError();
 }
 

@@ -60,11 +60,14 @@ CHUNK_TILE = 256
 CHUNK_MIN_TILES = 256
 
 
-def row_chunks(out_f: int, in_f: int, grad_bytes: int, bucket_bytes: float) -> int:
+def row_chunks(out_f: int, in_f: int, grad_bytes: int, bucket_bytes: float,
+               min_tiles: int = 0) -> int:
     if grad_bytes <= bucket_bytes or out_f % CHUNK_TILE or in_f % CHUNK_TILE:
         return 1
-    # (NNMPI_CHUNK_MIN_TILES: tests exercise the chunked schedule on small layers)
-    min_tiles = int(os.environ.get("NNMPI_CHUNK_MIN_TILES", CHUNK_MIN_TILES))
+    # min_tiles: tiles per chunk at least (0: NNMPI_CHUNK_MIN_TILES, else CHUNK_MIN_TILES; tests
+    # exercise the chunked schedule on small layers, bench.py tunes 2 vs 4 chunks per layer)
+    if min_tiles <= 0:
+        min_tiles = int(os.environ.get("NNMPI_CHUNK_MIN_TILES", CHUNK_MIN_TILES))
     c = 1
     while (out_f % (2 * c * CHUNK_TILE) == 0 and
            (out_f // (2 * c * CHUNK_TILE)) * (in_f // CHUNK_TILE) >= min_tiles):
@@ -75,7 +78,7 @@ def row_chunks(out_f: int, in_f: int, grad_bytes: int, bucket_bytes: float) -> i
 class Arena:
     def __init__(self, layer_shapes: List[Tuple[int, int]], device, shadow_dtype=None,
                  bucket_bytes: float = 25 * 2 ** 20, grad_elem_bytes: int = 4, pad_to: int = ALIGN,
-                 chunk_layers: bool = True):
+                 chunk_layers: bool = True, chunk_min_tiles: int = 0):
         """``pad_to``: the total length is rounded up to this multiple (a multiple of ALIGN) --
         the sharded optimizer uses ``world * ALIGN`` so every rank owns an equal, aligned shard.
         ``chunk_layers``: cut layers larger than a bucket into output-row chunk buckets."""
@@ -104,7 +107,8 @@ class Arena:
         self.layer_chunks: Dict[int, int] = {}
         if chunk_layers:
             for li, (out_f, in_f) in enumerate(layer_shapes):
-                c = row_chunks(out_f, in_f, out_f * in_f * grad_elem_bytes, bucket_bytes)
+                c = row_chunks(out_f, in_f, out_f * in_f * grad_elem_bytes, bucket_bytes,
+                               chunk_min_tiles)
                 if c > 1:
                     self.layer_chunks[li] = c
         self.buckets = self._plan_buckets(bucket_bytes, grad_elem_bytes)

@@ -138,6 +138,10 @@ class MLPEngine:
                     if b.rows in nxt:
                         self._defer_plan[b.index] = nxt[b.rows]
         self._defer_targets = {b.index for b in self._defer_plan.values()}
+        # NNMPI_DEFER_WAIT=chunk: every deferred update waits on its own partner's collective
+        # (default: one wait per partner layer, see _defer_update)
+        self._defer_wait_layer = os.environ.get("NNMPI_DEFER_WAIT", "layer") != "chunk"
+        self._waited = set()
         self.ev_ar = ({b.index: torch.cuda.Event(enable_timing=False)
                        for b in self._defer_plan.values()} if self._defer_plan else {})
         self.rows = 0
@@ -323,7 +327,19 @@ class MLPEngine:
             return False
         self._pending_sgd.pop(k)
         ar, main = self.arena, self.stream
-        main.wait_event(self.ev_ar[part.index])      # the partner's all-reduce has completed
+        if self._defer_wait_layer:
+            # ONE cross-queue wait per layer: on the collective of the partner layer's last
+            # chunk (the comm stream runs its collectives in order, so all earlier chunks of that
+            # layer are reduced too) -- issued a whole dgrad earlier, so already complete unless
+            # the links are slower than a dgrad; every cross-queue edge in a replayed graph costs
+            # 5-10 us whether or not its event has completed (docs/PERF.md)
+            li = part.layers[0]
+            if li not in self._waited:
+                last = max(b.index for b in ar.chunk_buckets(li))
+                main.wait_event(self.ev_ar[last])
+                self._waited.add(li)
+        else:
+            main.wait_event(self.ev_ar[part.index])      # the partner's all-reduce has completed
         woff = ar.by_name[f"layers.{2 * (i + 1)}.weight"].offset + part.rows[0] * in_f
         self.ops.linear_wgrad_defer(dz, x_in, ar.weight(i, g16)[r0:r1], ar.bias(i, g16)[r0:r1],
                                     ar, self.hp, self.nesterov, self._first, woff, g16)
@@ -397,6 +413,7 @@ class MLPEngine:
         self._reduced = {}
         self._pending_sgd = []
         self._written16 = []
+        self._waited = set()
         self._first = first
         x = self.X[:rows]
         h = self._forward(x)

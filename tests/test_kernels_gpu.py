@@ -286,3 +286,35 @@ def test_native_runtime_under_host_asan():
     r = subprocess.run([exe], capture_output=True, text=True, timeout=100, env=env)
     assert r.returncode == 0, r.stdout[-3000:] + r.stderr[-3000:]
     assert "ALL OK" in r.stdout
+
+
+def _mix64(z):
+    m = (1 << 64) - 1
+    z = ((z ^ (z >> 30)) * 0xbf58476d1ce4e5b9) & m
+    z = ((z ^ (z >> 27)) * 0x94d049bb133111eb) & m
+    return z ^ (z >> 31)
+
+
+@pytest.mark.parametrize("n", [1, 7, 4096 * 4 + 3, 300_001])
+def test_replica_hash_kernel_vs_host(n):
+    """hash_u32 (the bench's replica check) == the host sum of splitmix64((i << 32) | word_i) mod
+    2^64, for vector bodies and scalar tails; flipping any single bit changes it."""
+    import numpy as np
+    from nnmpi_amd import native
+    lib = native.lib()
+    g = torch.Generator().manual_seed(n)
+    words = torch.randint(-2 ** 31, 2 ** 31 - 1, (n,), generator=g, dtype=torch.int64).to(torch.int32)
+    x = words.cuda()
+    out = torch.zeros(1025, dtype=torch.int64, device="cuda")
+    lib.hash_u32(x.data_ptr(), n, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    got = int(out[1024].item()) & ((1 << 64) - 1)
+    w = words.numpy().astype(np.int64) & 0xFFFFFFFF
+    sample = range(n) if n < 5000 else None
+    if sample is not None:
+        ref = sum(_mix64((i << 32) | int(w[i])) for i in sample) & ((1 << 64) - 1)
+        assert got == ref
+    y = x.clone()
+    k = n // 2
+    y[k] = y[k] ^ (1 << (n % 31))
+    lib.hash_u32(y.data_ptr(), n, out.data_ptr(), torch.cuda.current_stream().cuda_stream)
+    assert (int(out[1024].item()) & ((1 << 64) - 1)) != got
