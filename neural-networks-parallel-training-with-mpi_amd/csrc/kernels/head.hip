@@ -743,14 +743,15 @@ __global__ void __launch_bounds__(64 * HWM_WAVES) head_wgrad_mfma_kernel(
   const int r = lane & 15, g = lane >> 4;
   const int c0 = blockIdx.x * HWM_COLS;
   const int split = blockIdx.y;
+  const int o0 = blockIdx.z * 16;           // output tile (heads wider than 16 outputs)
   const int s0 = split * rows_per_split;
   const int s1 = min(rows, s0 + rows_per_split);
   const int q = (s1 - s0 + HWM_WAVES - 1) / HWM_WAVES;
   const int r0 = s0 + w * q;
   const int r1 = min(s1, r0 + q);
   const int cc = min(c0 + 8 * r, in - 8);   // clamped column group (in % 8 == 0)
-  const int oc = min(r, out - 1);
-  const bool o_ok = r < out;
+  const int oc = min(o0 + r, out - 1);
+  const bool o_ok = o0 + r < out;
   f32x4 acc[8];
 #pragma unroll
   for (int t = 0; t < 8; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
@@ -786,7 +787,7 @@ __global__ void __launch_bounds__(64 * HWM_WAVES) head_wgrad_mfma_kernel(
   if (g == 0) cbias[w * 16 + r] = bsum;
   __syncthreads();
   const int o = threadIdx.x >> 4, c8 = (threadIdx.x & 15) * 8;
-  if (o < out && c0 + c8 < in) {
+  if (o0 + o < out && c0 + c8 < in) {
     const float* src = cmb + o * HWM_COLS + c8;
     f32x4 t0 = *reinterpret_cast<const f32x4*>(src), t1 = *reinterpret_cast<const f32x4*>(src + 4);
 #pragma unroll
@@ -794,15 +795,15 @@ __global__ void __launch_bounds__(64 * HWM_WAVES) head_wgrad_mfma_kernel(
       t0 += *reinterpret_cast<const f32x4*>(src + ww * 16 * HWM_COLS);
       t1 += *reinterpret_cast<const f32x4*>(src + ww * 16 * HWM_COLS + 4);
     }
-    float* dst = ws + ((long long)split * out + o) * in + c0 + c8;
+    float* dst = ws + ((long long)split * out + o0 + o) * in + c0 + c8;
     *reinterpret_cast<f32x4*>(dst) = t0;
     *reinterpret_cast<f32x4*>(dst + 4) = t1;
   }
-  if (blockIdx.x == 0 && threadIdx.x < out) {
+  if (blockIdx.x == 0 && threadIdx.x < 16 && o0 + (int)threadIdx.x < out) {
     float t = cbias[threadIdx.x];
 #pragma unroll
     for (int ww = 1; ww < HWM_WAVES; ++ww) t += cbias[ww * 16 + threadIdx.x];
-    wsb[(long long)split * out + threadIdx.x] = t;
+    wsb[(long long)split * out + o0 + threadIdx.x] = t;
   }
 }
 
@@ -810,7 +811,7 @@ static bool head_wgrad_use_mfma(int out) { return out > 1; }
 
 static int head_splits(int rows, int in, int out) {
   const int cols = head_wgrad_use_mfma(out) ? HWM_COLS : 512;
-  const int gx = (in + cols - 1) / cols;
+  const int gx = (in + cols - 1) / cols * (head_wgrad_use_mfma(out) ? (out + 15) / 16 : 1);
   int s = std::max(1, 256 / gx);
   s = std::min(s, std::max(1, rows / 64));
   return s;
@@ -821,16 +822,243 @@ size_t head_wgrad_workspace_bytes(int rows, int in, int out) {
   return (size_t)s * ((size_t)out * in + out) * sizeof(float);
 }
 
+
+// ------------------------------------------------------------------------------------------
+// General head on the matrix cores (bf16 activations, in % 256 == 0, out <= 128): the path for
+// heads whose fp32 weight image does not fit the skinny kernel's LDS (e.g. 8192 -> 10) or with
+// more than 16 outputs (e.g. 1024 -> 100).  Three stages instead of head_general.hip's four VALU
+// launches (1332 us for 4096 x 8192 -> 10, profiles/r3_head_general_vs_skinny_vs_torch.jsonl):
+//   1. head_logits_stream_kernel: logits on v_mfma_f32_16x16x4_f32 (exact fp32 products and
+//      sums of the bf16 activations and the fp32 weights, fixed order), W streamed from L2
+//      (every block re-reads it; a 16-row group reads NT x 16 x in floats), loss and dlogits in
+//      registers -> dl (fp32, for the weight gradient) and a bf16 copy padded to outp columns;
+//   2. dZ_prev = (dl . W) * act'(a): the bf16 dgrad GEMM (gemm_bf16.hip, K = out) on the bf16
+//      dl copy and a bf16 image of W -- the same rounding as every hidden layer's dgrad;
+//   3. gW, gb: head_wgrad's fp32 MFMA kernel in 16-output tiles + the deterministic reducer
+//      (the loss partials fold in there).
+// ------------------------------------------------------------------------------------------
+constexpr int HS_WAVES = 4;
+constexpr int HS_MAX_NT = 8;   // outputs <= 128
+
+template <int LOSS, int NT>
+__global__ void __launch_bounds__(64 * HS_WAVES) head_logits_stream_kernel(
+    const bf16* __restrict__ a, int rows, int in, const float* __restrict__ W,
+    const float* __restrict__ b, int out, const float* __restrict__ y,
+    const int64_t* __restrict__ labels, float inv_count, float* __restrict__ dl,
+    bf16* __restrict__ dl16, int outp, float* __restrict__ loss_part) {
+  __shared__ f32x4 part[HS_WAVES * NT * 64];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int r = lane & 15, g = lane >> 4;
+  const int Q = in / HS_WAVES;               // this wave's quarter of the features
+  const int ngroups = (rows + 15) / 16;
+  constexpr int U = NT <= 4 ? 2 : 1;         // 32-feature chunks per iteration (registers)
+  // weight rows of this lane's A operand: n = 16 t + r (clamped, masked)
+  const float* wrow[NT];
+  float wmask[NT];
+#pragma unroll
+  for (int t = 0; t < NT; ++t) {
+    wrow[t] = W + (long long)min(16 * t + r, out - 1) * in;
+    wmask[t] = (16 * t + r) < out ? 1.f : 0.f;
+  }
+  float block_loss = 0.f;
+  for (int grp = blockIdx.x; grp < ngroups; grp += gridDim.x) {
+    const int row = grp * 16 + r;
+    const bool valid = row < rows;
+    const bf16* ar = a + (long long)min(row, rows - 1) * in + w * Q + 8 * g;
+    f32x4 acc[NT];
+#pragma unroll
+    for (int t = 0; t < NT; ++t) acc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+    for (int c = 0; c < Q; c += 32 * U) {    // every load of the step before its MFMAs
+      bf16x8 xv[U];
+      f32x4 wv[U][NT][2];
+#pragma unroll
+      for (int u = 0; u < U; ++u) {
+        xv[u] = *reinterpret_cast<const bf16x8*>(ar + c + 32 * u);
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+          const float* wp = wrow[t] + w * Q + c + 32 * u + 8 * g;
+          wv[u][t][0] = *reinterpret_cast<const f32x4*>(wp) * wmask[t];
+          wv[u][t][1] = *reinterpret_cast<const f32x4*>(wp + 4) * wmask[t];
+        }
+      }
+#pragma unroll
+      for (int u = 0; u < U; ++u)
+#pragma unroll
+        for (int t = 0; t < NT; ++t) {
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[u][t][0][e], (float)xv[u][e], acc[t], 0, 0, 0);
+#pragma unroll
+          for (int e = 0; e < 4; ++e)
+            acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[u][t][1][e], (float)xv[u][e + 4], acc[t], 0, 0, 0);
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < NT; ++t) part[(w * NT + t) * 64 + lane] = acc[t];
+    __syncthreads();
+    if (w == 0) {
+      // lane (r, g) holds the logits of row r, outputs 16 t + 4 g + j (wave order sums)
+      float z[NT][4];
+#pragma unroll
+      for (int t = 0; t < NT; ++t) {
+        f32x4 v = part[t * 64 + lane];
+#pragma unroll
+        for (int ww = 1; ww < HS_WAVES; ++ww) v += part[(ww * NT + t) * 64 + lane];
+#pragma unroll
+        for (int j = 0; j < 4; ++j) {
+          const int n = 16 * t + 4 * g + j;
+          z[t][j] = v[j] + (n < out ? b[n] : 0.f);
+        }
+      }
+      float d[NT][4];
+      float row_loss = 0.f;
+      if constexpr (LOSS == LOSS_XENT) {
+        float mx = -INFINITY;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (16 * t + 4 * g + j < out) mx = fmaxf(mx, z[t][j]);
+        mx = fmaxf(mx, __shfl_xor(mx, 16, 64));
+        mx = fmaxf(mx, __shfl_xor(mx, 32, 64));
+        float se = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j)
+            if (16 * t + 4 * g + j < out) se += __expf(z[t][j] - mx);
+        se += __shfl_xor(se, 16, 64);
+        se += __shfl_xor(se, 32, 64);
+        const float lse = mx + __logf(se);
+        const int lab = (int)labels[min(row, rows - 1)];
+        float picked = 0.f;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int n = 16 * t + 4 * g + j;
+            if (n == lab) picked = z[t][j];
+            d[t][j] = (n < out && valid) ? (__expf(z[t][j] - lse) - (n == lab ? 1.f : 0.f)) * inv_count : 0.f;
+          }
+        picked += __shfl_xor(picked, 16, 64);
+        picked += __shfl_xor(picked, 32, 64);
+        row_loss = lse - picked;
+      } else {
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int n = 16 * t + 4 * g + j;
+            const float dd = n < out ? z[t][j] - y[(long long)min(row, rows - 1) * out + min(n, out - 1)] : 0.f;
+            row_loss += dd * dd;
+            d[t][j] = valid ? 2.f * dd * inv_count : 0.f;
+          }
+        row_loss += __shfl_xor(row_loss, 16, 64);
+        row_loss += __shfl_xor(row_loss, 32, 64);
+      }
+      if (valid) {
+        if (g == 0) block_loss += row_loss;
+#pragma unroll
+        for (int t = 0; t < NT; ++t)
+#pragma unroll
+          for (int j = 0; j < 4; ++j) {
+            const int n = 16 * t + 4 * g + j;
+            if (n < out) dl[(long long)row * out + n] = d[t][j];
+            if (n < outp) dl16[(long long)row * outp + n] = (bf16)d[t][j];
+          }
+      }
+    }
+    __syncthreads();   // part[] is rewritten by the next group
+  }
+  if (w == 0) {
+    const float t = wave_sum(block_loss);
+    if (lane == 0) loss_part[blockIdx.x] = t;
+  }
+}
+
+bool head_general_mfma_ok(int a_bf16, int in, int out) {
+  // (each wave's quarter of the features is walked in 64-feature steps)
+  return a_bf16 && in % 256 == 0 && out >= 1 && out <= 16 * HS_MAX_NT;
+}
+
+static int hs_outp(int out) { return (out + 7) / 8 * 8; }
+static int hs_blocks(int rows) { return std::max(1, std::min(1024, (rows + 15) / 16)); }
+
+// workspace (floats): dl [rows*out] | dl16 [rows*outp bf16] | W16 [out*in bf16] | loss partials |
+// head_wgrad workspace
+size_t head_general_mfma_workspace_bytes(int rows, int in, int out) {
+  const size_t f = (size_t)rows * out + ((size_t)rows * hs_outp(out) + 1) / 2 + 4 +
+                   ((size_t)out * in + 1) / 2 + 4 + hs_blocks(rows) + 4;
+  return (f + 64) * sizeof(float) + head_wgrad_workspace_bytes(rows, in, out);
+}
+
+hipError_t head_general_mfma(const bf16* a, int rows, int in, const float* W, const float* b,
+                             int out, const float* y, const int64_t* labels, int loss,
+                             float inv_count, int act_prev, bf16* dz_out, float* gW, float* gb,
+                             float* dlogits_out, float* ws, float loss_scale, float* loss_out,
+                             hipStream_t s) {
+  if (!head_general_mfma_ok(1, in, out) || rows < 1) return hipErrorInvalidValue;
+  const int outp = hs_outp(out), nb = hs_blocks(rows);
+  auto align16 = [](float* p) {
+    return reinterpret_cast<float*>((reinterpret_cast<uintptr_t>(p) + 15) & ~uintptr_t(15));
+  };
+  float* dl = dlogits_out ? dlogits_out : ws;
+  float* cur = align16(ws + (size_t)rows * out);
+  bf16* dl16 = reinterpret_cast<bf16*>(cur);
+  cur = align16(cur + ((size_t)rows * outp + 1) / 2);
+  bf16* W16 = reinterpret_cast<bf16*>(cur);
+  cur = align16(cur + ((size_t)out * in + 1) / 2);
+  float* lpart = cur;
+  float* wws = align16(lpart + nb);
+  // the padding columns of the bf16 dl copy stay zero (the dgrad GEMM reads 8-wide chunks)
+  if (outp != out) {
+    hipError_t e = hipMemsetAsync(dl16, 0, (size_t)rows * outp * sizeof(bf16), s);
+    if (e != hipSuccess) return e;
+  }
+  const int nt = (out + 15) / 16;
+#define HS_LAUNCH(L, NT)                                                                          \
+  hipLaunchKernelGGL((head_logits_stream_kernel<L, NT>), dim3(nb), dim3(64 * HS_WAVES), 0, s, a, \
+                     rows, in, W, b, out, y, labels, inv_count, dl, dl16, outp, lpart)
+#define HS_NT(L)                                                                                  \
+  switch (nt) {                                                                                   \
+    case 1: HS_LAUNCH(L, 1); break;                                                               \
+    case 2: HS_LAUNCH(L, 2); break;                                                               \
+    case 3: HS_LAUNCH(L, 3); break;                                                               \
+    case 4: HS_LAUNCH(L, 4); break;                                                               \
+    case 5: HS_LAUNCH(L, 5); break;                                                               \
+    case 6: HS_LAUNCH(L, 6); break;                                                               \
+    case 7: HS_LAUNCH(L, 7); break;                                                               \
+    default: HS_LAUNCH(L, 8); break;                                                              \
+  }
+  if (loss == LOSS_XENT) { HS_NT(LOSS_XENT) } else { HS_NT(LOSS_MSE) }
+#undef HS_NT
+#undef HS_LAUNCH
+  hipError_t e = hipGetLastError();
+  if (e != hipSuccess) return e;
+  if (dz_out) {
+    e = cast_f32_bf16(W, W16, (long long)out * in, s);
+    if (e != hipSuccess) return e;
+    // dZ[rows][in] = dl16[rows][out] . W16[out][in] * act'(a): K = out, lda = outp
+    e = linear_dgrad_bf16(dl16, outp, W16, in, a, in, dz_out, in, rows, in, out, act_prev, s);
+    if (e != hipSuccess) return e;
+  }
+  return head_wgrad(a, 1, rows, in, dl, out, gW, gb, wws, lpart, nb, loss_scale, loss_out, s,
+                    nullptr, nullptr);
+}
+
 hipError_t head_wgrad(const void* a, int a_bf16, int rows, int in, const float* dlogits, int out,
                       float* gW, float* gb, float* ws, const float* loss_part, int n_loss_part,
                       float loss_scale, float* loss_out, hipStream_t s, const SgdFuse* sgd,
                       SlabReduce* pending) {
-  if (out < 1 || out > HEAD_OMAX || in % 8 != 0 || rows < 1) return hipErrorInvalidValue;
+  // (more than 16 outputs: the MFMA kernel in 16-output tiles, grid z)
+  if (out < 1 || (out > HEAD_OMAX && !head_wgrad_use_mfma(out)) || in % 8 != 0 || rows < 1)
+    return hipErrorInvalidValue;
   const int S = head_splits(rows, in, out);
   const int rps = (rows + S - 1) / S;
   float* wsb = ws + (size_t)S * out * in;
   if (head_wgrad_use_mfma(out)) {
-    const dim3 grid((in + HWM_COLS - 1) / HWM_COLS, S), blk(64 * HWM_WAVES);
+    const dim3 grid((in + HWM_COLS - 1) / HWM_COLS, S, (out + 15) / 16), blk(64 * HWM_WAVES);
     if (a_bf16) hipLaunchKernelGGL(head_wgrad_mfma_kernel<bf16>, grid, blk, 0, s, reinterpret_cast<const bf16*>(a), rows, in, dlogits, out, rps, ws, wsb);
     else hipLaunchKernelGGL(head_wgrad_mfma_kernel<float>, grid, blk, 0, s, reinterpret_cast<const float*>(a), rows, in, dlogits, out, rps, ws, wsb);
   } else {

@@ -3,7 +3,9 @@
 // kernels do not take (out > 16, or an fp32 weight image over 64 KiB of LDS: e.g. 8192 -> 10
 // cross-entropy, 8192 -> 3 regression, 1024 -> 100 classes).
 //
-// Four launches, all fp32 math with a fixed summation order (deterministic):
+// bf16 activations with in % 256 == 0 and out <= 128 take the matrix-core path of head.hip
+// (head_general_mfma); everything else runs the four fp32 VALU launches below (fixed summation
+// order, deterministic):
 //   1. logits[r][o] = b[o] + sum_k a[r][k] W[o][k]          64x64 register-tiled SGEMM (LDS, K
 //                                                             chunks of 32, 4x4 outputs/thread)
 //   2. per row: loss, dl = dL/dlogits * inv_count (in place) one wave per row, any width
@@ -264,12 +266,19 @@ static int hg_splits(int rows, int out, int in) {
 
 static int hg_loss_blocks(int rows) { return (rows + HG_LOSS_ROWS - 1) / HG_LOSS_ROWS; }
 
+// 1: bf16 heads also take the VALU path below instead of head.hip's matrix-core path (A/B)
+static int g_head_general_valu = 0;
+void set_head_general_valu(int on) { g_head_general_valu = on; }
+
 // workspace: logits/dl [rows*out] | loss partials | gW partials [S*out*in] | gb partials [S*out]
 size_t head_general_workspace_bytes(int rows, int in, int out) {
   const int S = hg_splits(rows, out, in);
   const size_t n = (size_t)rows * out + hg_loss_blocks(rows) + 64 + (size_t)S * out * in +
                    (size_t)S * out + 64;
-  return n * sizeof(float);
+  // (either path: the matrix-core path of head.hip for bf16 activations, this one otherwise)
+  return std::max(n * sizeof(float),
+                  head_general_mfma_ok(1, in, out) ? head_general_mfma_workspace_bytes(rows, in, out)
+                                                   : (size_t)0);
 }
 
 hipError_t head_general(const void* a, int a_bf16, int rows, int in, const float* W, const float* b,
@@ -277,6 +286,10 @@ hipError_t head_general(const void* a, int a_bf16, int rows, int in, const float
                         int act_prev, void* dz_out, float* gW, float* gb, float* dlogits_out,
                         float* ws, float loss_scale, float* loss_out, hipStream_t s) {
   if (rows <= 0 || in <= 0 || out <= 0) return hipErrorInvalidValue;
+  if (head_general_mfma_ok(a_bf16, in, out) && !g_head_general_valu)
+    return head_general_mfma(static_cast<const bf16*>(a), rows, in, W, b, out, y, labels, loss,
+                             inv_count, act_prev, static_cast<bf16*>(dz_out), gW, gb, dlogits_out,
+                             ws, loss_scale, loss_out, s);
   const int S = hg_splits(rows, out, in);
   const int nl = hg_loss_blocks(rows);
   float* z = ws;

@@ -164,6 +164,15 @@ hipError_t head_fused(const void* a, int a_bf16, int rows, int in, const float* 
                       float* gb, float* ws, float* loss_part, float loss_scale, float* loss_out,
                       hipStream_t s, const SgdFuse* sgd = nullptr, SlabReduce* pending = nullptr);
 size_t head_wgrad_workspace_bytes(int rows, int in, int out);
+// General head on the matrix cores (head.hip): bf16 activations, in % 256 == 0, out <= 128
+bool head_general_mfma_ok(int a_bf16, int in, int out);
+void set_head_general_valu(int on);   // 1: the VALU general head for bf16 heads too (A/B)
+size_t head_general_mfma_workspace_bytes(int rows, int in, int out);
+hipError_t head_general_mfma(const bf16* a, int rows, int in, const float* W, const float* b,
+                             int out, const float* y, const int64_t* labels, int loss,
+                             float inv_count, int act_prev, bf16* dz_out, float* gW, float* gb,
+                             float* dlogits_out, float* ws, float loss_scale, float* loss_out,
+                             hipStream_t s);
 // sgd: apply the optimizer update in the combine; pending: return the combine unlaunched (see
 // bwd_group) instead of running it
 hipError_t head_wgrad(const void* a, int a_bf16, int rows, int in, const float* dlogits, int out,

@@ -142,6 +142,46 @@ def test_head(loss, out_f, dtype, rows, in_f):
     torch.testing.assert_close(res["hip"][3], res["ref"][3], rtol=1e-4, atol=1e-4)
 
 
+@pytest.mark.parametrize("loss,out_f,rows,in_f", [("xent", 10, 1000, 8192), ("xent", 100, 777, 1024),
+                                                 ("mse", 37, 300, 512), ("xent", 128, 64, 256)])
+def test_general_head_matrix_core_path_vs_valu_path(loss, out_f, rows, in_f):
+    """The matrix-core general head (bf16 activations) against the fp32 VALU general head on the
+    same inputs: loss and dlogits to fp32 summation-order noise, the weight / bias gradient
+    (fp32 MFMA on the fp32 dlogits) likewise, dZ to bf16 rounding (it runs the bf16 dgrad GEMM on
+    bf16 dlogits and weights, like every hidden layer)."""
+    from nnmpi_amd import native
+    from nnmpi_amd.ops.hip_ops import HipOps
+    lib = native.lib()
+    assert lib.head_general_mfma_ok(1, in_f, out_f)
+    ops = HipOps()
+    a = torch.relu(_rand(rows, in_f, seed=31)).to(torch.bfloat16)
+    W = _rand(out_f, in_f, seed=32, scale=0.05)
+    b = _rand(out_f, seed=33)
+    y = _rand(rows, out_f, seed=34) if loss == "mse" else None
+    lab = (torch.arange(rows, device=DEV) * 5 % out_f) if loss == "xent" else None
+    res = {}
+    try:
+        for valu in (0, 1):
+            lib.set_head_general_valu(valu)
+            gW = torch.zeros(out_f, in_f, device=DEV)
+            gb = torch.zeros(out_f, device=DEV)
+            dz = torch.zeros(rows, in_f, device=DEV, dtype=torch.bfloat16)
+            dl = torch.zeros(rows, out_f, device=DEV)
+            lo = torch.zeros(4, device=DEV)
+            ws = torch.zeros(ops.head_workspace_bytes(rows, in_f, out_f) // 4 + 16, device=DEV)
+            ops.head(a, W, b, y, lab, loss, 1.0 / rows, "relu", dz, gW, gb, dl, lo, 1.0 / rows, ws=ws)
+            torch.cuda.synchronize()
+            res[valu] = (gW, gb, dz, dl, lo[0].item())
+    finally:
+        lib.set_head_general_valu(0)
+    m, v = res[0], res[1]
+    assert m[4] == pytest.approx(v[4], rel=1e-5)
+    torch.testing.assert_close(m[3], v[3], rtol=1e-4, atol=1e-7)
+    torch.testing.assert_close(m[0], v[0], rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(m[1], v[1], rtol=1e-4, atol=1e-6)
+    torch.testing.assert_close(m[2].float(), v[2].float(), rtol=2e-2, atol=1e-5)
+
+
 @pytest.mark.parametrize("first,nesterov,wd,damp", [(True, False, 0.0, 0.0), (False, False, 0.0, 0.0),
                                                     (False, True, 1e-2, 0.0), (False, False, 1e-2, 0.3)])
 def test_sgd_matches_torch_optim(first, nesterov, wd, damp):
