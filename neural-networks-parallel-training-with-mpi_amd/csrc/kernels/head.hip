@@ -894,6 +894,14 @@ __global__ void __launch_bounds__(64 * HS_WAVES) head_logits_stream_kernel(
             acc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(wv[u][t][1][e], (float)xv[u][e + 4], acc[t], 0, 0, 0);
         }
     }
+    // The LDS store below reads the accumulators the loop's last MFMA wrote.  For NT == 1 the
+    // compiler (ROCm 7.2 hipcc, gfx950) placed that ds_write two instructions after the final
+    // v_mfma_f32_16x16x4_f32 with no wait states, so it stored a stale partial sum (logits off by
+    // a few percent at in >= 2048; NT >= 2 got its s_nops).  Pin 20 wait states between the two,
+    // more than any XDL-write -> LDS-read distance needs.
+    __builtin_amdgcn_sched_barrier(0);
+    asm volatile("s_nop 7\n\ts_nop 7\n\ts_nop 3" ::: "memory");
+    __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
     for (int t = 0; t < NT; ++t) part[(w * NT + t) * 64 + lane] = acc[t];
     __syncthreads();
@@ -985,11 +993,11 @@ bool head_general_mfma_ok(int a_bf16, int in, int out) {
 static int hs_outp(int out) { return (out + 7) / 8 * 8; }
 static int hs_blocks(int rows) { return std::max(1, std::min(1024, (rows + 15) / 16)); }
 
-// workspace (floats): dl [rows*out] | dl16 [rows*outp bf16] | W16 [out*in bf16] | loss partials |
-// head_wgrad workspace
+// workspace (floats): dl [rows*out] | dl16 [rows*outp bf16] | W16 [outp*in bf16] | loss partials
+// | head_wgrad workspace
 size_t head_general_mfma_workspace_bytes(int rows, int in, int out) {
   const size_t f = (size_t)rows * out + ((size_t)rows * hs_outp(out) + 1) / 2 + 4 +
-                   ((size_t)out * in + 1) / 2 + 4 + hs_blocks(rows) + 4;
+                   ((size_t)hs_outp(out) * in + 1) / 2 + 4 + hs_blocks(rows) + 4;
   return (f + 64) * sizeof(float) + head_wgrad_workspace_bytes(rows, in, out);
 }
 
@@ -1008,7 +1016,7 @@ hipError_t head_general_mfma(const bf16* a, int rows, int in, const float* W, co
   bf16* dl16 = reinterpret_cast<bf16*>(cur);
   cur = align16(cur + ((size_t)rows * outp + 1) / 2);
   bf16* W16 = reinterpret_cast<bf16*>(cur);
-  cur = align16(cur + ((size_t)out * in + 1) / 2);
+  cur = align16(cur + ((size_t)outp * in + 1) / 2);
   float* lpart = cur;
   float* wws = align16(lpart + nb);
   // the padding columns of the bf16 dl copy stay zero (the dgrad GEMM reads 8-wide chunks)
@@ -1039,8 +1047,13 @@ hipError_t head_general_mfma(const bf16* a, int rows, int in, const float* W, co
   if (dz_out) {
     e = cast_f32_bf16(W, W16, (long long)out * in, s);
     if (e != hipSuccess) return e;
-    // dZ[rows][in] = dl16[rows][out] . W16[out][in] * act'(a): K = out, lda = outp
-    e = linear_dgrad_bf16(dl16, outp, W16, in, a, in, dz_out, in, rows, in, out, act_prev, s);
+    // the bf16 GEMM wants K % 8 == 0: K = outp, with zero rows of W16 against dl16's zero columns
+    if (outp != out) {
+      e = hipMemsetAsync(W16 + (size_t)out * in, 0, (size_t)(outp - out) * in * sizeof(bf16), s);
+      if (e != hipSuccess) return e;
+    }
+    // dZ[rows][in] = dl16[rows][outp] . W16[outp][in] * act'(a)
+    e = linear_dgrad_bf16(dl16, outp, W16, in, a, in, dz_out, in, rows, in, outp, act_prev, s);
     if (e != hipSuccess) return e;
   }
   return head_wgrad(a, 1, rows, in, dl, out, gW, gb, wws, lpart, nb, loss_scale, loss_out, s,

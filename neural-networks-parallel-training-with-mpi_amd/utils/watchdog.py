@@ -65,6 +65,8 @@ class Watchdog:
             except Exception:
                 pass
         self.on_fail(why)
+        # (the default handler never returns; a custom one that does has taken the failure over)
+        backstop.cancel()
 
     @staticmethod
     def _backstop(why: str):

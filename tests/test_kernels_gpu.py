@@ -133,13 +133,30 @@ def test_head(loss, out_f, dtype, rows, in_f):
         lo = torch.zeros(4, device=DEV)
         ws = torch.zeros(ops.head_workspace_bytes(rows, in_f, out_f) // 4 + 16, device=DEV)
         o.head(a, W, b, y, lab, loss, 1.0 / rows, "relu", dz, gW, gb, dl, lo, 1.0 / rows, ws=ws)
-        res[name] = (gW, gb, dz, lo[0])
+        res[name] = (gW, gb, dz, lo[0], dl)
     tol = dict(rtol=2e-3, atol=2e-3)
     torch.testing.assert_close(res["hip"][0], res["ref"][0], **tol)
     torch.testing.assert_close(res["hip"][1], res["ref"][1], **tol)
-    dtol = dict(rtol=2e-2, atol=2e-3) if dtype == torch.bfloat16 else dict(rtol=1e-4, atol=1e-5)
-    torch.testing.assert_close(res["hip"][2].float(), res["ref"][2].float(), **dtol)
+    if dtype == torch.bfloat16:
+        _assert_dz_within_bf16_bound(res["hip"][2], res["ref"][2], res["ref"][4], W, a)
+    else:
+        torch.testing.assert_close(res["hip"][2], res["ref"][2], rtol=1e-4, atol=1e-5)
     torch.testing.assert_close(res["hip"][3], res["ref"][3], rtol=1e-4, atol=1e-4)
+
+
+def _assert_dz_within_bf16_bound(dz, ref, dl, W, a):
+    """dZ = (dl . W) * relu'(a) stored in bf16.  The matrix-core general head runs it as the bf16
+    dgrad GEMM on bf16 copies of dl and W (fp32 accumulation), so every product carries at most
+    two bf16 roundings (u = 2^-8 each) and the result one more, and the reference (itself stored
+    in bf16) one: elementwise |dz - ref| <= 2u |ref| + (2u + u^2) sum_n |dl_n W_nf| (+ a denormal
+    floor).  The exact fp32 kernels satisfy the tighter 2u |ref| part alone."""
+    u = 2.0 ** -8
+    mask = (a.float() > 0).double()
+    bound = (2 * u * ref.double().abs() + (2 * u + u * u) * (dl.double().abs() @ W.double().abs()) * mask
+             + 1e-30) * 1.01
+    err = (dz.double() - ref.double()).abs()
+    worst = float((err / bound).max())
+    assert worst <= 1.0, f"dZ outside the bf16 rounding bound: max err/bound {worst:.3f}"
 
 
 @pytest.mark.parametrize("loss,out_f,rows,in_f", [("xent", 10, 1000, 8192), ("xent", 100, 777, 1024),
@@ -179,7 +196,9 @@ def test_general_head_matrix_core_path_vs_valu_path(loss, out_f, rows, in_f):
     torch.testing.assert_close(m[3], v[3], rtol=1e-4, atol=1e-7)
     torch.testing.assert_close(m[0], v[0], rtol=1e-4, atol=1e-6)
     torch.testing.assert_close(m[1], v[1], rtol=1e-4, atol=1e-6)
-    torch.testing.assert_close(m[2].float(), v[2].float(), rtol=2e-2, atol=1e-5)
+    # the VALU path's dZ is the exact fp32 product rounded once; the MFMA path's is within the
+    # bf16 dgrad bound of it
+    _assert_dz_within_bf16_bound(m[2], v[2], v[3], W, a)
 
 
 @pytest.mark.parametrize("first,nesterov,wd,damp", [(True, False, 0.0, 0.0), (False, False, 0.0, 0.0),

@@ -165,6 +165,10 @@ def test_watchdog_fires_on_stall():
     time.sleep(0.8)
     wd.stop()
     assert hit and "no training progress" in hit[0]
+    # a handler that returns has taken the failure over: the abort backstop must not end the
+    # process later (it would kill the rest of the test session with status 3)
+    import threading
+    assert not [t for t in threading.enumerate() if isinstance(t, threading.Timer) and t.is_alive()]
 
 
 def test_watchdog_quiet_when_kicked():
@@ -253,3 +257,14 @@ def test_stale_native_library_is_rebuilt(monkeypatch):
 def test_built_library_carries_the_source_hash():
     from nnmpi_amd import _build
     assert _build.built_hash() == _build.source_hash()
+
+
+def test_no_mfma_result_read_without_wait_states():
+    """Disassemble the built gfx950 code objects and check that no instruction reads an MFMA's
+    destination registers without wait states behind the MFMA (the hipcc miss that made the
+    general head's one-tile logits kernel store a stale partial sum; nnmpi_amd/_isa_check.py)."""
+    import os
+    from nnmpi_amd import _build, _isa_check
+    if not os.path.exists(_isa_check.OBJDUMP) or not os.path.exists(_build.ext_path()):
+        pytest.skip("no llvm-objdump or no built library")
+    assert _isa_check.scan_library(_build.ext_path()) == []
