@@ -428,15 +428,17 @@ size_t wgrad_workspace_bytes(int M, int N, int K) {
 
 // GEMM parameters of a weight gradient and the split-K combine it needs (pending.S == 0: the
 // GEMM writes dW / db directly).
-int gemm_host::make_wgrad(const WgradArgs& a, GemmParams& p, SlabReduce& pending) {
+static int make_wgrad_s(const WgradArgs& a, GemmParams& p, SlabReduce& pending, int want) {
   // dW[M=out][N=in] = sum_k dZ[k][m] X[k][n]; db[m] = sum_k dZ[k][m].
   const int M = a.M, N = a.N, K = a.K;
-  const int splits = wgrad_splits(M, N, K);
   const int ksteps = (K + GEMM_BK - 1) / GEMM_BK;
+  // (the split count actually used: every split holds k_per_split k-steps, the last one fewer)
+  const int kps = (ksteps + want - 1) / want;
+  const int splits = std::max(1, (ksteps + kps - 1) / kps);
   p = GemmParams{};
   p.sgd_serial = sgd_serial();
   p.A = a.dZ; p.lda = a.lddz; p.B = a.X; p.ldb = a.ldx; p.M = M; p.N = N; p.K = K;
-  p.k_per_split = ((ksteps + splits - 1) / splits) * GEMM_BK;
+  p.k_per_split = kps * GEMM_BK;
   pending = SlabReduce{};
   if (splits == 1) {
     p.C = a.dW; p.ldc = N; p.c_split_stride = 0;
@@ -453,6 +455,10 @@ int gemm_host::make_wgrad(const WgradArgs& a, GemmParams& p, SlabReduce& pending
   if (a.db) { pending.bws = bws; pending.bstride = M; pending.bout = a.db; }
   pending.sg = a.sg;
   return splits;
+}
+
+int gemm_host::make_wgrad(const WgradArgs& a, GemmParams& p, SlabReduce& pending) {
+  return make_wgrad_s(a, p, pending, wgrad_splits(a.M, a.N, a.K));
 }
 
 hipError_t linear_wgrad_bf16_deferred(const bf16* dZ, int lddz, const bf16* X, int ldx, float* dW,
@@ -691,6 +697,123 @@ hipError_t bwd_group(const DgradArgs* dg, const WgradArgs* wg, const SlabReduce*
     if (e != hipSuccess) return e;
     return slab_reduce(pend, s);
   }
+  return hipGetLastError();
+}
+
+// ---- row-band step: all weight gradients in one launch, all combines in one launch -------
+// (rowband.hip).  The weight-gradient jobs are the grouped backward's 128x128 split-K tiles
+// (same tile body, same slab layout as the standalone launch); jobs follow each other in block
+// order, each padded to a multiple of 8 blocks so its XCD remap sees the round-robin XCD
+// assignment.
+struct WgradMultiParams {
+  GemmParams wg[RB_MAXL];
+  int gx[RB_MAXL], tiles[RB_MAXL], n[RB_MAXL], blocks[RB_MAXL];
+  int nj;
+};
+
+template <int GA>
+__global__ void __launch_bounds__(GRP_THREADS, 4) wgrad_multi_kernel(WgradMultiParams g) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  int bid = blockIdx.x;
+#pragma unroll
+  for (int j = 0; j < RB_MAXL; ++j) {
+    if (j >= g.nj) return;
+    if (bid < g.blocks[j]) {
+      const int l = xcd_remap(bid, g.blocks[j]);
+      if (l >= g.n[j]) return;
+      const int split = l / g.tiles[j], t = l % g.tiles[j];
+      dma_gemm_tile<GRP_BM, GRP_BN, GRP_WGM, GRP_WGN, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, GRP_NS, GA>(
+          g.wg[j], smem, t % g.gx[j], t / g.gx[j], split);
+      return;
+    }
+    bid -= g.blocks[j];
+  }
+}
+
+int wgrad_multi_splits(int nj, int M, int N, int K) {
+  // two 512-thread blocks per CU: fill the 512 slots of the chip in one wave of blocks
+  const int tiles = ((M + GRP_BM - 1) / GRP_BM) * ((N + GRP_BN - 1) / GRP_BN);
+  const int ksteps = (K + GEMM_BK - 1) / GEMM_BK;
+  int s = std::max(1, 512 / std::max(1, nj * tiles));
+  s = std::min(s, std::max(1, ksteps / 4));   // >= 4 k-steps per split
+  if (g_wgrad_splits > 0 && g_wgrad_splits < s) s = g_wgrad_splits;
+  return s;
+}
+
+hipError_t wgrad_multi(const WgradArgs* jobs, int nj, int splits, SlabReduce* pending, hipStream_t s) {
+  if (nj < 1 || nj > RB_MAXL) return hipErrorInvalidValue;
+  WgradMultiParams g{};
+  g.nj = nj;
+  int nb = 0;
+  for (int j = 0; j < nj; ++j) {
+    const WgradArgs& a = jobs[j];
+    if (wgrad_tile(a.M, a.N) != 128 || a.db == nullptr || a.ws == nullptr || a.dW16 != nullptr)
+      return hipErrorInvalidValue;
+    const int want = splits > 0 ? splits : wgrad_multi_splits(nj, a.M, a.N, a.K);
+    GemmParams p;
+    const int sp = make_wgrad_s(a, p, pending[j], want);
+    if (sp == 1) {   // un-split: the combine would have nothing to do -- keep the slab form
+      p.C = a.ws; p.c_split_stride = (long long)a.M * a.N; p.sg = SgdFuse{};
+      p.bias_grad = a.ws + (size_t)a.M * a.N; p.bg_split_stride = a.M;
+      p.c16 = nullptr; p.bg16 = nullptr;
+      pending[j] = SlabReduce{a.ws, 1, (long long)a.M * a.N, a.M, a.N, a.dW, a.N,
+                              a.ws + (size_t)a.M * a.N, a.M, a.db, nullptr, 0, 0.f, nullptr, a.sg};
+    }
+    set_extents<XMAJ, XMAJ>(p);
+    p.store_pol = slab_store_pol();
+    g.wg[j] = p;
+    g.gx[j] = (p.N + GRP_BN - 1) / GRP_BN;
+    g.tiles[j] = g.gx[j] * ((p.M + GRP_BM - 1) / GRP_BM);
+    g.n[j] = g.tiles[j] * sp;
+    g.blocks[j] = (g.n[j] + 7) & ~7;
+    nb += g.blocks[j];
+  }
+  const int ga = g_group_async >= 0 ? std::min(g_group_async, 2) : GROUP_ASYNC_DEFAULT;
+  using Fn = void (*)(WgradMultiParams);
+  static const Fn fns[3] = {wgrad_multi_kernel<0>, wgrad_multi_kernel<1>, wgrad_multi_kernel<2>};
+  static bool attr[3] = {};
+  if (!attr[ga]) {
+    (void)hipFuncSetAttribute((const void*)fns[ga], hipFuncAttributeMaxDynamicSharedMemorySize, GRP_SMEM);
+    attr[ga] = true;
+  }
+  hipLaunchKernelGGL(fns[ga], dim3(nb), dim3(GRP_THREADS), GRP_SMEM, s, g);
+  return hipGetLastError();
+}
+
+struct SlabMultiParams {
+  SlabReduce r[RB_MAXL + 1];
+  int ws[RB_MAXL + 1], nb_main[RB_MAXL + 1], nb_bias[RB_MAXL + 1], nb[RB_MAXL + 1];
+  int nr;
+};
+
+__global__ void __launch_bounds__(SLAB_THREADS) slab_multi_kernel(SlabMultiParams g) {
+  __shared__ f32x4 part[SLAB_PART_BYTES / 16];
+  int bid = blockIdx.x;
+#pragma unroll
+  for (int j = 0; j < RB_MAXL + 1; ++j) {
+    if (j >= g.nr) return;
+    if (bid < g.nb[j]) {
+      slab_reduce_any(g.ws[j], g.r[j], bid, g.nb_main[j], g.nb_bias[j], part);
+      return;
+    }
+    bid -= g.nb[j];
+  }
+}
+
+hipError_t slab_reduce_multi(const SlabReduce* r, int nr, hipStream_t s) {
+  if (nr < 1 || nr > RB_MAXL + 1) return hipErrorInvalidValue;
+  SlabMultiParams g{};
+  g.nr = nr;
+  int nb = 0;
+  for (int j = 0; j < nr; ++j) {
+    g.r[j] = r[j];
+    g.r[j].sgd_serial = sgd_serial();
+    g.ws[j] = slab_ws(r[j]);
+    slab_blocks(r[j], g.nb_main[j], g.nb_bias[j], g.nb[j]);
+    nb += g.nb[j];
+  }
+  if (nb == 0) return hipSuccess;
+  hipLaunchKernelGGL(slab_multi_kernel, dim3(nb), dim3(SLAB_THREADS), 0, s, g);
   return hipGetLastError();
 }
 

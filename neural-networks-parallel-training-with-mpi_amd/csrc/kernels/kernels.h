@@ -139,6 +139,47 @@ hipError_t linear_wgrad_bf16_out16_defer(const bf16* dZ, int lddz, const bf16* X
                                          bf16* db16, int M, int N, int K, const SgdFuse& other,
                                          const bf16* g16o, hipStream_t s);
 
+// ---- row-band step (rowband.hip): forward + MSE head + activation gradients of a narrow
+// square MLP (input and hidden widths H = 512, out == 1) in one launch, then every weight
+// gradient in one grouped launch and every combine in one more (see rowband.hip) ----
+constexpr int RB_MAXL = 4;   // hidden layers
+struct RowbandArgs {
+  const bf16* X; int ldx;
+  int rows, H, nh, act;
+  const bf16* W[RB_MAXL];   // compute (bf16) weights [H][H]
+  const float* b[RB_MAXL];  // biases [H]
+  bf16* a[RB_MAXL];         // saved activations a_l [rows][H]
+  bf16* dz[RB_MAXL];        // dZ_l [rows][H]
+  const float* wh; const float* bh;   // head weight [H] / bias [1] (fp32)
+  const float* y;           // targets [rows]
+  float inv_count;
+  float* wslab; float* bslab; float* loss_part;   // per-band head partials (rowband_blocks)
+  int rot = 1;              // column groups rotated by block (A/B: NNMPI_RB_ROT=0)
+  int diag = 0;             // timing diagnostics: 1 = forward passes only
+};
+int rowband_blocks(int rows);
+bool rowband_ok(int rows, int H, int in, int nh, int out, int loss, int act);
+hipError_t rowband_fwd_bwd(const RowbandArgs& p, hipStream_t s);
+// The whole step: grads (or, with sg.g_base set, the fused SGD-momentum update at the arena
+// positions of gW / gb / gWh / gbh), loss_out[0] = loss_scale * sum of squared errors.
+struct RowbandStep {
+  RowbandArgs fb;
+  float* gW[RB_MAXL]; float* gb[RB_MAXL];
+  float* gWh; float* gbh;
+  float* ws;          // rowband_workspace_bytes
+  float loss_scale; float* loss_out;
+  SgdFuse sg;
+  int splits;         // weight-gradient split-K slabs (0 = fill the chip)
+};
+size_t rowband_workspace_bytes(int rows, int H, int nh, int splits);
+hipError_t rowband_step(const RowbandStep& st, hipStream_t s);
+// Weight gradients of several layers in ONE grouped launch (128x128 tiles, split-K with
+// `splits` slabs each, 0 = fill the chip); pending[j] receives job j's combine.
+int wgrad_multi_splits(int nj, int M, int N, int K);
+hipError_t wgrad_multi(const WgradArgs* jobs, int nj, int splits, SlabReduce* pending, hipStream_t s);
+// Several independent combines in ONE launch (same per-block body as slab_reduce).
+hipError_t slab_reduce_multi(const SlabReduce* r, int nr, hipStream_t s);
+
 // ---- fp32 GEMM (gemm_f32.hip) ----
 hipError_t linear_fwd_f32(const float* X, int ldx, const float* W, int ldw, const float* bias,
                           float* Y, int ldy, int M, int N, int K, int act, hipStream_t s);

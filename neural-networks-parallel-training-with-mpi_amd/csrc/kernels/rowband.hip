@@ -1,0 +1,403 @@
+// Row-band step for narrow square MLPs (every hidden width and the input width = H = 512, a
+// regression head out == 1 with MSE): the reference's whole forward, loss and activation-gradient
+// chain (ref.py:42-44,170-176: Linear+ReLU x L-1, Linear, MSELoss, and autograd's mm /
+// threshold_backward down to dZ_0) in ONE launch, then every weight gradient in ONE grouped
+// launch and every combine (+ the fused SGD-momentum update on one rank) in ONE more.
+//
+// Why: everything up to the weight gradients is ROW-LOCAL -- row r of a_l depends only on row r
+// of a_{l-1}, the head's dlogit of row r only on row r of a_{L-2}, and row r of dZ_{l-1} only on
+// row r of dZ_l.  A block that owns a band of 32 rows can therefore run all of it with the
+// activations resident in LDS, and only the weights stream in: 512 x 512 bf16 = 512 KiB per
+// layer, resident in every XCD's L2 after the first touch (1.5 MiB for three layers), read
+// with 16-byte loads straight into MFMA B fragments.  The 128x128-tile launches it replaces pay
+// a launch boundary, a first-fetch / epilogue fixed cost and an activation re-read from the
+// Infinity Cache per GEMM (docs/PERF.md "Where a launch's time goes"): 8 launches per step
+// become 3.
+//
+// Block = 8 waves (512 threads) x 32 rows; wave w owns output columns [64w, 64w+64) of every
+// layer (2 x 4 v_mfma_f32_16x16x32_bf16 tiles).  LDS: two activation images (ping-pong, the
+// KMAJ image of gemm_tiles.h per 64-deep k-block: conflict-free row-fragment reads) + one
+// wave-private [64 k][64 x] XMAJ stage per wave for the dgrad's transposed weight operand
+// (ds_read_b64_tr_b16 reads, the same image as the GEMMs' XMAJ operand).  The weights of the
+// forward are KMAJ for the B operand already (W[n][k], k contiguous), so they go global ->
+// registers with no LDS hop; a 4-deep register ring keeps 32 16-byte loads per lane in flight.
+// Each layer's output is written into the other LDS image from the accumulators, and after the
+// block barrier copied out row-contiguously (activations and dZ are needed by the weight
+// gradients).
+#include "gemm_tiles.h"
+
+namespace nnmpi {
+
+constexpr int RB_ROWS = 32;
+constexpr int RB_WAVES = 8;
+constexpr int RB_THREADS = 64 * RB_WAVES;
+constexpr int RB_RING = 4;   // k-steps of weight loads in flight per lane
+
+template <int H>
+struct RbGeom {
+  static_assert(H == 512, "row-band step: H = 512");
+  static constexpr int KSTEPS = H / 64;
+  static constexpr int WCOLS = H / RB_WAVES;       // output columns per wave
+  static constexpr int NJ = WCOLS / 16;            // 16-column MFMA tiles per wave
+  static constexpr int KB_BYTES = RB_ROWS * 128;   // one 64-deep k-block of an image
+  static constexpr int BUF = RB_ROWS * H * 2;      // one activation image
+  static constexpr int STAGE = 64 * WCOLS * 2;     // wave-private dgrad weight stage
+  static constexpr int SCRATCH = 2 * RB_ROWS * 4;  // head: per-row dlogit + loss
+  static constexpr int SMEM = 2 * BUF + RB_WAVES * STAGE + SCRATCH;
+  static constexpr int FLD = 2 * NJ;               // forward: weight loads per lane per k-step
+  static constexpr int DLD = WCOLS / 8;            // dgrad: 16-B stage chunks per lane per k-step
+};
+
+// byte offset of element (row r, column k) in an activation image
+__device__ __forceinline__ int rb_off(int r, int k) {
+  return (k >> 6) * (RB_ROWS * 128) + kmaj_off(r, (k >> 3) & 7) + ((k & 7) << 1);
+}
+
+// Row-contiguous copy between an LDS image and a [rows][ld] bf16 matrix (rows row0 .. row0 +
+// nvalid - 1): each wave moves whole 128-byte row pieces (8 lanes per row).
+template <int H>
+__device__ __forceinline__ void rb_copy_out(const char* img, bf16* dst, int ld, int nvalid, int tid) {
+  constexpr int CH = RB_ROWS * H / 8;
+#pragma unroll
+  for (int it = 0; it < CH / RB_THREADS; ++it) {
+    const int id = tid + it * RB_THREADS;
+    const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(img + kb * (RB_ROWS * 128) + kmaj_off(r, k8));
+    if (r < nvalid) *reinterpret_cast<bf16x8*>(dst + (long long)r * ld + kb * 64 + k8 * 8) = v;
+  }
+}
+
+template <int H>
+__device__ __forceinline__ void rb_load_in(char* img, const bf16* src, int ld, int nvalid, int tid) {
+  constexpr int CH = RB_ROWS * H / 8;
+  bf16x8 v[CH / RB_THREADS];
+#pragma unroll
+  for (int it = 0; it < CH / RB_THREADS; ++it) {
+    const int id = tid + it * RB_THREADS;
+    const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
+    const int rr = min(r, nvalid - 1);   // clamped: every load issues; padding rows zeroed below
+    v[it] = *reinterpret_cast<const bf16x8*>(src + (long long)rr * ld + kb * 64 + k8 * 8);
+    if (r >= nvalid) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[it][e] = (bf16)0.f;
+    }
+  }
+#pragma unroll
+  for (int it = 0; it < CH / RB_THREADS; ++it) {
+    const int id = tid + it * RB_THREADS;
+    const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
+    *reinterpret_cast<bf16x8*>(img + kb * (RB_ROWS * 128) + kmaj_off(r, k8)) = v[it];
+  }
+}
+
+// One forward layer of the band: out = act(in . W^T + b) into the other image.
+template <int H, int ACT>
+__device__ __forceinline__ void rb_forward(const bf16* __restrict__ W, const float* __restrict__ bias,
+                                           const char* in, char* out, int w, int lane) {
+  using G = RbGeom<H>;
+  const int n0 = w * G::WCOLS;
+  f32x4 acc[2][G::NJ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < G::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // B fragment of tile j, half kk of k-step t: W[n0 + 16j + (lane & 15)][64t + 32kk + 8(lane >> 4) ..]
+  const bf16* wp = W + (long long)(n0 + (lane & 15)) * H + 8 * (lane >> 4);
+  bf16x8 ring[RB_RING][G::FLD];
+  auto issue = [&](int t, bf16x8 (&dst)[G::FLD]) {
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+      for (int j = 0; j < G::NJ; ++j)
+        dst[kk * G::NJ + j] = *reinterpret_cast<const bf16x8*>(wp + (long long)16 * j * H + 64 * t + 32 * kk);
+  };
+  f32x4 bv[G::NJ];
+#pragma unroll
+  for (int j = 0; j < G::NJ; ++j) bv[j] = *reinterpret_cast<const f32x4*>(bias + n0 + 16 * j + 4 * (lane >> 4));
+#pragma unroll
+  for (int s = 0; s < RB_RING; ++s) issue(s, ring[s]);
+  // (sched_barrier: keep each ring refill where it is issued -- left alone, the scheduler sinks
+  // the loads next to their MFMAs and the ring degenerates to 4 loads in flight)
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int t = 0; t < G::KSTEPS; ++t) {
+    const char* kb = in + t * G::KB_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[2];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = read_frag<64, KMAJ>(kb, 16 * i, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < G::NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[t % RB_RING][kk * G::NJ + j], af[i],
+                                                              acc[i][j], 0, 0, 0);
+    }
+    __builtin_amdgcn_sched_barrier(0);
+    // the slot just consumed is refilled for k-step t + RB_RING
+    if (t + RB_RING < G::KSTEPS) issue(t + RB_RING, ring[t % RB_RING]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // lane holds out[16i + (lane & 15)][n0 + 16j + 4(lane >> 4) .. +3]
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < G::NJ; ++j) {
+      const f32x4 v = acc[i][j] + bv[j];
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (bf16)act_fwd_t<ACT>(v[r]);
+      *reinterpret_cast<bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * j + 4 * (lane >> 4))) = o;
+    }
+}
+
+// One activation-gradient layer: out = (in . W) * act'(aux), in = dZ_l (image), aux = a_{l-1}
+// rows of this band in global memory (written by this block's earlier copy-out).
+template <int H, int ACT>
+__device__ __forceinline__ void rb_dgrad(const bf16* __restrict__ W, const char* in, char* out,
+                                         char* stage, const bf16* aux, int nvalid, int w, int lane) {
+  using G = RbGeom<H>;
+  const int n0 = w * G::WCOLS;
+  f32x4 acc[2][G::NJ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < G::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  // stage chunk q of k-step t: W[64t + (lane >> 3) + 8q][n0 + 8(lane & 7) .. +7] -> XMAJ image
+  const bf16* wp = W + (long long)(lane >> 3) * H + n0 + 8 * (lane & 7);
+  int soff[G::DLD];
+#pragma unroll
+  for (int q = 0; q < G::DLD; ++q) {
+    const int k = (lane >> 3) + 8 * q, ch = lane & 7;
+    soff[q] = k * (G::WCOLS * 2) + ((ch ^ swz_x<G::WCOLS>(k)) << 4);
+  }
+  bf16x8 ring[RB_RING][G::DLD];
+  auto issue = [&](int t, bf16x8 (&dst)[G::DLD]) {
+#pragma unroll
+    for (int q = 0; q < G::DLD; ++q)
+      dst[q] = *reinterpret_cast<const bf16x8*>(wp + (long long)(64 * t + 8 * q) * H);
+  };
+  // the epilogue's saved activations, loaded up front (their latency hides under the main loop)
+  bf16x4 ax[2][G::NJ];
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < G::NJ; ++j) {
+      const int m = min(16 * i + (lane & 15), nvalid - 1);
+      ax[i][j] = *reinterpret_cast<const bf16x4*>(aux + (long long)m * H + n0 + 16 * j + 4 * (lane >> 4));
+    }
+#pragma unroll
+  for (int s = 0; s < RB_RING; ++s) issue(s, ring[s]);
+  __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+  for (int t = 0; t < G::KSTEPS; ++t) {
+#pragma unroll
+    for (int q = 0; q < G::DLD; ++q) *reinterpret_cast<bf16x8*>(stage + soff[q]) = ring[t % RB_RING][q];
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + RB_RING < G::KSTEPS) issue(t + RB_RING, ring[t % RB_RING]);
+    __builtin_amdgcn_sched_barrier(0);
+    const char* kb = in + t * G::KB_BYTES;
+#pragma unroll
+    for (int kk = 0; kk < 2; ++kk) {
+      bf16x8 af[2], bfr[G::NJ];
+#pragma unroll
+      for (int i = 0; i < 2; ++i) af[i] = read_frag<64, KMAJ>(kb, 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < G::NJ; ++j) bfr[j] = read_frag<G::WCOLS, XMAJ>(stage, 16 * j, kk, lane);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < G::NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+    }
+  }
+#pragma unroll
+  for (int i = 0; i < 2; ++i)
+#pragma unroll
+    for (int j = 0; j < G::NJ; ++j) {
+      bf16x4 o;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc[i][j][r] * act_bwd_t<ACT>((float)ax[i][j][r]));
+      *reinterpret_cast<bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * j + 4 * (lane >> 4))) = o;
+    }
+}
+
+// Regression head (out == 1, MSE) on the band's last activations `in`: logit, loss, dlogit, the
+// head's weight/bias-gradient partials of this band, and dZ_{L-2} = dl * w * act'(a) into `out`.
+template <int H, int ACT>
+__device__ __forceinline__ void rb_head(const RowbandArgs& p, const char* in, char* out, float* dls,
+                                        float* lss, int row0, int nvalid, int tid) {
+  constexpr int CPT = H / 8 / 16;   // 8-column chunks per thread (16 threads per row)
+  const int r = tid >> 4, g = tid & 15;
+  float a[CPT][8], wv[CPT][8];
+  float dot = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int k = 8 * (g + 16 * c);
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(in + rb_off(r, k));
+    const float4 w0 = *reinterpret_cast<const float4*>(p.wh + k);
+    const float4 w1 = *reinterpret_cast<const float4*>(p.wh + k + 4);
+    wv[c][0] = w0.x; wv[c][1] = w0.y; wv[c][2] = w0.z; wv[c][3] = w0.w;
+    wv[c][4] = w1.x; wv[c][5] = w1.y; wv[c][6] = w1.z; wv[c][7] = w1.w;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) {
+      a[c][e] = (float)v[e];
+      dot += a[c][e] * wv[c][e];
+    }
+  }
+#pragma unroll
+  for (int sh = 8; sh >= 1; sh >>= 1) dot += __shfl_xor(dot, sh, 64);
+  const bool valid = r < nvalid;
+  const float yv = p.y[row0 + min(r, nvalid - 1)];
+  const float d = dot + p.bh[0] - yv;
+  const float dl = valid ? 2.f * d * p.inv_count : 0.f;
+  if (g == 0) {
+    dls[r] = dl;
+    lss[r] = valid ? d * d : 0.f;
+  }
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int k = 8 * (g + 16 * c);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 8; ++e) o[e] = (bf16)(dl * wv[c][e] * act_bwd_t<ACT>(a[c][e]));
+    *reinterpret_cast<bf16x8*>(out + rb_off(r, k)) = o;
+  }
+}
+
+template <int H, int ACT>
+__global__ void __launch_bounds__(RB_THREADS) rowband_kernel(RowbandArgs p) {
+  using G = RbGeom<H>;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  auto img = [&](int i) { return smem + i * G::BUF; };
+  char* stage = smem + 2 * G::BUF + w * G::STAGE;
+  float* dls = reinterpret_cast<float*>(smem + 2 * G::BUF + RB_WAVES * G::STAGE);
+  float* lss = dls + RB_ROWS;
+  const int blk = blockIdx.x;
+  const int row0 = blk * RB_ROWS;
+  const int nvalid = min(RB_ROWS, p.rows - row0);
+  const int nh = p.nh;
+  // column group of this wave: rotated by the block index, so the 32 CUs of an XCD, which run
+  // their passes in near lock-step, read different weight rows (different L2 channels) at any
+  // moment instead of all requesting the same lines together (p.rot = 0: wave w -> group w)
+  const int cg = (w + (p.rot ? blk : 0)) & (RB_WAVES - 1);
+
+  rb_load_in<H>(img(0), p.X + (long long)row0 * p.ldx, p.ldx, nvalid, tid);
+  __syncthreads();
+  int cur = 0;
+  for (int l = 0; l < nh; ++l) {
+    rb_forward<H, ACT>(p.W[l], p.b[l], img(cur), img(cur ^ 1), cg, lane);
+    __syncthreads();
+    cur ^= 1;
+    rb_copy_out<H>(img(cur), p.a[l] + (long long)row0 * H, H, nvalid, tid);
+  }
+  if (p.diag == 1) return;   // timing diagnostics: forward passes only
+  rb_head<H, ACT>(p, img(cur), img(cur ^ 1), dls, lss, row0, nvalid, tid);
+  __syncthreads();
+  // head weight-gradient partial of this band: column tid, rows in order
+  {
+    const float* dl = dls;
+    for (int k = tid; k < H; k += RB_THREADS) {
+      float s = 0.f;
+#pragma unroll 8
+      for (int r = 0; r < RB_ROWS; ++r)
+        s += dl[r] * (float)*reinterpret_cast<const bf16*>(img(cur) + rb_off(r, k));
+      p.wslab[(long long)blk * H + k] = s;
+    }
+    if (tid == 0) {
+      float b = 0.f, l = 0.f;
+      for (int r = 0; r < RB_ROWS; ++r) {
+        b += dl[r];
+        l += lss[r];
+      }
+      p.bslab[blk] = b;
+      p.loss_part[blk] = l;
+    }
+  }
+  cur ^= 1;
+  rb_copy_out<H>(img(cur), p.dz[nh - 1] + (long long)row0 * H, H, nvalid, tid);
+  // the first dgrad writes its output over the last activations the partial above still reads
+  if (nh > 1) __syncthreads();
+  for (int l = nh - 1; l >= 1; --l) {
+    rb_dgrad<H, ACT>(p.W[l], img(cur), img(cur ^ 1), stage, p.a[l - 1] + (long long)row0 * H,
+                     nvalid, cg, lane);
+    __syncthreads();
+    cur ^= 1;
+    rb_copy_out<H>(img(cur), p.dz[l - 1] + (long long)row0 * H, H, nvalid, tid);
+  }
+}
+
+int rowband_blocks(int rows) { return (rows + RB_ROWS - 1) / RB_ROWS; }
+
+bool rowband_ok(int rows, int H, int in, int nh, int out, int loss, int act) {
+  return rows > 0 && H == 512 && in == H && nh >= 1 && nh <= RB_MAXL && out == 1 &&
+         loss == LOSS_MSE && (act == ACT_RELU || act == ACT_TANH || act == ACT_NONE);
+}
+
+static int rb_env(const char* name, int dflt) {
+  const char* e = std::getenv(name);
+  return (e && e[0] >= '0' && e[0] <= '9') ? std::atoi(e) : dflt;
+}
+
+hipError_t rowband_fwd_bwd(const RowbandArgs& p0, hipStream_t s) {
+  RowbandArgs p = p0;
+  if (!rowband_ok(p.rows, p.H, p.H, p.nh, 1, LOSS_MSE, p.act)) return hipErrorInvalidValue;
+  static const int rot = rb_env("NNMPI_RB_ROT", 1), diag = rb_env("NNMPI_RB_DIAG", 0);
+  p.rot = rot;
+  p.diag = diag;
+  using G = RbGeom<512>;
+  using Fn = void (*)(RowbandArgs);
+  static const Fn fns[3] = {rowband_kernel<512, ACT_NONE>, rowband_kernel<512, ACT_RELU>,
+                            rowband_kernel<512, ACT_TANH>};
+  static bool attr = false;
+  if (!attr) {
+    for (Fn f : fns)
+      (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
+    attr = true;
+  }
+  const Fn f = fns[p.act == ACT_RELU ? 1 : p.act == ACT_TANH ? 2 : 0];
+  hipLaunchKernelGGL(f, dim3(rowband_blocks(p.rows)), dim3(RB_THREADS), G::SMEM, s, p);
+  return hipGetLastError();
+}
+
+// ---- the whole step: row-band launch, grouped weight gradients, grouped combines ----------
+static size_t rb_pad4(size_t n) { return (n + 3) & ~(size_t)3; }
+
+size_t rowband_workspace_bytes(int rows, int H, int nh, int splits) {
+  const size_t G = (size_t)rowband_blocks(rows);
+  const int S = splits > 0 ? splits : wgrad_multi_splits(nh, H, H, rows);
+  const size_t head = G * H + rb_pad4(G) + rb_pad4(G);
+  return (head + (size_t)nh * S * ((size_t)H * H + H)) * sizeof(float);
+}
+
+hipError_t rowband_step(const RowbandStep& st0, hipStream_t s) {
+  RowbandStep st = st0;
+  RowbandArgs& p = st.fb;
+  if (!rowband_ok(p.rows, p.H, p.H, p.nh, 1, LOSS_MSE, p.act) || !st.ws) return hipErrorInvalidValue;
+  const int H = p.H, nh = p.nh;
+  const size_t G = (size_t)rowband_blocks(p.rows);
+  float* ws = st.ws;
+  p.wslab = ws;
+  p.bslab = ws + G * H;
+  p.loss_part = p.bslab + rb_pad4(G);
+  float* slabs = p.loss_part + rb_pad4(G);
+  hipError_t e = rowband_fwd_bwd(p, s);
+  if (e != hipSuccess) return e;
+  const int S = st.splits > 0 ? st.splits : wgrad_multi_splits(nh, H, H, p.rows);
+  WgradArgs jobs[RB_MAXL];
+  SlabReduce red[RB_MAXL + 1];
+  for (int l = 0; l < nh; ++l) {
+    jobs[l] = WgradArgs{p.dz[l], H, l == 0 ? p.X : p.a[l - 1], l == 0 ? p.ldx : H, st.gW[l],
+                        st.gb[l], H, H, p.rows, slabs + (size_t)l * S * ((size_t)H * H + H), st.sg};
+  }
+  e = wgrad_multi(jobs, nh, S, red, s);
+  if (e != hipSuccess) return e;
+  red[nh] = SlabReduce{p.wslab, (int)G, H, 1, H, st.gWh, H, p.bslab, 1, st.gbh, p.loss_part, (int)G,
+                       st.loss_scale, st.loss_out, st.sg};
+  return slab_reduce_multi(red, nh + 1, s);
+}
+
+}  // namespace nnmpi

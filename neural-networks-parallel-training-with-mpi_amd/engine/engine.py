@@ -112,6 +112,18 @@ class MLPEngine:
                         all(ops.bwd_group_supported(self.R, *spec.layer_shape(i))
                             for i in range(L - 1)))
         self.ws_pair = [self.ws, torch.zeros_like(self.ws)] if self.grouped else [self.ws, self.ws]
+        # Row-band step (narrow square MSE regressor, e.g. the 512-wide proxy): the forward, the
+        # head and every activation gradient in ONE launch, all weight gradients in one more and
+        # every combine (+ the fused update on one rank) in a third -- see rowband.hip.  Taken
+        # whenever the gradient is reduced after the backward (one rank, the inline all-reduce,
+        # ZeRO-1): it produces every layer's gradient at once, so there is nothing for a
+        # per-bucket overlapped schedule to hide.  Opt-in (NNMPI_ROWBAND=1) until it beats the
+        # grouped schedule on the proxy step (docs/PERF.md).
+        self.rowband = (self.overlap and dtype == torch.bfloat16 and inline_sync and
+                        hasattr(ops, "rowband_ok") and os.environ.get("NNMPI_ROWBAND", "0") == "1"
+                        and ops.rowband_ok(self.R, w, self.act, spec.loss))
+        self.ws_rb = (torch.zeros(ops.rowband_workspace_bytes(self.R, w[1], L - 1) // 4 + 64,
+                                  dtype=torch.float32, device=dev) if self.rowband else None)
         if self.is_cuda:
             self.ev_wfree = [torch.cuda.Event(enable_timing=False) for _ in range(L)]
         # bf16-payload overlapped schedule: per-bucket updates read the bf16 payload
@@ -403,6 +415,8 @@ class MLPEngine:
     # on the critical path.  With one rank the update of the whole arena runs once at the end.
     def _step_body_overlap(self, first: bool):
         rows, ops, ar, L = self.rows, self.ops, self.arena, self.L
+        if self.rowband:
+            return self._step_body_rowband(first)
         if self.grouped:
             return self._step_body_grouped(first)
         if self.fuse_sgd:
@@ -517,6 +531,31 @@ class MLPEngine:
         for i in unfused:
             s, e = ar.layer_range[i]
             ops.sgd(ar, self.hp, self.nesterov, first, offset=s, numel=e - s)
+
+    # Row-band schedule (see rowband.hip): three launches per step.  One rank: the combine
+    # applies the SGD update; several ranks: the combine writes the gradient, then the inline
+    # all-reduce (or ZeRO-1's reduce-scatter / all-gather) and the update follow.
+    def _step_body_rowband(self, first: bool):
+        rows, ops, ar, L = self.rows, self.ops, self.arena, self.L
+        fz = ops.sgd_fusion(ar, self.hp, self.nesterov, first) if self.fuse_sgd else None
+        last = L - 1
+        layers = [(ar.compute_weight(i), ar.bias(i), self.acts[i][:rows], self._dzl(i, rows),
+                   ar.grad_weight(i), ar.grad_bias(i)) for i in range(L - 1)]
+        ops.rowband_step(self.X[:rows], layers, ar.weight(last), ar.bias(last), self.Y[:rows],
+                         self.inv_count, ar.grad_weight(last), ar.grad_bias(last), self.ws_rb,
+                         self.loss_scale, self.loss_out, self.act, sgd=fz)
+        self._mark("bwd")
+        if fz is not None:
+            return
+        if self.sharded:
+            self._update(first)
+            return
+        self.sync.begin()
+        for b in ar.buckets:
+            self.sync.launch_bucket(b, self.stream)
+        self.sync.finish()
+        self._mark("comm")
+        ops.sgd(ar, self.hp, self.nesterov, first)
 
     # Grouped schedule: the backward of layer i is ONE launch holding three independent jobs —
     # dgrad_i, wgrad_i (split-K partial slabs) and the slab combine of layer i+1 (with the SGD

@@ -290,6 +290,45 @@ class HipOps:
         if pending is not None:
             self.lib.slab_reduce(pending, self.stream)
 
+    # ---------------- row-band step (rowband.hip) ----------------
+    def rowband_ok(self, rows: int, widths, act: str, loss: str) -> bool:
+        """Input and hidden widths all equal (512), out == 1, MSE: the whole forward + head +
+        activation-gradient chain runs as one launch per step (see rowband.hip)."""
+        widths = list(widths)
+        if len(widths) < 3 or any(w != widths[0] for w in widths[:-1]):
+            return False
+        return bool(self.lib.rowband_ok(int(rows), widths[1], widths[0], len(widths) - 2,
+                                        widths[-1], LOSS_CODES.get(loss, -1), ACT_CODES[act]))
+
+    def rowband_workspace_bytes(self, rows: int, H: int, nh: int, splits: int = 0) -> int:
+        return int(self.lib.rowband_workspace_bytes(int(rows), int(H), int(nh), int(splits)))
+
+    def rowband_step(self, X, layers, wh, bh, y, inv_count: float, gWh, gbh, ws, loss_scale: float,
+                     loss_out, act: str, sgd=None, splits: int = 0):
+        """One step body of a narrow square MSE regressor in three launches.  ``layers``: per
+        hidden layer ``(W16, b, a_out, dz_out, gW, gb)``.  Writes every activation and dZ, the
+        gradients (or, with ``sgd``, applies the fused update at their arena positions) and
+        ``loss_out[0] = loss_scale * sum of squared errors``."""
+        rows, H = X.shape
+        nh = len(layers)
+        _check(X.dtype == torch.bfloat16 and X.stride(1) == 1, "rowband: bf16 rows")
+        _check(self.lib.rowband_ok(rows, H, H, nh, 1, 0, ACT_CODES[act]), "rowband: shape")
+        self._check_ws(ws, self.rowband_workspace_bytes(rows, H, nh, splits), "rowband")
+        lay = []
+        for W, b, a, dz, gW, gb in layers:
+            _check(tuple(W.shape) == (H, H) and W.is_contiguous() and W.dtype == torch.bfloat16,
+                   "rowband: bf16 [H, H] weights")
+            _check(a.shape[0] >= rows and dz.shape[0] >= rows and a.stride(0) == H and
+                   dz.stride(0) == H and a.dtype == dz.dtype == torch.bfloat16,
+                   "rowband: dense bf16 activation buffers")
+            _check(gW.is_contiguous() and gW.numel() == H * H and gb.numel() == H and
+                   b.numel() == H, "rowband: gradient / bias shapes")
+            lay.append((_p(W), _p(b), _p(a), _p(dz), _p(gW), _p(gb)))
+        _check(y.numel() >= rows and wh.numel() == H, "rowband: head shapes")
+        self.lib.rowband_step(_p(X), X.stride(0), rows, H, ACT_CODES[act], lay, _p(wh), _p(bh),
+                              _p(y), float(inv_count), _p(gWh), _p(gbh), _p(ws),
+                              float(loss_scale), _p(loss_out), sgd, int(splits), self.stream)
+
     # ---------------- tiny fused MLP ----------------
     def tiny_workspace_bytes(self, rows, numel) -> int:
         return int(self.lib.tiny_mlp_workspace_bytes(rows, numel))

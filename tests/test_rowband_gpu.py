@@ -1,0 +1,153 @@
+"""Row-band step (csrc/kernels/rowband.hip): the forward, the MSE head and every activation
+gradient of a narrow square regressor in one launch, the weight gradients in one grouped launch,
+the combines (+ fused SGD) in one more.  Numerics against the plain-PyTorch fp32 oracle with the
+same bf16 rounding contract (TorchOps), and against the grouped schedule it replaces."""
+import pytest
+import torch
+
+pytestmark = pytest.mark.gpu
+
+
+def _engine(widths, rows, dev, ops, *, seed=3, lr=0.0, momentum=0.0, fuse_sgd=True, rowband=None,
+            monkeypatch=None):
+    from nnmpi_amd.engine.arena import Arena
+    from nnmpi_amd.engine.engine import MLPEngine
+    from nnmpi_amd.models.mlp import MLPSpec, reference_init
+    from nnmpi_amd.parallel.sync import NoSync
+    spec = MLPSpec(tuple(widths), "relu", "mse")
+    ar = Arena([spec.layer_shape(i) for i in range(spec.n_layers)], dev, shadow_dtype=torch.bfloat16)
+    ar.bind_model(reference_init(widths, "relu", seed=seed))
+    if monkeypatch is not None and rowband is not None:
+        monkeypatch.setenv("NNMPI_ROWBAND", "1" if rowband else "0")
+    eng = MLPEngine(spec, ar, ops, NoSync(ar), device=dev, dtype=torch.bfloat16,
+                    rows_capacity=rows, lr=lr, momentum=momentum, use_graph=False,
+                    fuse_sgd=fuse_sgd)
+    return spec, ar, eng
+
+
+def _data(rows, widths, dev="cuda"):
+    from nnmpi_amd.data import synth
+    X, Y = synth.chunked_regression(0, rows, widths[0], out=1, device=dev)
+    return X.to(torch.bfloat16), Y
+
+
+@pytest.mark.parametrize("widths,rows", [([512, 512, 512, 512, 1], 1024),
+                                         ([512, 512, 512, 512, 1], 1000),
+                                         ([512, 512, 512, 1], 8191),
+                                         ([512, 512, 1], 37)])
+def test_rowband_gradients_vs_oracle(widths, rows, monkeypatch):
+    """Every layer's weight and bias gradient, the activations, every dZ and the loss of ONE
+    row-band step (no optimizer) vs the fp32 oracle: 1e-2 relative norm per tensor (a wrong
+    scale on any layer, a missed row of a partial band or a transposed weight operand fails)."""
+    from nnmpi_amd.ops.hip_ops import HipOps
+    from nnmpi_amd.ops.torch_ops import TorchOps
+    X, Y = _data(rows, widths)
+    out = []
+    for dev, ops in (("cuda", HipOps("cuda")), ("cpu", TorchOps("cpu"))):
+        spec, ar, eng = _engine(widths, rows, dev, ops, rowband=True, monkeypatch=monkeypatch)
+        eng.load_batch(X.to(dev), Y.to(dev))
+        eng.set_scales(1.0 / rows, 1.0 / rows, 1.0)
+        L = spec.n_layers
+        with torch.no_grad():
+            if dev == "cuda":
+                assert ops.rowband_ok(rows, widths, "relu", "mse")
+                layers = [(ar.compute_weight(i), ar.bias(i), eng.acts[i][:rows], eng._dzl(i, rows),
+                           ar.grad_weight(i), ar.grad_bias(i)) for i in range(L - 1)]
+                with torch.cuda.stream(eng.stream):
+                    ops.rowband_step(eng.X[:rows], layers, ar.weight(L - 1), ar.bias(L - 1),
+                                     eng.Y[:rows], eng.inv_count, ar.grad_weight(L - 1),
+                                     ar.grad_bias(L - 1), eng.ws_rb, eng.loss_scale, eng.loss_out,
+                                     "relu")
+                eng.synchronize()
+            else:
+                eng.forward_backward()
+        rec = {("g", li, k): t.double().cpu().clone()
+               for li in range(L) for k, t in enumerate((ar.grad_weight(li), ar.grad_bias(li)))}
+        for i in range(L - 1):
+            rec[("a", i)] = eng.acts[i][:rows].double().cpu().clone()
+            rec[("dz", i)] = eng._dzl(i, rows).double().cpu().clone()
+        rec["loss"] = float(eng.loss_out[0].item())
+        out.append(rec)
+    g, r = out
+    assert g["loss"] == pytest.approx(r["loss"], rel=1e-3)
+    for key in r:
+        if key == "loss":
+            continue
+        a, b = g[key], r[key]
+        rel = float((a - b).norm() / b.norm().clamp_min(1e-30))
+        assert rel < 1e-2, (key, rel)
+
+
+def test_rowband_engine_is_taken_and_trains_like_grouped(monkeypatch):
+    """The engine takes the row-band schedule for the proxy shape; 5 SGD-momentum steps track the
+    grouped schedule's trajectory (same math, different summation order: close, not bitwise)."""
+    from nnmpi_amd.ops.hip_ops import HipOps
+    widths, rows = [512, 512, 512, 512, 1], 2048
+    X, Y = _data(rows, widths)
+    res = []
+    for rb in (True, False):
+        spec, ar, eng = _engine(widths, rows, "cuda", HipOps("cuda"), lr=1e-3, momentum=0.9,
+                                rowband=rb, monkeypatch=monkeypatch)
+        assert eng.rowband == rb
+        eng.load_batch(X, Y)
+        eng.set_scales(1.0 / rows, 1.0 / rows, 1.0)
+        losses = []
+        for _ in range(5):
+            eng.step()
+            losses.append(eng.loss())
+        res.append((losses, ar.master.double().cpu().clone()))
+    (l1, p1), (l2, p2) = res
+    for a, b in zip(l1, l2):
+        assert a == pytest.approx(b, rel=2e-3)
+    assert float((p1 - p2).norm() / p2.norm()) < 1e-4
+    assert l1[-1] < l1[0]
+
+
+def test_rowband_fused_update_is_bitwise_equal_to_separate_pass(monkeypatch):
+    """One rank: the combines apply SGD-momentum themselves; bitwise the same parameters as the
+    row-band gradients followed by the standalone optimizer pass (same slab sums, same pinned
+    update arithmetic)."""
+    from nnmpi_amd.ops.hip_ops import HipOps
+    widths, rows = [512, 512, 512, 512, 1], 1500
+    X, Y = _data(rows, widths)
+    res = []
+    for fuse in (True, False):
+        _, ar, eng = _engine(widths, rows, "cuda", HipOps("cuda"), lr=1e-3, momentum=0.9,
+                             fuse_sgd=fuse, rowband=True, monkeypatch=monkeypatch)
+        assert eng.rowband
+        eng.load_batch(X, Y)
+        eng.set_scales(1.0 / rows, 1.0 / rows, 1.0)
+        for _ in range(3):
+            eng.step()
+        eng.synchronize()
+        res.append((ar.master.clone(), ar.momentum.clone(), ar.shadow.clone(), eng.loss()))
+    for a, b in zip(res[0][:3], res[1][:3]):
+        assert torch.equal(a, b)
+    assert res[0][3] == res[1][3]
+
+
+def test_rowband_graph_replay_is_bitwise_equal_to_eager(monkeypatch):
+    from nnmpi_amd.engine.arena import Arena
+    from nnmpi_amd.engine.engine import MLPEngine
+    from nnmpi_amd.models.mlp import MLPSpec, reference_init
+    from nnmpi_amd.ops.hip_ops import HipOps
+    from nnmpi_amd.parallel.sync import NoSync
+    monkeypatch.setenv("NNMPI_ROWBAND", "1")
+    widths, rows = [512, 512, 512, 512, 1], 8192
+    X, Y = _data(rows, widths)
+    spec = MLPSpec(tuple(widths), "relu", "mse")
+    out = []
+    for graph in (False, True):
+        ar = Arena([spec.layer_shape(i) for i in range(spec.n_layers)], "cuda",
+                   shadow_dtype=torch.bfloat16)
+        ar.bind_model(reference_init(widths, "relu", seed=5))
+        eng = MLPEngine(spec, ar, HipOps("cuda"), NoSync(ar), device="cuda", dtype=torch.bfloat16,
+                        rows_capacity=rows, lr=1e-3, momentum=0.9, use_graph=graph)
+        assert eng.rowband
+        eng.load_batch(X, Y)
+        eng.set_scales(1.0 / rows, 1.0 / rows, 1.0)
+        for _ in range(4):
+            eng.step()
+        eng.synchronize()
+        out.append(ar.master.clone())
+    assert torch.equal(out[0], out[1])
