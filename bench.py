@@ -508,6 +508,10 @@ def run(a, job):
     # graph mode: steps replayed as hipGraphs of `chunk` complete consecutive steps (one
     # replay's fixed cost per chunk); every graph is captured before the timed region
     eng.prepare_steps(a.steps, chunk)
+    # the step schedule the timed engine runs (rowband.hip / grouped backward / sequential)
+    step_schedule = ("rowband" if getattr(eng, "rowband", False) else
+                     "grouped" if getattr(eng, "grouped", False) else
+                     "overlap" if getattr(eng, "overlap", False) else "sequential")
     loss0 = eng.loss()
     milestone("timed")
     barrier()
@@ -658,6 +662,7 @@ def run(a, job):
                                 if use_comm else "none"),
                        "graph": gpu and not a.no_graph, "graph_chunk": chunk,
                        "overlap": not a.no_overlap, "grouped": not a.no_group,
+                       "schedule": step_schedule,
                        "comm_mode": mode_name if use_comm else None,
                        "comm_tune_ms_per_step": tune,
                        "grad_dtype": grad_dtype if use_comm else None,

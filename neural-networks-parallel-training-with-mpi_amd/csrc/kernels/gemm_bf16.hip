@@ -731,10 +731,12 @@ __global__ void __launch_bounds__(GRP_THREADS, 4) wgrad_multi_kernel(WgradMultiP
 }
 
 int wgrad_multi_splits(int nj, int M, int N, int K) {
-  // two 512-thread blocks per CU: fill the 512 slots of the chip in one wave of blocks
   const int tiles = ((M + GRP_BM - 1) / GRP_BM) * ((N + GRP_BN - 1) / GRP_BN);
   const int ksteps = (K + GEMM_BK - 1) / GEMM_BK;
-  int s = std::max(1, 512 / std::max(1, nj * tiles));
+  // one 512-thread block per CU: measured on the proxy step (3 jobs of 16 tiles, K = 8192), 5
+  // splits 25.2 + 8.6 us (grouped weight gradients + combines) vs 10 splits 23.7 + 11.9 and 16
+  // splits 27.2 + 14.3 (profiles/r3s2_rowband_splits_ab.txt): fewer slabs, less combine traffic
+  int s = std::max(1, 256 / std::max(1, nj * tiles));
   s = std::min(s, std::max(1, ksteps / 4));   // >= 4 k-steps per split
   if (g_wgrad_splits > 0 && g_wgrad_splits < s) s = g_wgrad_splits;
   return s;

@@ -17,10 +17,10 @@
 // Block = 8 waves (512 threads) x 32 rows; wave w owns output columns [64w, 64w+64) of every
 // layer (2 x 4 v_mfma_f32_16x16x32_bf16 tiles).  LDS: two activation images (ping-pong, the
 // KMAJ image of gemm_tiles.h per 64-deep k-block: conflict-free row-fragment reads) + one
-// wave-private [64 k][64 x] XMAJ stage per wave for the dgrad's transposed weight operand
+// wave-private 8 KiB weight stage per wave: [64 k][64 x] XMAJ for the dgrad's transposed operand
 // (ds_read_b64_tr_b16 reads, the same image as the GEMMs' XMAJ operand).  The weights of the
-// forward are KMAJ for the B operand already (W[n][k], k contiguous), so they go global ->
-// registers with no LDS hop; a 4-deep register ring keeps 32 16-byte loads per lane in flight.
+// forward (KMAJ: W[n][k], k contiguous) pass through the same stage as a KMAJ image; a 4-deep
+// register ring keeps 32 16-byte loads per lane in flight.
 // Each layer's output is written into the other LDS image from the accumulators, and after the
 // block barrier copied out row-contiguously (activations and dZ are needed by the weight
 // gradients).
@@ -56,14 +56,15 @@ __device__ __forceinline__ int rb_off(int r, int k) {
 // Row-contiguous copy between an LDS image and a [rows][ld] bf16 matrix (rows row0 .. row0 +
 // nvalid - 1): each wave moves whole 128-byte row pieces (8 lanes per row).
 template <int H>
-__device__ __forceinline__ void rb_copy_out(const char* img, bf16* dst, int ld, int nvalid, int tid) {
+__device__ __forceinline__ void rb_copy_out(const char* img, bf16* dst, int ld, int nvalid, int tid,
+                                            int pol) {
   constexpr int CH = RB_ROWS * H / 8;
 #pragma unroll
   for (int it = 0; it < CH / RB_THREADS; ++it) {
     const int id = tid + it * RB_THREADS;
     const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
     const bf16x8 v = *reinterpret_cast<const bf16x8*>(img + kb * (RB_ROWS * 128) + kmaj_off(r, k8));
-    if (r < nvalid) *reinterpret_cast<bf16x8*>(dst + (long long)r * ld + kb * 64 + k8 * 8) = v;
+    if (r < nvalid) store16(reinterpret_cast<bf16x8*>(dst + (long long)r * ld + kb * 64 + k8 * 8), v, pol);
   }
 }
 
@@ -90,10 +91,14 @@ __device__ __forceinline__ void rb_load_in(char* img, const bf16* src, int ld, i
   }
 }
 
-// One forward layer of the band: out = act(in . W^T + b) into the other image.
+// One forward layer of the band: out = act(in . W^T + b) into the other image.  The wave's
+// weight rows stream through its private stage as a KMAJ image ([64 n][64 k] per k-step,
+// 8 lanes per 128-byte row piece: whole cache lines per load instruction -- loading the B
+// fragments straight from global memory touched 16 half lines per instruction and ran the
+// pass at 17 us vs 10 us for the staged dgrad pass, profiles/r3s2_rowband_variants.txt).
 template <int H, int ACT>
 __device__ __forceinline__ void rb_forward(const bf16* __restrict__ W, const float* __restrict__ bias,
-                                           const char* in, char* out, int w, int lane) {
+                                           const char* in, char* out, char* stage, int w, int lane) {
   using G = RbGeom<H>;
   const int n0 = w * G::WCOLS;
   f32x4 acc[2][G::NJ];
@@ -101,15 +106,16 @@ __device__ __forceinline__ void rb_forward(const bf16* __restrict__ W, const flo
   for (int i = 0; i < 2; ++i)
 #pragma unroll
     for (int j = 0; j < G::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // B fragment of tile j, half kk of k-step t: W[n0 + 16j + (lane & 15)][64t + 32kk + 8(lane >> 4) ..]
-  const bf16* wp = W + (long long)(n0 + (lane & 15)) * H + 8 * (lane >> 4);
-  bf16x8 ring[RB_RING][G::FLD];
-  auto issue = [&](int t, bf16x8 (&dst)[G::FLD]) {
+  // stage chunk q of k-step t: W[n0 + (lane >> 3) + 8q][64t + 8(lane & 7) .. +7]
+  const bf16* wp = W + (long long)(n0 + (lane >> 3)) * H + 8 * (lane & 7);
+  int soff[G::DLD];
 #pragma unroll
-    for (int kk = 0; kk < 2; ++kk)
+  for (int q = 0; q < G::DLD; ++q) soff[q] = kmaj_off((lane >> 3) + 8 * q, lane & 7);
+  bf16x8 ring[RB_RING][G::DLD];
+  auto issue = [&](int t, bf16x8 (&dst)[G::DLD]) {
 #pragma unroll
-      for (int j = 0; j < G::NJ; ++j)
-        dst[kk * G::NJ + j] = *reinterpret_cast<const bf16x8*>(wp + (long long)16 * j * H + 64 * t + 32 * kk);
+    for (int q = 0; q < G::DLD; ++q)
+      dst[q] = *reinterpret_cast<const bf16x8*>(wp + (long long)8 * q * H + 64 * t);
   };
   f32x4 bv[G::NJ];
 #pragma unroll
@@ -117,27 +123,29 @@ __device__ __forceinline__ void rb_forward(const bf16* __restrict__ W, const flo
 #pragma unroll
   for (int s = 0; s < RB_RING; ++s) issue(s, ring[s]);
   // (sched_barrier: keep each ring refill where it is issued -- left alone, the scheduler sinks
-  // the loads next to their MFMAs and the ring degenerates to 4 loads in flight)
+  // the loads next to their first use and the ring degenerates to a few loads in flight)
   __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
   for (int t = 0; t < G::KSTEPS; ++t) {
+#pragma unroll
+    for (int q = 0; q < G::DLD; ++q) *reinterpret_cast<bf16x8*>(stage + soff[q]) = ring[t % RB_RING][q];
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + RB_RING < G::KSTEPS) issue(t + RB_RING, ring[t % RB_RING]);
+    __builtin_amdgcn_sched_barrier(0);
     const char* kb = in + t * G::KB_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[2];
+      bf16x8 af[2], bfr[G::NJ];
 #pragma unroll
       for (int i = 0; i < 2; ++i) af[i] = read_frag<64, KMAJ>(kb, 16 * i, kk, lane);
+#pragma unroll
+      for (int j = 0; j < G::NJ; ++j) bfr[j] = read_frag<64, KMAJ>(stage, 16 * j, kk, lane);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
         for (int j = 0; j < G::NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[t % RB_RING][kk * G::NJ + j], af[i],
-                                                              acc[i][j], 0, 0, 0);
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
-    __builtin_amdgcn_sched_barrier(0);
-    // the slot just consumed is refilled for k-step t + RB_RING
-    if (t + RB_RING < G::KSTEPS) issue(t + RB_RING, ring[t % RB_RING]);
-    __builtin_amdgcn_sched_barrier(0);
   }
   // lane holds out[16i + (lane & 15)][n0 + 16j + 4(lane >> 4) .. +3]
 #pragma unroll
@@ -289,10 +297,10 @@ __global__ void __launch_bounds__(RB_THREADS) rowband_kernel(RowbandArgs p) {
   __syncthreads();
   int cur = 0;
   for (int l = 0; l < nh; ++l) {
-    rb_forward<H, ACT>(p.W[l], p.b[l], img(cur), img(cur ^ 1), cg, lane);
+    rb_forward<H, ACT>(p.W[l], p.b[l], img(cur), img(cur ^ 1), stage, cg, lane);
     __syncthreads();
     cur ^= 1;
-    rb_copy_out<H>(img(cur), p.a[l] + (long long)row0 * H, H, nvalid, tid);
+    rb_copy_out<H>(img(cur), p.a[l] + (long long)row0 * H, H, nvalid, tid, p.store_pol);
   }
   if (p.diag == 1) return;   // timing diagnostics: forward passes only
   rb_head<H, ACT>(p, img(cur), img(cur ^ 1), dls, lss, row0, nvalid, tid);
@@ -318,7 +326,7 @@ __global__ void __launch_bounds__(RB_THREADS) rowband_kernel(RowbandArgs p) {
     }
   }
   cur ^= 1;
-  rb_copy_out<H>(img(cur), p.dz[nh - 1] + (long long)row0 * H, H, nvalid, tid);
+  rb_copy_out<H>(img(cur), p.dz[nh - 1] + (long long)row0 * H, H, nvalid, tid, p.store_pol);
   // the first dgrad writes its output over the last activations the partial above still reads
   if (nh > 1) __syncthreads();
   for (int l = nh - 1; l >= 1; --l) {
@@ -326,7 +334,7 @@ __global__ void __launch_bounds__(RB_THREADS) rowband_kernel(RowbandArgs p) {
                      nvalid, cg, lane);
     __syncthreads();
     cur ^= 1;
-    rb_copy_out<H>(img(cur), p.dz[l - 1] + (long long)row0 * H, H, nvalid, tid);
+    rb_copy_out<H>(img(cur), p.dz[l - 1] + (long long)row0 * H, H, nvalid, tid, p.store_pol);
   }
 }
 
@@ -346,6 +354,8 @@ hipError_t rowband_fwd_bwd(const RowbandArgs& p0, hipStream_t s) {
   RowbandArgs p = p0;
   if (!rowband_ok(p.rows, p.H, p.H, p.nh, 1, LOSS_MSE, p.act)) return hipErrorInvalidValue;
   static const int rot = rb_env("NNMPI_RB_ROT", 1), diag = rb_env("NNMPI_RB_DIAG", 0);
+  static const int pol = rb_env("NNMPI_RB_STORE", 0);
+  p.store_pol = pol;
   p.rot = rot;
   p.diag = diag;
   using G = RbGeom<512>;
@@ -366,9 +376,16 @@ hipError_t rowband_fwd_bwd(const RowbandArgs& p0, hipStream_t s) {
 // ---- the whole step: row-band launch, grouped weight gradients, grouped combines ----------
 static size_t rb_pad4(size_t n) { return (n + 3) & ~(size_t)3; }
 
+// weight-gradient slabs per layer: explicit, else NNMPI_RB_SPLITS (A/B), else fill the chip
+static int rb_splits(int splits, int nh, int H, int rows) {
+  if (splits > 0) return splits;
+  static const int env = rb_env("NNMPI_RB_SPLITS", 0);
+  return env > 0 ? env : wgrad_multi_splits(nh, H, H, rows);
+}
+
 size_t rowband_workspace_bytes(int rows, int H, int nh, int splits) {
   const size_t G = (size_t)rowband_blocks(rows);
-  const int S = splits > 0 ? splits : wgrad_multi_splits(nh, H, H, rows);
+  const int S = rb_splits(splits, nh, H, rows);
   const size_t head = G * H + rb_pad4(G) + rb_pad4(G);
   return (head + (size_t)nh * S * ((size_t)H * H + H)) * sizeof(float);
 }
@@ -386,7 +403,7 @@ hipError_t rowband_step(const RowbandStep& st0, hipStream_t s) {
   float* slabs = p.loss_part + rb_pad4(G);
   hipError_t e = rowband_fwd_bwd(p, s);
   if (e != hipSuccess) return e;
-  const int S = st.splits > 0 ? st.splits : wgrad_multi_splits(nh, H, H, p.rows);
+  const int S = rb_splits(st.splits, nh, H, p.rows);
   WgradArgs jobs[RB_MAXL];
   SlabReduce red[RB_MAXL + 1];
   for (int l = 0; l < nh; ++l) {

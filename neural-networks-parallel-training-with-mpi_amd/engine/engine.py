@@ -117,10 +117,10 @@ class MLPEngine:
         # every combine (+ the fused update on one rank) in a third -- see rowband.hip.  Taken
         # whenever the gradient is reduced after the backward (one rank, the inline all-reduce,
         # ZeRO-1): it produces every layer's gradient at once, so there is nothing for a
-        # per-bucket overlapped schedule to hide.  Opt-in (NNMPI_ROWBAND=1) until it beats the
-        # grouped schedule on the proxy step (docs/PERF.md).
+        # per-bucket overlapped schedule to hide.  NNMPI_ROWBAND=0 keeps the grouped schedule
+        # (proxy step 0.082 vs 0.094 ms, profiles/r3s2_rowband_*).
         self.rowband = (self.overlap and dtype == torch.bfloat16 and inline_sync and
-                        hasattr(ops, "rowband_ok") and os.environ.get("NNMPI_ROWBAND", "0") == "1"
+                        hasattr(ops, "rowband_ok") and os.environ.get("NNMPI_ROWBAND", "1") != "0"
                         and ops.rowband_ok(self.R, w, self.act, spec.loss))
         self.ws_rb = (torch.zeros(ops.rowband_workspace_bytes(self.R, w[1], L - 1) // 4 + 64,
                                   dtype=torch.float32, device=dev) if self.rowband else None)

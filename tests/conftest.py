@@ -11,6 +11,19 @@ if ROOT not in sys.path:
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")
     config.addinivalue_line("markers", "slow: longer multi-process runs")
+    config.addinivalue_line("markers", "rowband: runs with the row-band step schedule enabled "
+                            "(the production default for 512-wide MSE regressors)")
+
+
+@pytest.fixture(autouse=True)
+def _pin_step_schedule(request, monkeypatch):
+    """Most engine tests compare two schedules of the same step bitwise (grouped vs ungrouped,
+    inline vs overlapped all-reduce, eager vs graph); they pin the grouped backward, which every
+    comm mode can run.  The row-band step (csrc/kernels/rowband.hip, the default for 512-wide MSE
+    regressors with an inline / single-rank gradient sync) has a different summation order, so
+    its own tests -- and the bench tests of the driver's default path -- opt in with the
+    ``rowband`` marker."""
+    monkeypatch.setenv("NNMPI_ROWBAND", "1" if "rowband" in request.keywords else "0")
 
 
 def pytest_report_header(config):

@@ -130,6 +130,7 @@ def test_bench_more_gpus_than_visible_fails():
 
 
 @pytest.mark.gpu
+@pytest.mark.rowband
 def test_bench_two_rank_rehearsal_on_one_gpu():
     """The whole multi-rank bench path -- tune of inline / ZeRO-1 / overlap schedules with the
     RCCL collectives captured in hipGraphs, timed region, efficiency / comm-only / strong-scaling
@@ -148,6 +149,7 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
 
 
 @pytest.mark.gpu
+@pytest.mark.rowband
 def test_bench_driver_torchrun_form_on_one_gpu():
     """The driver's exact N-GPU launch (torch.distributed.run ... bench.py --gpus N) with the GPU
     ranks sharing the one device: per-rank supervisors under torchrun's agent store, RCCL ranks,

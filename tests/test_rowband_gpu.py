@@ -5,7 +5,7 @@ same bf16 rounding contract (TorchOps), and against the grouped schedule it repl
 import pytest
 import torch
 
-pytestmark = pytest.mark.gpu
+pytestmark = [pytest.mark.gpu, pytest.mark.rowband]
 
 
 def _engine(widths, rows, dev, ops, *, seed=3, lr=0.0, momentum=0.0, fuse_sgd=True, rowband=None,
@@ -151,3 +151,18 @@ def test_rowband_graph_replay_is_bitwise_equal_to_eager(monkeypatch):
         eng.synchronize()
         out.append(ar.master.clone())
     assert torch.equal(out[0], out[1])
+
+
+def test_bench_default_proxy_step_runs_the_rowband_schedule():
+    """The driver's default 1-GPU bench (the BASELINE proxy) times the row-band step."""
+    import json
+    import os
+    import subprocess
+    import sys
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    r = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--steps", "6",
+                        "--warmup", "2"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0, r.stderr[-3000:]
+    d = json.loads(r.stdout.strip().splitlines()[-1])
+    assert d["config"]["schedule"] == "rowband"
+    assert d["replicas_bitwise_equal"] is True and d["final_loss"] == d["final_loss"]
