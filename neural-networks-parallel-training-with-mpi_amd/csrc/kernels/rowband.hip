@@ -93,9 +93,10 @@ __device__ __forceinline__ void rb_load_in(char* img, const bf16* src, int ld, i
 
 // One forward layer of the band: out = act(in . W^T + b) into the other image.  The wave's
 // weight rows stream through its private stage as a KMAJ image ([64 n][64 k] per k-step,
-// 8 lanes per 128-byte row piece: whole cache lines per load instruction -- loading the B
-// fragments straight from global memory touched 16 half lines per instruction and ran the
-// pass at 17 us vs 10 us for the staged dgrad pass, profiles/r3s2_rowband_variants.txt).
+// 8 lanes per 128-byte row piece: whole cache lines per load instruction).  Loading the B
+// fragments straight from global memory (16 rows x 32-64 B per load instruction, two k
+// permutations tried) ran the three forward passes in 51 us vs 29 us staged
+// (profiles/r3s2_rowband_ab.txt, r3s2_rowband_fwd_direct_and_wgrad_ns_ab.txt).
 template <int H, int ACT>
 __device__ __forceinline__ void rb_forward(const bf16* __restrict__ W, const float* __restrict__ bias,
                                            const char* in, char* out, char* stage, int w, int lane) {
@@ -148,71 +149,6 @@ __device__ __forceinline__ void rb_forward(const bf16* __restrict__ W, const flo
     }
   }
   // lane holds out[16i + (lane & 15)][n0 + 16j + 4(lane >> 4) .. +3]
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < G::NJ; ++j) {
-      const f32x4 v = acc[i][j] + bv[j];
-      bf16x4 o;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = (bf16)act_fwd_t<ACT>(v[r]);
-      *reinterpret_cast<bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * j + 4 * (lane >> 4))) = o;
-    }
-}
-
-// Forward variant without the LDS stage (NNMPI_RB_FWD=1, A/B): the weights go global ->
-// registers straight into B fragments, with the k index of fragment half kk permuted to
-// k = 16 * (lane >> 4) + 8 * kk + e, so the two halves of a lane are 32 contiguous bytes and the
-// two load instructions of a row group cover whole 128-byte lines back to back (the direct form
-// with k = 32 * kk + 8 * (lane >> 4) + e touched 16 half lines per instruction: 17 us per pass).
-// The A fragments are read from the image with the same permutation; the result differs from
-// the staged form only in the fp32 summation order.
-template <int H, int ACT>
-__device__ __forceinline__ void rb_forward_direct(const bf16* __restrict__ W,
-                                                  const float* __restrict__ bias, const char* in,
-                                                  char* out, int w, int lane) {
-  using G = RbGeom<H>;
-  const int n0 = w * G::WCOLS;
-  f32x4 acc[2][G::NJ];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < G::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  const bf16* wp = W + (long long)(n0 + (lane & 15)) * H + 16 * (lane >> 4);
-  bf16x8 ring[RB_RING][G::FLD];
-  auto issue = [&](int t, bf16x8 (&dst)[G::FLD]) {
-#pragma unroll
-    for (int j = 0; j < G::NJ; ++j)
-#pragma unroll
-      for (int kk = 0; kk < 2; ++kk)
-        dst[kk * G::NJ + j] = *reinterpret_cast<const bf16x8*>(wp + (long long)16 * j * H + 64 * t + 8 * kk);
-  };
-  f32x4 bv[G::NJ];
-#pragma unroll
-  for (int j = 0; j < G::NJ; ++j) bv[j] = *reinterpret_cast<const f32x4*>(bias + n0 + 16 * j + 4 * (lane >> 4));
-#pragma unroll
-  for (int s = 0; s < RB_RING; ++s) issue(s, ring[s]);
-  __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-  for (int t = 0; t < G::KSTEPS; ++t) {
-    const char* kb = in + t * G::KB_BYTES;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[2];
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-        af[i] = *reinterpret_cast<const bf16x8*>(kb + kmaj_off(16 * i + (lane & 15), 2 * (lane >> 4) + kk));
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < G::NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[t % RB_RING][kk * G::NJ + j], af[i],
-                                                              acc[i][j], 0, 0, 0);
-    }
-    __builtin_amdgcn_sched_barrier(0);
-    if (t + RB_RING < G::KSTEPS) issue(t + RB_RING, ring[t % RB_RING]);
-    __builtin_amdgcn_sched_barrier(0);
-  }
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -339,7 +275,7 @@ __device__ __forceinline__ void rb_head(const RowbandArgs& p, const char* in, ch
   }
 }
 
-template <int H, int ACT, int FWD>
+template <int H, int ACT>
 __global__ void __launch_bounds__(RB_THREADS) rowband_kernel(RowbandArgs p) {
   using G = RbGeom<H>;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
@@ -362,8 +298,7 @@ __global__ void __launch_bounds__(RB_THREADS) rowband_kernel(RowbandArgs p) {
   __syncthreads();
   int cur = 0;
   for (int l = 0; l < nh; ++l) {
-    if constexpr (FWD == 1) rb_forward_direct<H, ACT>(p.W[l], p.b[l], img(cur), img(cur ^ 1), cg, lane);
-    else rb_forward<H, ACT>(p.W[l], p.b[l], img(cur), img(cur ^ 1), stage, cg, lane);
+    rb_forward<H, ACT>(p.W[l], p.b[l], img(cur), img(cur ^ 1), stage, cg, lane);
     __syncthreads();
     cur ^= 1;
     rb_copy_out<H>(img(cur), p.a[l] + (long long)row0 * H, H, nvalid, tid, p.store_pol);
@@ -426,18 +361,15 @@ hipError_t rowband_fwd_bwd(const RowbandArgs& p0, hipStream_t s) {
   p.diag = diag;
   using G = RbGeom<512>;
   using Fn = void (*)(RowbandArgs);
-  static const Fn fns[2][3] = {
-      {rowband_kernel<512, ACT_NONE, 0>, rowband_kernel<512, ACT_RELU, 0>, rowband_kernel<512, ACT_TANH, 0>},
-      {rowband_kernel<512, ACT_NONE, 1>, rowband_kernel<512, ACT_RELU, 1>, rowband_kernel<512, ACT_TANH, 1>}};
+  static const Fn fns[3] = {rowband_kernel<512, ACT_NONE>, rowband_kernel<512, ACT_RELU>,
+                            rowband_kernel<512, ACT_TANH>};
   static bool attr = false;
   if (!attr) {
-    for (auto& row : fns)
-      for (Fn f : row)
-        (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
+    for (Fn f : fns)
+      (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
     attr = true;
   }
-  static const int fwd = rb_env("NNMPI_RB_FWD", 0) == 1 ? 1 : 0;
-  const Fn f = fns[fwd][p.act == ACT_RELU ? 1 : p.act == ACT_TANH ? 2 : 0];
+  const Fn f = fns[p.act == ACT_RELU ? 1 : p.act == ACT_TANH ? 2 : 0];
   hipLaunchKernelGGL(f, dim3(rowband_blocks(p.rows)), dim3(RB_THREADS), G::SMEM, s, p);
   return hipGetLastError();
 }
