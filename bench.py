@@ -509,9 +509,7 @@ def run(a, job):
     # replay's fixed cost per chunk); every graph is captured before the timed region
     eng.prepare_steps(a.steps, chunk)
     # the step schedule the timed engine runs (rowband.hip / grouped backward / sequential)
-    step_schedule = ("rowband" if getattr(eng, "rowband", False) else
-                     "grouped" if getattr(eng, "grouped", False) else
-                     "overlap" if getattr(eng, "overlap", False) else "sequential")
+    step_schedule = eng.schedule_name()
     loss0 = eng.loss()
     milestone("timed")
     barrier()

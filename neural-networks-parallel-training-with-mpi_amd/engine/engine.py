@@ -124,6 +124,10 @@ class MLPEngine:
                         and ops.rowband_ok(self.R, w, self.act, spec.loss))
         self.ws_rb = (torch.zeros(ops.rowband_workspace_bytes(self.R, w[1], L - 1) // 4 + 64,
                                   dtype=torch.float32, device=dev) if self.rowband else None)
+        # A band's passes cost the same whatever the number of bands (per-CU bound: 47 us at
+        # 1,024 rows as at 8,192, profiles/r3s2_rowband_pmc.txt), so small batches (strong-scaling
+        # shards, mini-batches) keep the grouped schedule: 0.053 vs ~0.064 ms at 1,024 rows.
+        self.rowband_min_rows = int(os.environ.get("NNMPI_ROWBAND_MIN_ROWS", "6144"))
         if self.is_cuda:
             self.ev_wfree = [torch.cuda.Event(enable_timing=False) for _ in range(L)]
         # bf16-payload overlapped schedule: per-bucket updates read the bf16 payload
@@ -415,7 +419,7 @@ class MLPEngine:
     # on the critical path.  With one rank the update of the whole arena runs once at the end.
     def _step_body_overlap(self, first: bool):
         rows, ops, ar, L = self.rows, self.ops, self.arena, self.L
-        if self.rowband:
+        if self.uses_rowband(rows):
             return self._step_body_rowband(first)
         if self.grouped:
             return self._step_body_grouped(first)
@@ -531,6 +535,19 @@ class MLPEngine:
         for i in unfused:
             s, e = ar.layer_range[i]
             ops.sgd(ar, self.hp, self.nesterov, first, offset=s, numel=e - s)
+
+    def uses_rowband(self, rows: Optional[int] = None) -> bool:
+        """True when a step of ``rows`` rows (default: the loaded batch) runs the row-band step."""
+        rows = self.rows if rows is None else rows
+        return bool(self.rowband and rows >= max(1, self.rowband_min_rows))
+
+    def schedule_name(self) -> str:
+        """The step schedule a batch of the loaded size runs (bench / result reports)."""
+        if self.uses_rowband():
+            return "rowband"
+        if self.grouped:
+            return "grouped"
+        return "overlap" if self.overlap else "sequential"
 
     # Row-band schedule (see rowband.hip): three launches per step.  One rank: the combine
     # applies the SGD update; several ranks: the combine writes the gradient, then the inline

@@ -395,7 +395,8 @@ def _run(j: Job) -> TrainResult:
     res.schedule = {"device": j.device.type, "comm": j.comm_kind, "sync": type(sync).__name__,
                     "grad_dtype": grad_payload(cfg, j.device.type, arena.numel),
                     "inline": bool(getattr(sync, "inline", False)),
-                    "grouped": bool(eng.grouped), "deferred_updates": len(eng._defer_plan),
+                    "grouped": bool(eng.grouped), "rowband": eng.uses_rowband(rows_local),
+                    "deferred_updates": len(eng._defer_plan),
                     "graph": bool(eng.use_graph)}
     n_micro = max(1, math.ceil(max_rows / mb)) if mb else 1
     steps_per_epoch = math.ceil(n_micro / K) if K > 1 else (1 if not bs else n_micro)

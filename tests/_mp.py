@@ -21,7 +21,8 @@ def _entry(rank, world, port, cfg, outdir, fn_name):
     from nnmpi_amd.engine import trainer
     res = getattr(trainer, fn_name)(cfg)
     torch.save({"losses": res.losses, "global_losses": res.global_losses, "val": res.val_losses,
-                "final": res.final_params, "rows": res.rows, "steps": res.steps},
+                "final": res.final_params, "rows": res.rows, "steps": res.steps,
+                "schedule": res.schedule},
                os.path.join(outdir, f"r{rank}.pt"))
 
 

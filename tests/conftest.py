@@ -24,6 +24,9 @@ def _pin_step_schedule(request, monkeypatch):
     its own tests -- and the bench tests of the driver's default path -- opt in with the
     ``rowband`` marker."""
     monkeypatch.setenv("NNMPI_ROWBAND", "1" if "rowband" in request.keywords else "0")
+    if "rowband" in request.keywords:
+        # (the tests' batches are small; production takes the row-band step from 6,144 rows)
+        monkeypatch.setenv("NNMPI_ROWBAND_MIN_ROWS", "0")
 
 
 def pytest_report_header(config):

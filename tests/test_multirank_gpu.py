@@ -311,3 +311,23 @@ def test_rccl_one_rank_failure_ends_every_rank():
     for r in range(world):
         if r != fail:
             assert "nnmpi watchdog" in errs[r] or "RCCL" in errs[r], errs[r][-2000:]
+
+
+@pytest.mark.rowband
+def test_rowband_rccl_two_ranks_inline_and_zero1_match_one_rank():
+    """The row-band step at P=2 through RCCL (inline all-reduce, and ZeRO-1's reduce-scatter /
+    sharded update / all-gather): replicas bitwise equal, the two syncs bitwise equal to each
+    other (a + b either way), and the P=1 trajectory of the same global data within the bf16
+    contract (the split of the batch changes the fp32 summation order of the weight gradients)."""
+    kw = dict(widths=[512, 512, 512, 1], n_features=512, n_samples=4096, scaling="global",
+              averaging="weighted", lr=1e-4, nepochs=4)
+    one = run_ranks_proc(_cfg(comm="none", **kw), 1)
+    a = run_ranks_proc(_cfg(comm="native", comm_mode="inline", **kw), 2, env_per_rank=rccl_env)
+    b = run_ranks_proc(_cfg(comm="native", comm_mode="inline", shard_optimizer=True, **kw), 2,
+                       env_per_rank=rccl_env)
+    assert one[0]["schedule"]["rowband"] and a[0]["schedule"]["rowband"] and b[0]["schedule"]["rowband"]
+    _replicas_equal(a)
+    _replicas_equal(b)
+    assert torch.equal(a[0]["final"], b[0]["final"])
+    torch.testing.assert_close(a[0]["final"], one[0]["final"], rtol=2e-2, atol=2e-3)
+

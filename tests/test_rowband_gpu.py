@@ -9,14 +9,14 @@ pytestmark = [pytest.mark.gpu, pytest.mark.rowband]
 
 
 def _engine(widths, rows, dev, ops, *, seed=3, lr=0.0, momentum=0.0, fuse_sgd=True, rowband=None,
-            monkeypatch=None):
+            monkeypatch=None, act="relu"):
     from nnmpi_amd.engine.arena import Arena
     from nnmpi_amd.engine.engine import MLPEngine
     from nnmpi_amd.models.mlp import MLPSpec, reference_init
     from nnmpi_amd.parallel.sync import NoSync
-    spec = MLPSpec(tuple(widths), "relu", "mse")
+    spec = MLPSpec(tuple(widths), act, "mse")
     ar = Arena([spec.layer_shape(i) for i in range(spec.n_layers)], dev, shadow_dtype=torch.bfloat16)
-    ar.bind_model(reference_init(widths, "relu", seed=seed))
+    ar.bind_model(reference_init(widths, act, seed=seed))
     if monkeypatch is not None and rowband is not None:
         monkeypatch.setenv("NNMPI_ROWBAND", "1" if rowband else "0")
     eng = MLPEngine(spec, ar, ops, NoSync(ar), device=dev, dtype=torch.bfloat16,
@@ -31,11 +31,13 @@ def _data(rows, widths, dev="cuda"):
     return X.to(torch.bfloat16), Y
 
 
-@pytest.mark.parametrize("widths,rows", [([512, 512, 512, 512, 1], 1024),
-                                         ([512, 512, 512, 512, 1], 1000),
-                                         ([512, 512, 512, 1], 8191),
-                                         ([512, 512, 1], 37)])
-def test_rowband_gradients_vs_oracle(widths, rows, monkeypatch):
+@pytest.mark.parametrize("widths,rows,act", [([512, 512, 512, 512, 1], 1024, "relu"),
+                                             ([512, 512, 512, 512, 1], 1000, "relu"),
+                                             ([512, 512, 512, 1], 8191, "relu"),
+                                             ([512, 512, 1], 37, "relu"),
+                                             ([512, 512, 512, 512, 1], 777, "tanh"),
+                                             ([512] * 5 + [1], 2048, "relu")])
+def test_rowband_gradients_vs_oracle(widths, rows, act, monkeypatch):
     """Every layer's weight and bias gradient, the activations, every dZ and the loss of ONE
     row-band step (no optimizer) vs the fp32 oracle: 1e-2 relative norm per tensor (a wrong
     scale on any layer, a missed row of a partial band or a transposed weight operand fails)."""
@@ -44,20 +46,21 @@ def test_rowband_gradients_vs_oracle(widths, rows, monkeypatch):
     X, Y = _data(rows, widths)
     out = []
     for dev, ops in (("cuda", HipOps("cuda")), ("cpu", TorchOps("cpu"))):
-        spec, ar, eng = _engine(widths, rows, dev, ops, rowband=True, monkeypatch=monkeypatch)
+        spec, ar, eng = _engine(widths, rows, dev, ops, rowband=True, monkeypatch=monkeypatch,
+                                act=act)
         eng.load_batch(X.to(dev), Y.to(dev))
         eng.set_scales(1.0 / rows, 1.0 / rows, 1.0)
         L = spec.n_layers
         with torch.no_grad():
             if dev == "cuda":
-                assert ops.rowband_ok(rows, widths, "relu", "mse")
+                assert ops.rowband_ok(rows, widths, act, "mse")
                 layers = [(ar.compute_weight(i), ar.bias(i), eng.acts[i][:rows], eng._dzl(i, rows),
                            ar.grad_weight(i), ar.grad_bias(i)) for i in range(L - 1)]
                 with torch.cuda.stream(eng.stream):
                     ops.rowband_step(eng.X[:rows], layers, ar.weight(L - 1), ar.bias(L - 1),
                                      eng.Y[:rows], eng.inv_count, ar.grad_weight(L - 1),
                                      ar.grad_bias(L - 1), eng.ws_rb, eng.loss_scale, eng.loss_out,
-                                     "relu")
+                                     act)
                 eng.synchronize()
             else:
                 eng.forward_backward()
@@ -166,3 +169,24 @@ def test_bench_default_proxy_step_runs_the_rowband_schedule():
     d = json.loads(r.stdout.strip().splitlines()[-1])
     assert d["config"]["schedule"] == "rowband"
     assert d["replicas_bitwise_equal"] is True and d["final_loss"] == d["final_loss"]
+
+
+def test_small_batches_keep_the_grouped_schedule(monkeypatch):
+    """Below NNMPI_ROWBAND_MIN_ROWS (default 6,144) a step runs the grouped schedule: a band's
+    passes cost the same however few bands there are, so small batches are faster grouped."""
+    from nnmpi_amd.ops.hip_ops import HipOps
+    monkeypatch.delenv("NNMPI_ROWBAND_MIN_ROWS", raising=False)
+    widths = [512, 512, 512, 512, 1]
+    _, _, eng = _engine(widths, 8192, "cuda", HipOps("cuda"), rowband=True, monkeypatch=monkeypatch)
+    X, Y = _data(8192, widths)
+    eng.load_batch(X[:1024], Y[:1024])
+    assert eng.rowband and not eng.uses_rowband() and eng.schedule_name() == "grouped"
+    eng.set_scales(1.0 / 1024, 1.0 / 1024, 1.0)
+    eng.step()
+    l_small = eng.loss()
+    eng.load_batch(X, Y)
+    assert eng.uses_rowband() and eng.schedule_name() == "rowband"
+    eng.set_scales(1.0 / 8192, 1.0 / 8192, 1.0)
+    eng.step()
+    assert l_small == l_small and eng.loss() == eng.loss()
+
