@@ -154,9 +154,6 @@ struct RowbandArgs {
   const float* y;           // targets [rows]
   float inv_count;
   float* wslab; float* bslab; float* loss_part;   // per-band head partials (rowband_blocks)
-  int rot = 1;              // column groups rotated by block (A/B: NNMPI_RB_ROT=0)
-  int diag = 0;             // timing diagnostics: 1 = forward passes only
-  int store_pol = 0;        // activation / dZ copy-out stores: 0 plain, 1 nt, 2 sc1 (A/B)
 };
 int rowband_blocks(int rows);
 bool rowband_ok(int rows, int H, int in, int nh, int out, int loss, int act);

@@ -56,15 +56,14 @@ __device__ __forceinline__ int rb_off(int r, int k) {
 // Row-contiguous copy between an LDS image and a [rows][ld] bf16 matrix (rows row0 .. row0 +
 // nvalid - 1): each wave moves whole 128-byte row pieces (8 lanes per row).
 template <int H>
-__device__ __forceinline__ void rb_copy_out(const char* img, bf16* dst, int ld, int nvalid, int tid,
-                                            int pol) {
+__device__ __forceinline__ void rb_copy_out(const char* img, bf16* dst, int ld, int nvalid, int tid) {
   constexpr int CH = RB_ROWS * H / 8;
 #pragma unroll
   for (int it = 0; it < CH / RB_THREADS; ++it) {
     const int id = tid + it * RB_THREADS;
     const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
     const bf16x8 v = *reinterpret_cast<const bf16x8*>(img + kb * (RB_ROWS * 128) + kmaj_off(r, k8));
-    if (r < nvalid) store16(reinterpret_cast<bf16x8*>(dst + (long long)r * ld + kb * 64 + k8 * 8), v, pol);
+    if (r < nvalid) *reinterpret_cast<bf16x8*>(dst + (long long)r * ld + kb * 64 + k8 * 8) = v;
   }
 }
 
@@ -289,10 +288,9 @@ __global__ void __launch_bounds__(RB_THREADS) rowband_kernel(RowbandArgs p) {
   const int row0 = blk * RB_ROWS;
   const int nvalid = min(RB_ROWS, p.rows - row0);
   const int nh = p.nh;
-  // column group of this wave: rotated by the block index, so the 32 CUs of an XCD, which run
-  // their passes in near lock-step, read different weight rows (different L2 channels) at any
-  // moment instead of all requesting the same lines together (p.rot = 0: wave w -> group w)
-  const int cg = (w + (p.rot ? blk : 0)) & (RB_WAVES - 1);
+  // column group of this wave, rotated by the block index (measured neutral against w -> w,
+  // profiles/r3s2_rowband_ab.txt; kept: it spreads the XCD's concurrent weight reads)
+  const int cg = (w + blk) & (RB_WAVES - 1);
 
   rb_load_in<H>(img(0), p.X + (long long)row0 * p.ldx, p.ldx, nvalid, tid);
   __syncthreads();
@@ -301,9 +299,8 @@ __global__ void __launch_bounds__(RB_THREADS) rowband_kernel(RowbandArgs p) {
     rb_forward<H, ACT>(p.W[l], p.b[l], img(cur), img(cur ^ 1), stage, cg, lane);
     __syncthreads();
     cur ^= 1;
-    rb_copy_out<H>(img(cur), p.a[l] + (long long)row0 * H, H, nvalid, tid, p.store_pol);
+    rb_copy_out<H>(img(cur), p.a[l] + (long long)row0 * H, H, nvalid, tid);
   }
-  if (p.diag == 1) return;   // timing diagnostics: forward passes only
   rb_head<H, ACT>(p, img(cur), img(cur ^ 1), dls, lss, row0, nvalid, tid);
   __syncthreads();
   // head weight-gradient partial of this band: column tid, rows in order
@@ -327,7 +324,7 @@ __global__ void __launch_bounds__(RB_THREADS) rowband_kernel(RowbandArgs p) {
     }
   }
   cur ^= 1;
-  rb_copy_out<H>(img(cur), p.dz[nh - 1] + (long long)row0 * H, H, nvalid, tid, p.store_pol);
+  rb_copy_out<H>(img(cur), p.dz[nh - 1] + (long long)row0 * H, H, nvalid, tid);
   // the first dgrad writes its output over the last activations the partial above still reads
   if (nh > 1) __syncthreads();
   for (int l = nh - 1; l >= 1; --l) {
@@ -335,7 +332,7 @@ __global__ void __launch_bounds__(RB_THREADS) rowband_kernel(RowbandArgs p) {
                      nvalid, cg, lane);
     __syncthreads();
     cur ^= 1;
-    rb_copy_out<H>(img(cur), p.dz[l - 1] + (long long)row0 * H, H, nvalid, tid, p.store_pol);
+    rb_copy_out<H>(img(cur), p.dz[l - 1] + (long long)row0 * H, H, nvalid, tid);
   }
 }
 
@@ -354,11 +351,7 @@ static int rb_env(const char* name, int dflt) {
 hipError_t rowband_fwd_bwd(const RowbandArgs& p0, hipStream_t s) {
   RowbandArgs p = p0;
   if (!rowband_ok(p.rows, p.H, p.H, p.nh, 1, LOSS_MSE, p.act)) return hipErrorInvalidValue;
-  static const int rot = rb_env("NNMPI_RB_ROT", 1), diag = rb_env("NNMPI_RB_DIAG", 0);
-  static const int pol = rb_env("NNMPI_RB_STORE", 0);
-  p.store_pol = pol;
-  p.rot = rot;
-  p.diag = diag;
+
   using G = RbGeom<512>;
   using Fn = void (*)(RowbandArgs);
   static const Fn fns[3] = {rowband_kernel<512, ACT_NONE>, rowband_kernel<512, ACT_RELU>,

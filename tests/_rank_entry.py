@@ -17,5 +17,6 @@ from nnmpi_amd.utils.config import TrainConfig  # noqa: E402
 cfg = TrainConfig(**json.loads(sys.argv[1]))
 res = trainer.run_worker(cfg)
 torch.save({"losses": res.losses, "global_losses": res.global_losses, "val": res.val_losses,
-            "final": res.final_params, "rows": res.rows, "steps": res.steps},
+            "final": res.final_params, "rows": res.rows, "steps": res.steps,
+            "schedule": res.schedule},
            os.path.join(sys.argv[2], f"r{res.rank}.pt"))
