@@ -15,15 +15,15 @@
 // become 3.
 //
 // Block = 8 waves (512 threads) x 32 rows; wave w owns output columns [64w, 64w+64) of every
-// layer (2 x 4 v_mfma_f32_16x16x32_bf16 tiles).  LDS: two activation images (ping-pong, the
-// KMAJ image of gemm_tiles.h per 64-deep k-block: conflict-free row-fragment reads) + one
-// wave-private 8 KiB weight stage per wave: [64 k][64 x] XMAJ for the dgrad's transposed operand
-// (ds_read_b64_tr_b16 reads, the same image as the GEMMs' XMAJ operand).  The weights of the
-// forward (KMAJ: W[n][k], k contiguous) pass through the same stage as a KMAJ image; a 4-deep
-// register ring keeps 32 16-byte loads per lane in flight.
-// Each layer's output is written into the other LDS image from the accumulators, and after the
-// block barrier copied out row-contiguously (activations and dZ are needed by the weight
-// gradients).
+// layer (2 x 4 v_mfma_f32_16x16x32_bf16 tiles).  LDS (the whole 160 KiB): ONE activation image
+// of the band (the KMAJ image of gemm_tiles.h per 64-deep k-block: conflict-free row-fragment
+// reads), updated in place by every pass -- a barrier separates a pass's main loop from its
+// epilogue -- and two 8 KiB weight stages per wave: KMAJ [64 n][64 k] for the forward's B
+// operand, XMAJ [64 k][64 x] for the dgrad's transposed operand (ds_read_b64_tr_b16, the GEMMs'
+// XMAJ image).  The weights stream global -> registers (whole 128-byte lines per load
+// instruction, a 3-deep ring of k-steps pinned with sched_barrier) -> the stage buffer the
+// fragment reads of the current k-step are not using.  After each pass the image is copied out
+// row-contiguously (activations and dZ are needed by the weight gradients).
 #include "gemm_tiles.h"
 
 namespace nnmpi {
@@ -31,7 +31,7 @@ namespace nnmpi {
 constexpr int RB_ROWS = 32;
 constexpr int RB_WAVES = 8;
 constexpr int RB_THREADS = 64 * RB_WAVES;
-constexpr int RB_RING = 4;   // k-steps of weight loads in flight per lane
+constexpr int RB_RING = 3;   // k-steps of weight loads in flight per lane (beyond the staged one)
 
 template <int H>
 struct RbGeom {
@@ -42,8 +42,7 @@ struct RbGeom {
   static constexpr int KB_BYTES = RB_ROWS * 128;   // one 64-deep k-block of an image
   static constexpr int BUF = RB_ROWS * H * 2;      // one activation image
   static constexpr int STAGE = 64 * WCOLS * 2;     // wave-private dgrad weight stage
-  static constexpr int SCRATCH = 2 * RB_ROWS * 4;  // head: per-row dlogit + loss
-  static constexpr int SMEM = 2 * BUF + RB_WAVES * STAGE + SCRATCH;
+  static constexpr int SMEM = BUF + RB_WAVES * 2 * STAGE;   // 160 KiB: the whole LDS
   static constexpr int FLD = 2 * NJ;               // forward: weight loads per lane per k-step
   static constexpr int DLD = WCOLS / 8;            // dgrad: 16-B stage chunks per lane per k-step
 };
@@ -111,7 +110,8 @@ __device__ __forceinline__ void rb_forward(const bf16* __restrict__ W, const flo
   int soff[G::DLD];
 #pragma unroll
   for (int q = 0; q < G::DLD; ++q) soff[q] = kmaj_off((lane >> 3) + 8 * q, lane & 7);
-  bf16x8 ring[RB_RING][G::DLD];
+  constexpr int RING = RB_RING;
+  bf16x8 ring[RING][G::DLD];
   auto issue = [&](int t, bf16x8 (&dst)[G::DLD]) {
 #pragma unroll
     for (int q = 0; q < G::DLD; ++q)
@@ -121,17 +121,22 @@ __device__ __forceinline__ void rb_forward(const bf16* __restrict__ W, const flo
 #pragma unroll
   for (int j = 0; j < G::NJ; ++j) bv[j] = *reinterpret_cast<const f32x4*>(bias + n0 + 16 * j + 4 * (lane >> 4));
 #pragma unroll
-  for (int s = 0; s < RB_RING; ++s) issue(s, ring[s]);
+  for (int s = 0; s < RING; ++s) issue(s, ring[s]);
   // (sched_barrier: keep each ring refill where it is issued -- left alone, the scheduler sinks
   // the loads next to their first use and the ring degenerates to a few loads in flight)
   __builtin_amdgcn_sched_barrier(0);
+  {
+    // two stage buffers: the stage write of k-step t+1 is issued behind the fragment reads of
+    // k-step t, so the MFMAs of t wait for their reads only, not for the next write
+#pragma unroll
+    for (int q = 0; q < G::DLD; ++q) *reinterpret_cast<bf16x8*>(stage + soff[q]) = ring[0][q];
+    __builtin_amdgcn_sched_barrier(0);
+    if (RING < G::KSTEPS) issue(RING, ring[0]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
 #pragma unroll
   for (int t = 0; t < G::KSTEPS; ++t) {
-#pragma unroll
-    for (int q = 0; q < G::DLD; ++q) *reinterpret_cast<bf16x8*>(stage + soff[q]) = ring[t % RB_RING][q];
-    __builtin_amdgcn_sched_barrier(0);
-    if (t + RB_RING < G::KSTEPS) issue(t + RB_RING, ring[t % RB_RING]);
-    __builtin_amdgcn_sched_barrier(0);
+    const char* st = stage + (t & 1) * G::STAGE;
     const char* kb = in + t * G::KB_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -139,7 +144,22 @@ __device__ __forceinline__ void rb_forward(const bf16* __restrict__ W, const flo
 #pragma unroll
       for (int i = 0; i < 2; ++i) af[i] = read_frag<64, KMAJ>(kb, 16 * i, kk, lane);
 #pragma unroll
-      for (int j = 0; j < G::NJ; ++j) bfr[j] = read_frag<64, KMAJ>(stage, 16 * j, kk, lane);
+      for (int j = 0; j < G::NJ; ++j) bfr[j] = read_frag<64, KMAJ>(st, 16 * j, kk, lane);
+      {
+        if (kk == 1) {
+          // the next k-step's stage write goes out behind this half's reads: the MFMAs below
+          // wait for the reads only
+          __builtin_amdgcn_sched_barrier(0);
+          if (t + 1 < G::KSTEPS) {
+            char* nx = stage + ((t + 1) & 1) * G::STAGE;
+#pragma unroll
+            for (int q = 0; q < G::DLD; ++q) *reinterpret_cast<bf16x8*>(nx + soff[q]) = ring[(t + 1) % RING][q];
+            __builtin_amdgcn_sched_barrier(0);
+            if (t + 1 + RING < G::KSTEPS) issue(t + 1 + RING, ring[(t + 1) % RING]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -147,6 +167,7 @@ __device__ __forceinline__ void rb_forward(const bf16* __restrict__ W, const flo
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
   }
+  __syncthreads();   // in place: every wave has read the whole input image
   // lane holds out[16i + (lane & 15)][n0 + 16j + 4(lane >> 4) .. +3]
 #pragma unroll
   for (int i = 0; i < 2; ++i)
@@ -180,7 +201,8 @@ __device__ __forceinline__ void rb_dgrad(const bf16* __restrict__ W, const char*
     const int k = (lane >> 3) + 8 * q, ch = lane & 7;
     soff[q] = k * (G::WCOLS * 2) + ((ch ^ swz_x<G::WCOLS>(k)) << 4);
   }
-  bf16x8 ring[RB_RING][G::DLD];
+  constexpr int RING = RB_RING;
+  bf16x8 ring[RING][G::DLD];
   auto issue = [&](int t, bf16x8 (&dst)[G::DLD]) {
 #pragma unroll
     for (int q = 0; q < G::DLD; ++q)
@@ -196,15 +218,18 @@ __device__ __forceinline__ void rb_dgrad(const bf16* __restrict__ W, const char*
       ax[i][j] = *reinterpret_cast<const bf16x4*>(aux + (long long)m * H + n0 + 16 * j + 4 * (lane >> 4));
     }
 #pragma unroll
-  for (int s = 0; s < RB_RING; ++s) issue(s, ring[s]);
+  for (int s = 0; s < RING; ++s) issue(s, ring[s]);
   __builtin_amdgcn_sched_barrier(0);
+  {
+#pragma unroll
+    for (int q = 0; q < G::DLD; ++q) *reinterpret_cast<bf16x8*>(stage + soff[q]) = ring[0][q];
+    __builtin_amdgcn_sched_barrier(0);
+    if (RING < G::KSTEPS) issue(RING, ring[0]);
+    __builtin_amdgcn_sched_barrier(0);
+  }
 #pragma unroll
   for (int t = 0; t < G::KSTEPS; ++t) {
-#pragma unroll
-    for (int q = 0; q < G::DLD; ++q) *reinterpret_cast<bf16x8*>(stage + soff[q]) = ring[t % RB_RING][q];
-    __builtin_amdgcn_sched_barrier(0);
-    if (t + RB_RING < G::KSTEPS) issue(t + RB_RING, ring[t % RB_RING]);
-    __builtin_amdgcn_sched_barrier(0);
+    const char* st = stage + (t & 1) * G::STAGE;
     const char* kb = in + t * G::KB_BYTES;
 #pragma unroll
     for (int kk = 0; kk < 2; ++kk) {
@@ -212,7 +237,22 @@ __device__ __forceinline__ void rb_dgrad(const bf16* __restrict__ W, const char*
 #pragma unroll
       for (int i = 0; i < 2; ++i) af[i] = read_frag<64, KMAJ>(kb, 16 * i, kk, lane);
 #pragma unroll
-      for (int j = 0; j < G::NJ; ++j) bfr[j] = read_frag<G::WCOLS, XMAJ>(stage, 16 * j, kk, lane);
+      for (int j = 0; j < G::NJ; ++j) bfr[j] = read_frag<G::WCOLS, XMAJ>(st, 16 * j, kk, lane);
+      {
+        if (kk == 1) {
+          // the next k-step's stage write goes out behind this half's reads: the MFMAs below
+          // wait for the reads only
+          __builtin_amdgcn_sched_barrier(0);
+          if (t + 1 < G::KSTEPS) {
+            char* nx = stage + ((t + 1) & 1) * G::STAGE;
+#pragma unroll
+            for (int q = 0; q < G::DLD; ++q) *reinterpret_cast<bf16x8*>(nx + soff[q]) = ring[(t + 1) % RING][q];
+            __builtin_amdgcn_sched_barrier(0);
+            if (t + 1 + RING < G::KSTEPS) issue(t + 1 + RING, ring[(t + 1) % RING]);
+          }
+          __builtin_amdgcn_sched_barrier(0);
+        }
+      }
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -220,6 +260,7 @@ __device__ __forceinline__ void rb_dgrad(const bf16* __restrict__ W, const char*
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
     }
   }
+  __syncthreads();   // in place: every wave has read the whole input image
 #pragma unroll
   for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -229,6 +270,29 @@ __device__ __forceinline__ void rb_dgrad(const bf16* __restrict__ W, const char*
       for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc[i][j][r] * act_bwd_t<ACT>((float)ax[i][j][r]));
       *reinterpret_cast<bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * j + 4 * (lane >> 4))) = o;
     }
+}
+
+// The band's head weight/bias-gradient and loss partials: column k of wslab by thread k, rows in
+// order (deterministic), from the per-row dlogits / squared errors in LDS.
+template <int H>
+__device__ __forceinline__ void rb_head_partials(const RowbandArgs& p, const char* act,
+                                                 const float* dls, const float* lss, int tid) {
+  const int blk = blockIdx.x;
+  for (int k = tid; k < H; k += RB_THREADS) {
+    float s = 0.f;
+#pragma unroll 8
+    for (int r = 0; r < RB_ROWS; ++r) s += dls[r] * (float)*reinterpret_cast<const bf16*>(act + rb_off(r, k));
+    p.wslab[(long long)blk * H + k] = s;
+  }
+  if (tid == 0) {
+    float b = 0.f, l = 0.f;
+    for (int r = 0; r < RB_ROWS; ++r) {
+      b += dls[r];
+      l += lss[r];
+    }
+    p.bslab[blk] = b;
+    p.loss_part[blk] = l;
+  }
 }
 
 // Regression head (out == 1, MSE) on the band's last activations `in`: logit, loss, dlogit, the
@@ -264,6 +328,12 @@ __device__ __forceinline__ void rb_head(const RowbandArgs& p, const char* in, ch
     dls[r] = dl;
     lss[r] = valid ? d * d : 0.f;
   }
+  {
+    // in place: the band's weight-gradient partial reads the activations before dZ replaces them
+    __syncthreads();
+    rb_head_partials<H>(p, in, dls, lss, tid);
+    __syncthreads();
+  }
 #pragma unroll
   for (int c = 0; c < CPT; ++c) {
     const int k = 8 * (g + 16 * c);
@@ -274,65 +344,43 @@ __device__ __forceinline__ void rb_head(const RowbandArgs& p, const char* in, ch
   }
 }
 
+// The band's whole chain.  ONE activation image, updated in place by every pass (a barrier
+// between a pass's main loop and its epilogue), and two 8 KiB stage buffers per wave: the whole
+// 160 KiB LDS.  (Two ping-pong images + one stage buffer per wave: 0.0815-0.0819 vs 0.0804-0.0808
+// ms/step, profiles/r3s2_rowband_inplace_db_ab.txt.)
 template <int H, int ACT>
 __global__ void __launch_bounds__(RB_THREADS) rowband_kernel(RowbandArgs p) {
   using G = RbGeom<H>;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  auto img = [&](int i) { return smem + i * G::BUF; };
-  char* stage = smem + 2 * G::BUF + w * G::STAGE;
-  float* dls = reinterpret_cast<float*>(smem + 2 * G::BUF + RB_WAVES * G::STAGE);
+  char* img = smem;
+  char* stage = smem + G::BUF + w * 2 * G::STAGE;
+  // head scratch: wave 0's stage, idle between the last forward pass and the first dgrad
+  float* dls = reinterpret_cast<float*>(smem + G::BUF);
   float* lss = dls + RB_ROWS;
   const int blk = blockIdx.x;
   const int row0 = blk * RB_ROWS;
   const int nvalid = min(RB_ROWS, p.rows - row0);
   const int nh = p.nh;
-  // column group of this wave, rotated by the block index (measured neutral against w -> w,
-  // profiles/r3s2_rowband_ab.txt; kept: it spreads the XCD's concurrent weight reads)
   const int cg = (w + blk) & (RB_WAVES - 1);
 
-  rb_load_in<H>(img(0), p.X + (long long)row0 * p.ldx, p.ldx, nvalid, tid);
+  rb_load_in<H>(img, p.X + (long long)row0 * p.ldx, p.ldx, nvalid, tid);
   __syncthreads();
-  int cur = 0;
   for (int l = 0; l < nh; ++l) {
-    rb_forward<H, ACT>(p.W[l], p.b[l], img(cur), img(cur ^ 1), stage, cg, lane);
+    rb_forward<H, ACT>(p.W[l], p.b[l], img, img, stage, cg, lane);
     __syncthreads();
-    cur ^= 1;
-    rb_copy_out<H>(img(cur), p.a[l] + (long long)row0 * H, H, nvalid, tid);
+    rb_copy_out<H>(img, p.a[l] + (long long)row0 * H, H, nvalid, tid);
   }
-  rb_head<H, ACT>(p, img(cur), img(cur ^ 1), dls, lss, row0, nvalid, tid);
+  // (the partials' reads and the dZ writes are ordered by the head's own barriers; the stage
+  // scratch is free: every wave has passed the last forward pass's barriers)
+  rb_head<H, ACT>(p, img, img, dls, lss, row0, nvalid, tid);
   __syncthreads();
-  // head weight-gradient partial of this band: column tid, rows in order
-  {
-    const float* dl = dls;
-    for (int k = tid; k < H; k += RB_THREADS) {
-      float s = 0.f;
-#pragma unroll 8
-      for (int r = 0; r < RB_ROWS; ++r)
-        s += dl[r] * (float)*reinterpret_cast<const bf16*>(img(cur) + rb_off(r, k));
-      p.wslab[(long long)blk * H + k] = s;
-    }
-    if (tid == 0) {
-      float b = 0.f, l = 0.f;
-      for (int r = 0; r < RB_ROWS; ++r) {
-        b += dl[r];
-        l += lss[r];
-      }
-      p.bslab[blk] = b;
-      p.loss_part[blk] = l;
-    }
-  }
-  cur ^= 1;
-  rb_copy_out<H>(img(cur), p.dz[nh - 1] + (long long)row0 * H, H, nvalid, tid);
-  // the first dgrad writes its output over the last activations the partial above still reads
-  if (nh > 1) __syncthreads();
+  rb_copy_out<H>(img, p.dz[nh - 1] + (long long)row0 * H, H, nvalid, tid);
   for (int l = nh - 1; l >= 1; --l) {
-    rb_dgrad<H, ACT>(p.W[l], img(cur), img(cur ^ 1), stage, p.a[l - 1] + (long long)row0 * H,
-                     nvalid, cg, lane);
+    rb_dgrad<H, ACT>(p.W[l], img, img, stage, p.a[l - 1] + (long long)row0 * H, nvalid, cg, lane);
     __syncthreads();
-    cur ^= 1;
-    rb_copy_out<H>(img(cur), p.dz[l - 1] + (long long)row0 * H, H, nvalid, tid);
+    rb_copy_out<H>(img, p.dz[l - 1] + (long long)row0 * H, H, nvalid, tid);
   }
 }
 
