@@ -312,7 +312,8 @@ class HipOps:
         rows, H = X.shape
         nh = len(layers)
         _check(X.dtype == torch.bfloat16 and X.stride(1) == 1, "rowband: bf16 rows")
-        _check(self.lib.rowband_ok(rows, H, H, nh, 1, 0, ACT_CODES[act]), "rowband: shape")
+        _check(self.lib.rowband_ok(rows, H, H, nh, 1, LOSS_CODES["mse"], ACT_CODES[act]),
+               "rowband: shape")
         self._check_ws(ws, self.rowband_workspace_bytes(rows, H, nh, splits), "rowband")
         lay = []
         for W, b, a, dz, gW, gb in layers:

@@ -268,3 +268,28 @@ def test_no_mfma_result_read_without_wait_states():
     if not os.path.exists(_isa_check.OBJDUMP) or not os.path.exists(_build.ext_path()):
         pytest.skip("no llvm-objdump or no built library")
     assert _isa_check.scan_library(_build.ext_path()) == []
+
+
+def test_rowband_host_sizing_invariants():
+    """Host-side sizing of the row-band step (rowband.hip), no GPU needed: the engine sizes the
+    workspace once for its row capacity and then runs batches of any size up to it, so the bytes
+    a batch needs must never exceed the capacity's; the weight-gradient split count is one block
+    per CU for the proxy (3 layers x 16 tiles x 5 splits = 240) and >= 4 k-steps per split."""
+    from nnmpi_amd import native
+    lib = native.lib()
+    assert lib.wgrad_multi_splits(3, 512, 512, 8192) == 5
+    assert lib.wgrad_multi_splits(1, 512, 512, 8192) == 16
+    assert lib.wgrad_multi_splits(3, 512, 512, 512) == 2          # 8 k-steps: >= 4 per split
+    assert lib.rowband_blocks(8192) == 256 and lib.rowband_blocks(8191) == 256
+    assert lib.rowband_blocks(37) == 2
+    cap = lib.rowband_workspace_bytes(8192, 512, 3, 0)
+    prev = 0
+    for rows in (1, 31, 32, 33, 1000, 4096, 6144, 8000, 8191, 8192):
+        need = lib.rowband_workspace_bytes(rows, 512, 3, 0)
+        assert prev <= need <= cap, rows
+        prev = need
+    assert lib.rowband_ok(8192, 512, 512, 3, 1, 0, 1)
+    assert not lib.rowband_ok(8192, 1024, 1024, 3, 1, 0, 1)      # H = 512 only
+    assert not lib.rowband_ok(8192, 512, 784, 3, 1, 0, 1)        # input width = H
+    assert not lib.rowband_ok(8192, 512, 512, 3, 10, 1, 1)       # MSE regression head only
+    assert not lib.rowband_ok(0, 512, 512, 3, 1, 0, 1)
