@@ -18,7 +18,21 @@ namespace nnmpi {
 constexpr int TW = 16;
 constexpr int TL = 4;
 
-template <int ACT, int LOSS>
+// Layer widths: FIX = 1 compiles the reference model (2 -> 3 -> 1, ref.py:41-45) in, so every
+// `o < wout` / `i < win` test of the unrolled 16 x 16 loops folds away.  With runtime widths the
+// kernel executes ~1,000 uniform compare-and-branch pairs per step whatever the model's size
+// (16.9 us per step for the 2-3-1 model, profiles/r2s2_final_kstats_ref.csv).
+template <int FIX>
+__device__ __forceinline__ int tiny_w(const TinyMLPDesc& d, int l) {
+  if constexpr (FIX == 1) {
+    constexpr int w[TL + 1] = {2, 3, 1, 0, 0};
+    return w[l];
+  } else {
+    return d.widths[l];
+  }
+}
+
+template <int ACT, int LOSS, int FIX>
 __global__ void __launch_bounds__(256) tiny_mlp_kernel(TinyMLPDesc d, const float* P,
                                                        const float* __restrict__ X,
                                                        const float* __restrict__ Y,
@@ -38,20 +52,20 @@ __global__ void __launch_bounds__(256) tiny_mlp_kernel(TinyMLPDesc d, const floa
   for (int i = tid; i < numel; i += 256) PL[pbase + i] = P[pbase + i];
   __shared__ float red[4];
   __syncthreads();
-  const int L = d.n_layers;
-  const int out_w = d.widths[L];
+  const int L = FIX == 1 ? 2 : d.n_layers;
+  const int out_w = FIX == 1 ? 1 : d.widths[L];
   float wave_loss = 0.f;
   for (int base = blockIdx.x * 256; base < rows; base += gridDim.x * 256) {
     const int r = base + w * 64 + lane;
     const bool valid = r < rows;
     float a[TL + 1][TW];
 #pragma unroll
-    for (int k = 0; k < TW; ++k) a[0][k] = (valid && k < d.widths[0]) ? X[(long long)r * d.widths[0] + k] : 0.f;
+    for (int k = 0; k < TW; ++k) a[0][k] = (valid && k < tiny_w<FIX>(d, 0)) ? X[(long long)r * tiny_w<FIX>(d, 0) + k] : 0.f;
     float outv[TW];
 #pragma unroll
     for (int l = 0; l < TL; ++l) {
       if (l < L) {
-        const int win = d.widths[l], wout = d.widths[l + 1];
+        const int win = tiny_w<FIX>(d, l), wout = tiny_w<FIX>(d, l + 1);
         const float* W = PL + d.w_off[l];
         const float* B = PL + d.b_off[l];
 #pragma unroll
@@ -102,7 +116,7 @@ __global__ void __launch_bounds__(256) tiny_mlp_kernel(TinyMLPDesc d, const floa
 #pragma unroll
     for (int l = TL - 1; l >= 0; --l) {
       if (l < L) {
-        const int win = d.widths[l], wout = d.widths[l + 1];
+        const int win = tiny_w<FIX>(d, l), wout = tiny_w<FIX>(d, l + 1);
         const float* W = PL + d.w_off[l];
         float* gw = wsum + w * numel + d.w_off[l] - d.w_off[L - 1];
         float* gb = wsum + w * numel + d.b_off[l] - d.w_off[L - 1];
@@ -190,9 +204,14 @@ hipError_t tiny_mlp_step(const TinyMLPDesc& d, const float* params, const float*
   if (nb == 1 && sgd) sg = *sgd;
   float* lout = nb == 1 ? loss_out : nullptr;
 #define TINY_LAUNCH(A, LS)                                                                   \
-  hipLaunchKernelGGL((tiny_mlp_kernel<A, LS>), dim3(nb), dim3(256), smem, s, d, params, X, y, \
+  hipLaunchKernelGGL((tiny_mlp_kernel<A, LS, 0>), dim3(nb), dim3(256), smem, s, d, params, X, y, \
                      labels, rows, inv_count, gout, slab, numel, loss_part, loss_scale, lout, sg)
-  if (d.loss == LOSS_XENT) {
+  const bool ref_shape = d.n_layers == 2 && d.widths[0] == 2 && d.widths[1] == 3 && d.widths[2] == 1;
+  if (ref_shape && d.loss == LOSS_MSE && d.act == ACT_RELU) {
+    hipLaunchKernelGGL((tiny_mlp_kernel<ACT_RELU, LOSS_MSE, 1>), dim3(nb), dim3(256), smem, s, d,
+                       params, X, y, labels, rows, inv_count, gout, slab, numel, loss_part,
+                       loss_scale, lout, sg);
+  } else if (d.loss == LOSS_XENT) {
     if (d.act == ACT_TANH) TINY_LAUNCH(ACT_TANH, LOSS_XENT);
     else TINY_LAUNCH(ACT_RELU, LOSS_XENT);
   } else {
