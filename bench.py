@@ -298,8 +298,8 @@ def run(a, job):
         make_ops = lambda: HipOps(dev)  # noqa: E731
     else:
         dev = torch.device("cpu")
-        from nnmpi_amd.ops.torch_ops import TorchOps
-        make_ops = lambda: TorchOps(dev)  # noqa: E731
+        from nnmpi_amd.engine.trainer import cpu_ops
+        make_ops = lambda: cpu_ops(dev)  # noqa: E731
         a.comm = "torch"
     pg = pdist.ProcessGroupContext(job, 600.0, want_nccl=(gpu and a.comm == "torch" and world > 1))
     milestone("rendezvous")

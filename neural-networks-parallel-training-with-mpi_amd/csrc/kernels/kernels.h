@@ -246,6 +246,13 @@ hipError_t tiny_mlp_step(const TinyMLPDesc& d, const float* params, const float*
                          float* grad, int arena_numel, float* ws, float* loss_out, hipStream_t s,
                          const SgdFuse* sgd = nullptr, float loss_scale = -1.f);
 bool tiny_mlp_can_fuse_sgd(int rows);
+// CPU twins (csrc/host/tiny_host.cpp): the same step and update on host memory (the CPU /
+// gloo path of BASELINE config 1).  Returns nonzero on a bad description.
+int tiny_mlp_step_host(const TinyMLPDesc& d, float* params, const float* X, const float* y,
+                       const int64_t* labels, int rows, float inv_count, float* grad,
+                       int arena_numel, float* loss_out, float loss_scale, const SgdFuse* sgd);
+void sgd_momentum_host(float* p, float* g, float* buf, long long n, const float* hp, int nesterov,
+                       int first, int zero_grad);
 
 // ---- optimizer / elementwise (optim.hip) ----
 // hp = {lr, momentum, dampening, weight_decay, grad_scale}

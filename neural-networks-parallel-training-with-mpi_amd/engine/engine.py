@@ -58,8 +58,9 @@ class MLPEngine:
         self.act = spec.activation
         self.loss_kind = spec.loss
         if use_tiny is None:
-            use_tiny = (self.is_cuda and dtype == torch.float32 and L <= TINY_MAX_LAYERS
-                        and max(w) <= TINY_MAX_WIDTH)
+            # GPU: tiny_mlp.hip; CPU: the host twin when the op set has it (ops/host_ops.py)
+            use_tiny = ((self.is_cuda or hasattr(ops, "tiny_step")) and dtype == torch.float32
+                        and L <= TINY_MAX_LAYERS and max(w) <= TINY_MAX_WIDTH)
         self.use_tiny = bool(use_tiny)
         # host-driven torch.distributed transports (gloo copies device tensors through the host;
         # torch's nccl runs on its own side stream) cannot live inside a replayed hipGraph

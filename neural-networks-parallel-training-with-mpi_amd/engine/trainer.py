@@ -270,7 +270,20 @@ def make_ops(j: Job):
         from ..ops.hip_ops import HipOps
         return HipOps(j.device)
     from ..ops.torch_ops import TorchOps
-    return TorchOps(j.device)
+    return cpu_ops(j.device)
+
+
+def cpu_ops(device):
+    """CPU op set: native host steps for tiny models when the native library loads (HostOps),
+    else the plain-PyTorch oracle (TorchOps)."""
+    from ..ops.torch_ops import TorchOps
+    try:
+        from ..ops.host_ops import HostOps, host_ops_enabled
+        if host_ops_enabled():
+            return HostOps(device)
+    except (ImportError, OSError, RuntimeError):
+        pass
+    return TorchOps(device)
 
 
 def loss_scales(cfg: TrainConfig, rows_local: int, rows_all: List[int], out_f: int):
