@@ -275,7 +275,8 @@ def run(a, job):
     from nnmpi_amd.engine.trainer import loss_scales
     from nnmpi_amd.models.mlp import MLPSpec, reference_init
     from nnmpi_amd.parallel import dist as pdist
-    from nnmpi_amd.parallel.sync import NativeRcclSync, NoSync, ShardedSync, TorchDistSync
+    from nnmpi_amd.parallel.sync import (NativeRcclSync, NoSync, ShardedSync, ShmSync,
+                                         TorchDistSync, shm_sync_ok)
     from nnmpi_amd.parallel.supervisor import supervised, write_result
     from nnmpi_amd.utils.config import TrainConfig
     from nnmpi_amd.utils.metrics import comm_volume, scaling_report
@@ -367,8 +368,12 @@ def run(a, job):
         else:
             dist.broadcast(arena.master, src=0, group=comm_group)
             arena.sync_shadow()
-            sync = (ShardedSync(arena, world, rank, group=comm_group) if zero1 else
-                    TorchDistSync(arena, comm_group, world, grad_dtype=grad_dtype))
+            if zero1:
+                sync = ShardedSync(arena, world, rank, group=comm_group)
+            elif shm_sync_ok(dev.type, world, job.local_world, grad_dtype):
+                sync = ShmSync(arena, comm_group, world, rank)
+            else:
+                sync = TorchDistSync(arena, comm_group, world, grad_dtype=grad_dtype)
         eng = MLPEngine(spec, arena, make_ops(), sync, device=dev, dtype=dtype,
                         rows_capacity=max(rows, 1), lr=a.lr, momentum=0.9,
                         use_graph=not a.no_graph, overlap=not a.no_overlap,

@@ -21,6 +21,8 @@ Implementations
   reference's centralised pattern over RCCL (ncclReduce to rank 0 + ncclBroadcast).
 * :class:`ShardedSync` — sharded optimizer state (ZeRO-1): reduce-scatter of the gradient, SGD
   on the rank's own 1/P slice of the arena only, all-gather of the updated parameters.
+* :class:`ShmSync` — CPU ranks on one machine: the all-reduce through a shared-memory segment
+  (``csrc/host/shm_comm.cpp``), the transport MPI uses between ranks of a node.
 """
 from __future__ import annotations
 
@@ -437,3 +439,57 @@ class ShardedSync(GradSync):
                 s.synchronize()
             else:
                 dist.all_gather(self._views(buf), own.clone(), group=self.group)
+
+
+def shm_sync_ok(device_type: str, world: int, local_world: int, grad_dtype: str = "fp32",
+                mode: str = "allreduce") -> bool:
+    """CPU ranks that all run on this machine, fp32 all-reduce: the shared-memory transport
+    applies (NNMPI_SHM=0 keeps gloo)."""
+    import os
+    return (device_type == "cpu" and world > 1 and local_world == world and grad_dtype == "fp32"
+            and mode == "allreduce" and os.environ.get("NNMPI_SHM", "1") != "0")
+
+
+class ShmSync(GradSync):
+    """Gradient all-reduce of CPU ranks on one machine through shared memory.
+
+    The reference's mpiexec ranks exchange gradients through MPI, which moves intra-node
+    messages through shared memory; gloo (``TorchDistSync``) goes through loopback TCP -- for the
+    reference config's 13-parameter gradient ~0.3-0.4 ms per all-reduce, ten times the whole
+    native step (ops/host_ops.py).  Here every call is a copy into this rank's slot of a mapped
+    segment, one arrival counter and a rank-ordered sum (identical bits on every rank), inline in
+    the step like the native RCCL path's inline form.  Set up over the job's gloo group: rank 0
+    creates the segment under a random name, the others attach, then the name is unlinked (the
+    mapping lives until the last rank exits, nothing is left in /dev/shm)."""
+
+    def __init__(self, arena, group, world: int, rank: int, timeout_s: float = 120.0):
+        super().__init__(arena)
+        import os
+        import secrets
+        from .. import native
+        self.world, self.rank, self.group, self.timeout_s = world, rank, group, float(timeout_s)
+        if len(arena.buckets) > 1:
+            arena.replan_single_bucket()   # one call per step amortises the arrival wait
+        obj = [f"/nnmpi-{os.getpid()}-{secrets.token_hex(6)}" if rank == 0 else None]
+        dist.broadcast_object_list(obj, src=0, group=group)
+        self.name = obj[0]
+        cap = max(b.numel for b in arena.buckets)
+        lib = native.lib()
+        if rank == 0:
+            self.comm = lib.ShmComm(self.name, rank, world, cap, True)
+        dist.barrier(group=group)
+        if rank != 0:
+            self.comm = lib.ShmComm(self.name, rank, world, cap, False)
+        dist.barrier(group=group)
+        if rank == 0:
+            self.comm.unlink()
+
+    def _launch(self, bucket):
+        view = self.arena.grad[bucket.offset:bucket.offset + bucket.numel]
+        self.note(1, bucket.index, bucket.offset, bucket.numel, 0)
+        self.comm.allreduce_sum(view.data_ptr(), bucket.numel, self.timeout_s)
+
+    def comm_only(self):
+        for b in self.arena.buckets:
+            self._launch(b)
+

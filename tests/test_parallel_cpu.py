@@ -76,9 +76,11 @@ def test_sequence_checker_catches_bucket_layout_mismatch():
     cfg = dict(device="cpu", print_rank="none", widths=[512, 512, 1], n_features=512,
                n_samples=64, bucket_mb=0.1, seqcheck=True, nepochs=2, data_gen="device",
                data_dist="local")
+    # (per-bucket gloo collectives: the shared-memory sync reduces one whole-arena bucket)
     with pytest.raises(AssertionError, match="CollectiveMismatch"):
-        run_ranks_proc(cfg, 2, env_per_rank=lambda r: {"NNMPI_CHUNK_MIN_TILES": "1"} if r else {})
-    out = run_ranks_proc(cfg, 2)             # same layout everywhere: passes
+        run_ranks_proc(cfg, 2, env_per_rank=lambda r: ({"NNMPI_CHUNK_MIN_TILES": "1", "NNMPI_SHM": "0"}
+                                                      if r else {"NNMPI_SHM": "0"}))
+    out = run_ranks_proc(cfg, 2, env_per_rank=lambda r: {"NNMPI_SHM": "0"})   # same layout: passes
     assert torch.equal(out[0]["final"], out[1]["final"])
 
 
