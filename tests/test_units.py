@@ -293,3 +293,50 @@ def test_rowband_host_sizing_invariants():
     assert not lib.rowband_ok(8192, 512, 784, 3, 1, 0, 1)        # input width = H
     assert not lib.rowband_ok(8192, 512, 512, 3, 10, 1, 1)       # MSE regression head only
     assert not lib.rowband_ok(0, 512, 512, 3, 1, 0, 1)
+
+
+def test_shm_allreduce_sums_in_rank_order_and_times_out():
+    """The shared-memory all-reduce of CPU ranks (csrc/host/shm_comm.cpp), two handles in one
+    process on two threads: every rank gets the rank-ordered fp32 sum (the same bits), repeated
+    calls reuse the two slot banks, and a call whose peer never arrives raises instead of hanging."""
+    import os
+    import secrets
+    import threading
+    import numpy as np
+    from nnmpi_amd import native
+    lib = native.lib()
+    name = f"/nnmpi-test-{os.getpid()}-{secrets.token_hex(4)}"
+    c0 = lib.ShmComm(name, 0, 2, 64, True)
+    c1 = lib.ShmComm(name, 1, 2, 64, False)
+    c0.unlink()
+    rng = np.random.default_rng(0)
+    for call in range(5):
+        a = rng.standard_normal(37).astype(np.float32)
+        b = rng.standard_normal(37).astype(np.float32)
+        want = a + b
+        bufs = [a.copy(), b.copy()]
+        ts = [threading.Thread(target=c.allreduce_sum, args=(buf.ctypes.data, 37, 10.0))
+              for c, buf in zip((c0, c1), bufs)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+        assert np.array_equal(bufs[0], want) and np.array_equal(bufs[1], want), call
+    lonely = np.ones(8, dtype=np.float32)
+    with pytest.raises(RuntimeError, match="stalled"):
+        c0.allreduce_sum(lonely.ctypes.data, 8, 0.2)
+    with pytest.raises(RuntimeError, match="larger"):
+        c1.allreduce_sum(lonely.ctypes.data, 65, 0.2)
+
+
+def test_shm_sync_matches_gloo_at_two_ranks():
+    """Two CPU ranks: the shared-memory all-reduce (default) and gloo give the same parameters bit
+    for bit (a + b either way) and the same losses."""
+    from _mp import run_ranks_proc
+    cfg = dict(device="cpu", print_rank="none", nepochs=5)
+    a = run_ranks_proc(cfg, 2)
+    b = run_ranks_proc(cfg, 2, env_per_rank=lambda r: {"NNMPI_SHM": "0"})
+    assert a[0]["schedule"]["sync"] == "ShmSync" and b[0]["schedule"]["sync"] == "TorchDistSync"
+    assert torch.equal(a[0]["final"], a[1]["final"])
+    assert torch.equal(a[0]["final"], b[0]["final"])
+    assert a[0]["losses"] == b[0]["losses"]
