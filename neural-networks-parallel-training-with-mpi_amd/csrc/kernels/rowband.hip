@@ -21,7 +21,7 @@
 // epilogue -- and two 8 KiB weight stages per wave: KMAJ [64 n][64 k] for the forward's B
 // operand, XMAJ [64 k][64 x] for the dgrad's transposed operand (ds_read_b64_tr_b16, the GEMMs'
 // XMAJ image).  The weights stream global -> registers (whole 128-byte lines per load
-// instruction, a 3-deep ring of k-steps pinned with sched_barrier) -> the stage buffer the
+// instruction, a 1-deep ring of k-steps pinned with sched_barrier) -> the stage buffer the
 // fragment reads of the current k-step are not using.  After each pass the image is copied out
 // row-contiguously (activations and dZ are needed by the weight gradients).
 #include "gemm_tiles.h"
@@ -31,7 +31,10 @@ namespace nnmpi {
 constexpr int RB_ROWS = 32;
 constexpr int RB_WAVES = 8;
 constexpr int RB_THREADS = 64 * RB_WAVES;
-constexpr int RB_RING = 3;   // k-steps of weight loads in flight per lane (beyond the staged one)
+// k-steps of weight loads in flight per lane beyond the staged one: 1 measured fastest with the
+// double-buffered stage (0.0772-0.0775 ms/step vs 0.0783-0.0784 at 2 and 0.0802-0.0805 at 3,
+// profiles/r3s2_rowband_ring_depth_ab.txt) -- deeper rings only add VGPRs and queued requests
+constexpr int RB_RING = 1;
 
 template <int H>
 struct RbGeom {
@@ -95,7 +98,7 @@ __device__ __forceinline__ void rb_load_in(char* img, const bf16* src, int ld, i
 // fragments straight from global memory (16 rows x 32-64 B per load instruction, two k
 // permutations tried) ran the three forward passes in 51 us vs 29 us staged
 // (profiles/r3s2_rowband_ab.txt, r3s2_rowband_fwd_direct_and_wgrad_ns_ab.txt).
-template <int H, int ACT>
+template <int H, int ACT, int RING = RB_RING>
 __device__ __forceinline__ void rb_forward(const bf16* __restrict__ W, const float* __restrict__ bias,
                                            const char* in, char* out, char* stage, int w, int lane) {
   using G = RbGeom<H>;
@@ -110,7 +113,6 @@ __device__ __forceinline__ void rb_forward(const bf16* __restrict__ W, const flo
   int soff[G::DLD];
 #pragma unroll
   for (int q = 0; q < G::DLD; ++q) soff[q] = kmaj_off((lane >> 3) + 8 * q, lane & 7);
-  constexpr int RING = RB_RING;
   bf16x8 ring[RING][G::DLD];
   auto issue = [&](int t, bf16x8 (&dst)[G::DLD]) {
 #pragma unroll
@@ -183,7 +185,7 @@ __device__ __forceinline__ void rb_forward(const bf16* __restrict__ W, const flo
 
 // One activation-gradient layer: out = (in . W) * act'(aux), in = dZ_l (image), aux = a_{l-1}
 // rows of this band in global memory (written by this block's earlier copy-out).
-template <int H, int ACT>
+template <int H, int ACT, int RING = RB_RING>
 __device__ __forceinline__ void rb_dgrad(const bf16* __restrict__ W, const char* in, char* out,
                                          char* stage, const bf16* aux, int nvalid, int w, int lane) {
   using G = RbGeom<H>;
@@ -201,7 +203,6 @@ __device__ __forceinline__ void rb_dgrad(const bf16* __restrict__ W, const char*
     const int k = (lane >> 3) + 8 * q, ch = lane & 7;
     soff[q] = k * (G::WCOLS * 2) + ((ch ^ swz_x<G::WCOLS>(k)) << 4);
   }
-  constexpr int RING = RB_RING;
   bf16x8 ring[RING][G::DLD];
   auto issue = [&](int t, bf16x8 (&dst)[G::DLD]) {
 #pragma unroll
@@ -348,7 +349,7 @@ __device__ __forceinline__ void rb_head(const RowbandArgs& p, const char* in, ch
 // between a pass's main loop and its epilogue), and two 8 KiB stage buffers per wave: the whole
 // 160 KiB LDS.  (Two ping-pong images + one stage buffer per wave: 0.0815-0.0819 vs 0.0804-0.0808
 // ms/step, profiles/r3s2_rowband_inplace_db_ab.txt.)
-template <int H, int ACT>
+template <int H, int ACT, int RING = RB_RING>
 __global__ void __launch_bounds__(RB_THREADS) rowband_kernel(RowbandArgs p) {
   using G = RbGeom<H>;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
@@ -368,7 +369,7 @@ __global__ void __launch_bounds__(RB_THREADS) rowband_kernel(RowbandArgs p) {
   rb_load_in<H>(img, p.X + (long long)row0 * p.ldx, p.ldx, nvalid, tid);
   __syncthreads();
   for (int l = 0; l < nh; ++l) {
-    rb_forward<H, ACT>(p.W[l], p.b[l], img, img, stage, cg, lane);
+    rb_forward<H, ACT, RING>(p.W[l], p.b[l], img, img, stage, cg, lane);
     __syncthreads();
     rb_copy_out<H>(img, p.a[l] + (long long)row0 * H, H, nvalid, tid);
   }
@@ -378,7 +379,7 @@ __global__ void __launch_bounds__(RB_THREADS) rowband_kernel(RowbandArgs p) {
   __syncthreads();
   rb_copy_out<H>(img, p.dz[nh - 1] + (long long)row0 * H, H, nvalid, tid);
   for (int l = nh - 1; l >= 1; --l) {
-    rb_dgrad<H, ACT>(p.W[l], img, img, stage, p.a[l - 1] + (long long)row0 * H, nvalid, cg, lane);
+    rb_dgrad<H, ACT, RING>(p.W[l], img, img, stage, p.a[l - 1] + (long long)row0 * H, nvalid, cg, lane);
     __syncthreads();
     rb_copy_out<H>(img, p.dz[l - 1] + (long long)row0 * H, H, nvalid, tid);
   }
