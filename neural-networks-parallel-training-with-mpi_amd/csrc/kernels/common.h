@@ -125,7 +125,7 @@ __device__ __forceinline__ SgdPre4 sgd_pre4(const SgdFuse& f, const float* gaddr
   q.lr = f.hp[0]; q.mom = f.hp[1]; q.damp = f.hp[2]; q.wd = f.hp[3]; q.gs = f.hp[4];
   return q;
 }
-__device__ __forceinline__ void sgd_apply4(const SgdFuse& f, SgdPre4 q, f32x4 g) {
+__device__ __forceinline__ f32x4 sgd_apply4(const SgdFuse& f, SgdPre4 q, f32x4 g) {
 #pragma unroll
   for (int r = 0; r < 4; ++r) {
     float bb = q.b[r];
@@ -140,9 +140,10 @@ __device__ __forceinline__ void sgd_apply4(const SgdFuse& f, SgdPre4 q, f32x4 g)
     for (int r = 0; r < 4; ++r) sv[r] = (bf16)q.p[r];
     *reinterpret_cast<bf16x4*>(f.s_base + q.off) = sv;
   }
+  return q.p;
 }
 
-__device__ __forceinline__ void sgd_fused_store4(const SgdFuse& f, const float* gaddr, f32x4 g) {
+__device__ __forceinline__ f32x4 sgd_fused_store4(const SgdFuse& f, const float* gaddr, f32x4 g) {
   const long long off = gaddr - f.g_base;
   f32x4 p = *reinterpret_cast<const f32x4*>(f.p_base + off);
   f32x4 b = *reinterpret_cast<const f32x4*>(f.m_base + off);
@@ -160,6 +161,29 @@ __device__ __forceinline__ void sgd_fused_store4(const SgdFuse& f, const float* 
 #pragma unroll
     for (int r = 0; r < 4; ++r) sv[r] = (bf16)p[r];
     *reinterpret_cast<bf16x4*>(f.s_base + off) = sv;
+  }
+  return p;
+}
+
+// Element offset of (row n, column k) of a [N][K] bf16 matrix (K % 32 == 0) in its FRAGMENT-MAJOR
+// image (rowband.hip v2): fragment (n >> 4, k >> 5) is 1 KiB, the v_mfma_f32_16x16x32_bf16
+// operand map -- lane (n & 15) + 16 * ((k >> 3) & 3) holds its 8 consecutive k at (k & 7).
+__host__ __device__ __forceinline__ long long rb_pk_off(int n, int k, int K) {
+  return (((long long)(n >> 4) * (K >> 5) + (k >> 5)) * 64 + ((n & 15) + 16 * ((k >> 3) & 3))) * 8 + (k & 7);
+}
+
+// The updated values p of M[m][n .. n+3] ([M][N] row-major, n % 4 == 0) into the fragment-major
+// images of M (pkf, may be null) and of M^T (pkd, may be null).
+__device__ __forceinline__ void rb_pack_store4(bf16* pkf, bf16* pkd, int m, int n, int M, int N, f32x4 p) {
+  if (pkf) {
+    bf16x4 v;
+#pragma unroll
+    for (int r = 0; r < 4; ++r) v[r] = (bf16)p[r];
+    *reinterpret_cast<bf16x4*>(pkf + rb_pk_off(m, n, N)) = v;
+  }
+  if (pkd) {
+#pragma unroll
+    for (int r = 0; r < 4; ++r) pkd[rb_pk_off(n + r, m, M)] = (bf16)p[r];
   }
 }
 

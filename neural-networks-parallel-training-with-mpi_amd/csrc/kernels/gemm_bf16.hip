@@ -104,9 +104,12 @@ __device__ __forceinline__ void slab_reduce_block(const SlabReduce& r, int b, in
       f32x4 t = part[cg * WS * 64 + lane];
 #pragma unroll
       for (int k = 1; k < WS; ++k) t += part[(cg * WS + k) * 64 + lane];
-      if (upd) sgd_apply4(r.sg, pre, t);
-      else if (r.sg.g_base) sgd_fused_store4(r.sg, o, t);
-      else *reinterpret_cast<f32x4*>(o) = t;
+      if (r.sg.g_base) {
+        const f32x4 pn = upd ? sgd_apply4(r.sg, pre, t) : sgd_fused_store4(r.sg, o, t);
+        if (r.pkf || r.pkd) rb_pack_store4(r.pkf, r.pkd, (int)m, (int)n, r.M, r.N, pn);
+      } else {
+        *reinterpret_cast<f32x4*>(o) = t;
+      }
     }
     return;
   }

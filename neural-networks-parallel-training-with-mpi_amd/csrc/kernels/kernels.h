@@ -40,6 +40,10 @@ struct SlabReduce {
   float* loss_out;
   SgdFuse sg;               // sg.g_base != null: apply the optimizer update instead of storing
   int sgd_serial = 0;       // 1: optimizer operands loaded after the sums (A/B, NNMPI_SGD_SERIAL)
+  // with sg: also write the updated [M][N] matrix into its fragment-major image (pkf) and that
+  // of its transpose (pkd) -- the row-band v2 weight images (rowband.hip); null = none
+  bf16* pkf = nullptr;
+  bf16* pkd = nullptr;
 };
 
 enum Epi : int { EPI_BIAS_ACT = 0, EPI_DACT = 1, EPI_F32 = 2 };
@@ -146,7 +150,10 @@ constexpr int RB_MAXL = 4;   // hidden layers
 struct RowbandArgs {
   const bf16* X; int ldx;
   int rows, H, nh, act;
-  const bf16* W[RB_MAXL];   // compute (bf16) weights [H][H]
+  int in;                   // input width (v2; v1: == H)
+  const bf16* Pf[RB_MAXL];  // v2: fragment-major image of W_l (null: the v1 kernel)
+  const bf16* Pd[RB_MAXL];  // v2: fragment-major image of W_l^T (l >= 1)
+  const bf16* W[RB_MAXL];   // compute (bf16) weights [H][in_l]
   const float* b[RB_MAXL];  // biases [H]
   bf16* a[RB_MAXL];         // saved activations a_l [rows][H]
   bf16* dz[RB_MAXL];        // dZ_l [rows][H]
@@ -157,6 +164,11 @@ struct RowbandArgs {
 };
 int rowband_blocks(int rows);
 bool rowband_ok(int rows, int H, int in, int nh, int out, int loss, int act);
+bool rowband2_ok(int rows, int H, int in, int nh, int out, int loss, int act);
+// elements of the fragment-major weight images one model needs (rowband_pack)
+size_t rowband_packed_elems(int H, int in, int nh);
+// rebuild the images Pf / Pd from the row-major bf16 weights W (one launch)
+hipError_t rowband_pack(const RowbandArgs& p, hipStream_t s);
 hipError_t rowband_fwd_bwd(const RowbandArgs& p, hipStream_t s);
 // The whole step: grads (or, with sg.g_base set, the fused SGD-momentum update at the arena
 // positions of gW / gb / gWh / gbh), loss_out[0] = loss_scale * sum of squared errors.
@@ -169,7 +181,7 @@ struct RowbandStep {
   SgdFuse sg;
   int splits;         // weight-gradient split-K slabs (0 = fill the chip)
 };
-size_t rowband_workspace_bytes(int rows, int H, int nh, int splits);
+size_t rowband_workspace_bytes(int rows, int H, int in, int nh, int splits);
 hipError_t rowband_step(const RowbandStep& st, hipStream_t s);
 // Weight gradients of several layers in ONE grouped launch (128x128 tiles, split-K with
 // `splits` slabs each, 0 = fill the chip); pending[j] receives job j's combine.

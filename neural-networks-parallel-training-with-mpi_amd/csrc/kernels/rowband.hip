@@ -385,11 +385,356 @@ __global__ void __launch_bounds__(RB_THREADS) rowband_kernel(RowbandArgs p) {
   }
 }
 
-int rowband_blocks(int rows) { return (rows + RB_ROWS - 1) / RB_ROWS; }
+// =============================================================================================
+// v2: packed weights streamed straight into MFMA fragments.
+//
+// The v1 passes above move every weight byte global -> VGPR -> ds_write -> ds_read -> MFMA: per
+// CU and 64-deep k-step 64 KiB of LDS writes plus 64 KiB of LDS reads on top of the 64 KiB the
+// L2 delivers, and ~2.7 non-MFMA VALU per MFMA (profiles/r3s2_rowband_pmc.txt).  Here the weights
+// are kept (besides the arena's row-major bf16 shadow) in a FRAGMENT-MAJOR image: 1 KiB per
+// 16 x 32 operand fragment, lane l's 16 bytes at l * 16, so ONE global_load_dwordx4 fills one
+// v_mfma_f32_16x16x32_bf16 operand with a whole contiguous KiB (8 full cache lines).  Two images
+// per hidden layer: W (forward B operand, [out][in]) and W^T (dgrad B operand, [in][out]).  The
+// weights never touch the LDS; the LDS holds only the band's activation images.
+//
+// Each wave's weight loads form ONE stream across all matrices of the step (forward layers,
+// then the dgrad layers): a D-deep register ring of k-steps whose refills run past the end of a
+// matrix into the next one, so the epilogue, barrier, copy-out and head of a layer overlap the
+// next layer's first weight fetches.
+//
+// LDS: max(nh, 2) activation slots of RB_ROWS x max(H, in) bf16 (KMAJ image per 64-deep block),
+// no ping-pong barrier: forward layer l reads slot S_{l-1} (slot 0 = the input rows) and writes
+// slot S_l, so every saved activation the dgrads need stays resident; the head works in place
+// on a_{nh-1}; dgrad l writes dZ_{l-1} in place over its own act'(a_{l-1}) operand (each lane
+// reads then writes the same elements).  One barrier per layer.
+// =============================================================================================
+// k-steps of the register ring (1 being consumed, D-1 in flight).  The ring is what hides the
+// L2 latency: at D = 2 (8 KiB in flight per wave) the proxy's band streamed ~60 GB/s per CU,
+// latency-bound (profiles/r4_rowband_v2_*).  Deeper where the registers allow it (every matrix
+// of the stream must have a multiple of D k-steps: its ring phase is compile-time).
+template <int H>
+constexpr int rb2_depth() { return (H == 256 || H == 512) ? 4 : 2; }
+static int rb2_depth_rt(int H) { return (H == 256 || H == 512) ? 4 : 2; }
 
-bool rowband_ok(int rows, int H, int in, int nh, int out, int loss, int act) {
-  return rows > 0 && H == 512 && in == H && nh >= 1 && nh <= RB_MAXL && out == 1 &&
-         loss == LOSS_MSE && (act == ACT_RELU || act == ACT_TANH || act == ACT_NONE);
+template <int H>
+struct Rb2Geom {
+  static_assert(H % 128 == 0 && H >= 256 && H <= 1024, "row-band v2: H = 256 .. 1024, H % 128 == 0");
+  static constexpr int NJ = H / 128;          // 16-column MFMA tiles per wave (8 waves x NJ x 16 = H)
+  static constexpr int NF = 2 * NJ;           // 1 KiB operand fragments per 64-deep k-step per wave
+  static constexpr int WCOLS = H / RB_WAVES;  // output columns per wave
+  static constexpr int KB_BYTES = RB_ROWS * 128;
+};
+
+// One k-step (NF fragments) of the weight stream into ring slot `dst`: matrix base `b` (already
+// offset to this wave's first tile), `ts` bytes between the wave's tiles, k-step `s`.  The loads
+// are inline asm, counted by hand (rb2_wait): hipcc's own vmcnt bookkeeping merges the ring's
+// loop-carried slots conservatively at the loop headers and waited for nearly the whole ring in
+// the first sub-step (vmcnt(3) where 24 loads may stay in flight), so the ring bought nothing.
+// kk-major issue order: the first k-half's fragments land first.  SGPR base + one lane-offset
+// VGPR per load (global_load_dwordx4 v, v_off, s[base]).
+template <int NJ>
+__device__ __forceinline__ void rb2_issue(bf16x8 (&dst)[2 * NJ], const char* b, int ts, int s, int voff) {
+  const char* base = b + s * 2048;
+#pragma unroll
+  for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const char* bj = base + j * ts;
+      if (kk == 0)
+        asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(dst[2 * j]) : "v"(voff), "s"(bj));
+      else
+        asm volatile("global_load_dwordx4 %0, %1, %2 offset:1024" : "=v"(dst[2 * j + 1]) : "v"(voff), "s"(bj));
+    }
+}
+
+// Wait until at most N of this wave's vector-memory operations are outstanding, then pin the
+// k-half `kk` fragments of `f` behind the wait (their consumers cannot be hoisted above it; the
+// asm loads' destinations count as written at issue for the compiler -- cdna_hip_programming.md
+// §5.7 item 1, form (ii)).
+template <int N, int NJ>
+__device__ __forceinline__ void rb2_wait(bf16x8 (&f)[2 * NJ], int kk) {
+  asm volatile("s_waitcnt vmcnt(%0)" ::"n"(N));
+#pragma unroll
+  for (int j = 0; j < NJ; ++j) asm volatile("" : "+v"(f[2 * j + kk]));
+}
+
+// The stream's matrix q: forward layers 0 .. nh-1, then the dgrad images of layers nh-1 .. 1;
+// past the end, the last matrix again with a zero tile stride (L1-resident dummy refills).
+struct Rb2Mat {
+  const char* b;   // this wave's first tile
+  int ts;          // bytes between the wave's tiles
+  int ks;          // 64-deep k-steps
+};
+template <int H>
+__device__ __forceinline__ Rb2Mat rb2_mat(const RowbandArgs& p, int q, int cg) {
+  using G = Rb2Geom<H>;
+  const int nh = p.nh;
+  const bool past = q >= 2 * nh - 1;
+  if (past) q = 2 * nh - 2;
+  const char* base;
+  int K;
+  if (q < nh) {
+    base = reinterpret_cast<const char*>(p.Pf[q]);
+    K = q == 0 ? p.in : H;
+  } else {
+    base = reinterpret_cast<const char*>(p.Pd[2 * nh - 1 - q]);
+    K = H;
+  }
+  const int ts = (K >> 5) * 1024;
+  Rb2Mat m;
+  m.b = base + (long long)cg * G::NJ * ts;
+  m.ts = past ? 0 : ts;
+  m.ks = K >> 6;
+  return m;
+}
+
+// Main loop of one matrix: acc[i][j] += band rows 16i.. x fragments of this wave's tile j, the
+// B operand from the ring.  Slot d holds k-step s0 + d on entry to sub-step d; after its MFMAs
+// it is refilled with k-step s0 + d + D of this matrix or, past its end, of the next one.  (A
+// do-while: every matrix has >= D k-steps, and a loop the compiler must assume can be skipped
+// makes it wait for the refills at the loop exit -- rule: no global load between the ring
+// refills and their use, or vmcnt drains the ring.)
+template <int H, int D, int ABL = 0>
+__device__ __forceinline__ void rb2_mainloop(bf16x8 (&ring)[D][Rb2Geom<H>::NF],
+                                             f32x4 (&acc)[2][Rb2Geom<H>::NJ], const char* img,
+                                             const Rb2Mat& cur, const Rb2Mat& nxt, int lane) {
+  using G = Rb2Geom<H>;
+  const int voff = lane * 16;
+  int s0 = 0;
+  do {
+#pragma unroll
+    for (int d = 0; d < D; ++d) {
+      const int s = s0 + d;
+      const char* kb = img + s * G::KB_BYTES;
+      bf16x8 af[2][2];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk)
+#pragma unroll
+        for (int i = 0; i < 2; ++i) af[i][kk] = read_frag<64, KMAJ>(kb, 16 * i, kk, lane);
+      // slot d: every later slot (D - 1 k-steps) may stay in flight, and the second k-half
+      if (ABL != 2) rb2_wait<(D - 1) * G::NF + G::NJ, G::NJ>(ring[d], 0);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < G::NJ; ++j) {
+          if (ABL == 1) asm volatile("" ::"v"(ring[d][2 * j]), "v"(af[i][0]));
+          else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[d][2 * j], af[i][0], acc[i][j], 0, 0, 0);
+        }
+      __builtin_amdgcn_sched_barrier(0);   // (the first half's MFMAs stay ahead of the second wait)
+      if (ABL != 2) rb2_wait<(D - 1) * G::NF, G::NJ>(ring[d], 1);
+#pragma unroll
+      for (int i = 0; i < 2; ++i)
+#pragma unroll
+        for (int j = 0; j < G::NJ; ++j) {
+          if (ABL == 1) asm volatile("" ::"v"(ring[d][2 * j + 1]), "v"(af[i][1]));
+          else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[d][2 * j + 1], af[i][1], acc[i][j], 0, 0, 0);
+        }
+      // (sched_barrier: the refill stays behind this sub-step's MFMAs, which read the slot)
+      __builtin_amdgcn_sched_barrier(0);
+      const int sn = s + D;
+      const bool inc = sn < cur.ks;
+      if (ABL != 2) rb2_issue<G::NJ>(ring[d], inc ? cur.b : nxt.b, inc ? cur.ts : nxt.ts, inc ? sn : sn - cur.ks, voff);
+      __builtin_amdgcn_sched_barrier(0);
+    }
+    s0 += D;
+  } while (s0 < cur.ks);
+}
+
+// Runtime-width row-contiguous copy between an image of `width` columns and [rows][ld] memory.
+__device__ __forceinline__ void rb2_load_in(char* img, const bf16* src, int ld, int width, int nvalid, int tid) {
+  const int nch = RB_ROWS * width / 8;
+  for (int id = tid; id < nch; id += RB_THREADS) {
+    const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
+    bf16x8 v = *reinterpret_cast<const bf16x8*>(src + (long long)min(r, nvalid - 1) * ld + kb * 64 + k8 * 8);
+    if (r >= nvalid) {
+#pragma unroll
+      for (int e = 0; e < 8; ++e) v[e] = (bf16)0.f;
+    }
+    *reinterpret_cast<bf16x8*>(img + kb * (RB_ROWS * 128) + kmaj_off(r, k8)) = v;
+  }
+}
+
+// LDS parameter block after the activation slots (floats): every bias, the head weight, the
+// band's targets, the head bias and the head's per-row scratch.  Loaded once at kernel start:
+// a global load issued after the ring's refills would make its wait drain the whole ring.
+struct Rb2Par {
+  float* bias;   // [nh][H]
+  float* wh;     // [H]
+  float* y;      // [RB_ROWS]
+  float* bh;     // [4]
+  float* dls;    // [RB_ROWS]
+  float* lss;    // [RB_ROWS]
+};
+__host__ __device__ __forceinline__ int rb2_par_bytes(int H, int nh) {
+  return ((nh + 1) * H + 3 * RB_ROWS + 4) * 4;
+}
+__device__ __forceinline__ Rb2Par rb2_par(char* base, int H, int nh) {
+  Rb2Par q;
+  q.bias = reinterpret_cast<float*>(base);
+  q.wh = q.bias + nh * H;
+  q.y = q.wh + H;
+  q.bh = q.y + RB_ROWS;
+  q.dls = q.bh + 4;
+  q.lss = q.dls + RB_ROWS;
+  return q;
+}
+
+// Regression head of the band (out == 1, MSE) in place on `z` = a_{nh-1}: logit, loss, dlogit,
+// the band's head-gradient partials, then dZ_{nh-1} = dl * w * act'(a) over a.
+template <int H, int ACT>
+__device__ __forceinline__ void rb2_head(const RowbandArgs& p, char* z, const Rb2Par& q, int nvalid, int tid) {
+  constexpr int CPT = H / 8 / 16;   // 8-column chunks per thread (16 threads per row)
+  const int r = tid >> 4, g = tid & 15;
+  // (a and w are re-read from the LDS for the dZ pass instead of held: the weight ring is live
+  // across the head, and holding them costs 16 * CPT registers)
+  float dot = 0.f;
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int k = 8 * (g + 16 * c);
+    const bf16x8 v = *reinterpret_cast<const bf16x8*>(z + rb_off(r, k));
+    const f32x4 w0 = *reinterpret_cast<const f32x4*>(q.wh + k);
+    const f32x4 w1 = *reinterpret_cast<const f32x4*>(q.wh + k + 4);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dot += (float)v[e] * w0[e];
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dot += (float)v[4 + e] * w1[e];
+  }
+#pragma unroll
+  for (int sh = 8; sh >= 1; sh >>= 1) dot += __shfl_xor(dot, sh, 64);
+  const bool valid = r < nvalid;
+  const float d = dot + q.bh[0] - q.y[r];
+  const float dl = valid ? 2.f * d * p.inv_count : 0.f;
+  if (g == 0) {
+    q.dls[r] = dl;
+    q.lss[r] = valid ? d * d : 0.f;
+  }
+  __syncthreads();
+  rb_head_partials<H>(p, z, q.dls, q.lss, tid);
+  __syncthreads();   // every partial has read a before dZ replaces it
+#pragma unroll
+  for (int c = 0; c < CPT; ++c) {
+    const int k = 8 * (g + 16 * c);
+    bf16x8* pz = reinterpret_cast<bf16x8*>(z + rb_off(r, k));
+    const bf16x8 v = *pz;
+    const f32x4 w0 = *reinterpret_cast<const f32x4*>(q.wh + k);
+    const f32x4 w1 = *reinterpret_cast<const f32x4*>(q.wh + k + 4);
+    bf16x8 o;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      o[e] = (bf16)(dl * w0[e] * act_bwd_t<ACT>((float)v[e]));
+      o[4 + e] = (bf16)(dl * w1[e] * act_bwd_t<ACT>((float)v[4 + e]));
+    }
+    *pz = o;
+  }
+}
+
+template <int H, int ACT, int D, int ABL = 0>
+__global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
+  using G = Rb2Geom<H>;
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int blk = blockIdx.x;
+  const int row0 = blk * RB_ROWS;
+  const int nvalid = min(RB_ROWS, p.rows - row0);
+  const int nh = p.nh, IN = p.in;
+  // column group of this wave, rotated per block so the 32 blocks of an XCD do not all fetch
+  // the same weight lines at the same moment
+  const int cg = (w + blk) & (RB_WAVES - 1);
+  const int n0 = cg * G::WCOLS;
+  const int SL = RB_ROWS * max(H, IN) * 2;
+  const int nslot = max(nh, 2);
+  auto slot = [&](int i) { return smem + i * SL; };
+  const Rb2Par q = rb2_par(smem + nslot * SL, H, nh);
+
+  // the band's rows and the small operands first, then the ring: every global load the
+  // compiler waits for precedes the ring refills, so its vmcnt bookkeeping sees the same D
+  // ring slots in flight on every path into the main loops
+  rb2_load_in(slot(0), p.X + (long long)row0 * p.ldx, p.ldx, IN, nvalid, tid);
+  for (int i = tid; i < nh * (H / 4); i += RB_THREADS) {
+    const int l = i / (H / 4), c = i % (H / 4);
+    reinterpret_cast<f32x4*>(q.bias)[i] = reinterpret_cast<const f32x4*>(p.b[l])[c];
+  }
+  for (int i = tid; i < H / 4; i += RB_THREADS) reinterpret_cast<f32x4*>(q.wh)[i] = reinterpret_cast<const f32x4*>(p.wh)[i];
+  if (tid < RB_ROWS) q.y[tid] = p.y[row0 + min(tid, nvalid - 1)];
+  if (tid == 0) q.bh[0] = p.bh[0];
+  bf16x8 ring[D][G::NF];
+  Rb2Mat cur = rb2_mat<H>(p, 0, cg);
+#pragma unroll
+  for (int d = 0; d < D; ++d) rb2_issue<G::NJ>(ring[d], cur.b, cur.ts, d, lane * 16);
+  __syncthreads();
+
+  f32x4 acc[2][G::NJ];
+  // ---- forward: a_l = act(a_{l-1} W_l^T + b_l) ----
+  for (int l = 0; l < nh; ++l) {
+    const Rb2Mat nxt = rb2_mat<H>(p, l + 1, cg);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < G::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const char* in = slot(l == 0 ? 0 : l);
+    char* out = l < nh - 1 ? slot(l + 1) : slot(nh >= 2 ? 0 : 1);
+    rb2_mainloop<H, D, ABL>(ring, acc, in, cur, nxt, lane);
+    // lane holds out[16i + (lane & 15)][n0 + 16j + 4(lane >> 4) .. +3]
+    const float* bl = q.bias + l * H + n0 + 4 * (lane >> 4);
+#pragma unroll
+    for (int j = 0; j < G::NJ; ++j) {
+      const f32x4 bv = *reinterpret_cast<const f32x4*>(bl + 16 * j);
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const f32x4 v = acc[i][j] + bv;
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (bf16)act_fwd_t<ACT>(v[r]);
+        *reinterpret_cast<bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * j + 4 * (lane >> 4))) = o;
+      }
+    }
+    __syncthreads();
+    if (ABL != 3) rb_copy_out<H>(out, p.a[l] + (long long)row0 * H, H, nvalid, tid);
+    cur = nxt;
+  }
+  // ---- head (in place on a_{nh-1}) ----
+  char* z = slot(nh >= 2 ? 0 : 1);
+  rb2_head<H, ACT>(p, z, q, nvalid, tid);
+  __syncthreads();
+  rb_copy_out<H>(z, p.dz[nh - 1] + (long long)row0 * H, H, nvalid, tid);
+  // ---- activation gradients: dZ_{l-1} = (dZ_l W_l) * act'(a_{l-1}), in place over a_{l-1} ----
+  for (int l = nh - 1; l >= 1; --l) {
+    const Rb2Mat nxt = rb2_mat<H>(p, 2 * nh - l, cg);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < G::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    char* out = slot(l);   // holds a_{l-1}
+    rb2_mainloop<H, D, ABL>(ring, acc, z, cur, nxt, lane);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < G::NJ; ++j) {
+        bf16x4* po = reinterpret_cast<bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * j + 4 * (lane >> 4)));
+        const bf16x4 ax = *po;
+        bf16x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc[i][j][r] * act_bwd_t<ACT>((float)ax[r]));
+        *po = o;
+      }
+    __syncthreads();
+    if (ABL != 3) rb_copy_out<H>(out, p.dz[l - 1] + (long long)row0 * H, H, nvalid, tid);
+    z = out;
+    cur = nxt;
+  }
+}
+
+static int rb2_smem(int H, int in, int nh) {
+  return std::max(nh, 2) * RB_ROWS * std::max(H, in) * 2 + rb2_par_bytes(H, nh);
+}
+
+static bool rowband2_shape_ok(int H, int in, int nh) {
+  // (the instantiated widths: rowband_fwd_bwd)
+  if (H != 256 && H != 384 && H != 512 && H != 768 && H != 1024) return false;
+  const int D = rb2_depth_rt(H);
+  if (in % 64 || in < 64 || (in / 64) % D || (H / 64) % D) return false;
+  return rb2_smem(H, in, nh) <= 160 * 1024;
 }
 
 static int rb_env(const char* name, int dflt) {
@@ -397,8 +742,120 @@ static int rb_env(const char* name, int dflt) {
   return (e && e[0] >= '0' && e[0] <= '9') ? std::atoi(e) : dflt;
 }
 
+template <int H>
+static hipError_t rowband2_launch(const RowbandArgs& p, hipStream_t s) {
+  using Fn = void (*)(RowbandArgs);
+  constexpr int D = rb2_depth<H>();
+  static const Fn fns[3] = {rowband2_kernel<H, ACT_NONE, D>, rowband2_kernel<H, ACT_RELU, D>,
+                            rowband2_kernel<H, ACT_TANH, D>};
+  static bool attr = false;
+  if (!attr) {
+    for (Fn f : fns)
+      (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  Fn f = fns[p.act == ACT_RELU ? 1 : p.act == ACT_TANH ? 2 : 0];
+  static const int abl = rb_env("NNMPI_RB2_ABL", 0);   // TEMPORARY ablation (measurement only)
+  if (abl > 0 && H == 512 && p.act == ACT_RELU) {
+    static const Fn ab[4] = {nullptr, rowband2_kernel<512, ACT_RELU, 4, 1>, rowband2_kernel<512, ACT_RELU, 4, 2>,
+                             rowband2_kernel<512, ACT_RELU, 4, 3>};
+    f = ab[abl & 3];
+    (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+  }
+  hipLaunchKernelGGL(f, dim3(rowband_blocks(p.rows)), dim3(RB_THREADS), rb2_smem(H, p.in, p.nh), s, p);
+  return hipGetLastError();
+}
+
+// ---- fragment-major weight images (rb_pk_off) of every hidden layer: Pf[l] = W_l ([H][in_l]),
+// Pd[l] = W_l^T ([in_l][H], l >= 1), one thread per 16-byte fragment piece ----
+struct RbPackJob {
+  const bf16* W;     // source [rows][ld] row-major
+  bf16* dst;         // fragment-major image of M = W (trans 0) or W^T (trans 1), M is [NR][KC]
+  int ld, KC, trans;
+  long long start;   // first 16-byte piece of this job in the launch
+};
+struct RbPackParams {
+  RbPackJob job[2 * RB_MAXL];
+  int nj;
+  long long total;
+};
+
+__global__ void __launch_bounds__(256) rb_pack_kernel(RbPackParams g) {
+  const long long id = (long long)blockIdx.x * 256 + threadIdx.x;
+  if (id >= g.total) return;
+  int j = 0;
+#pragma unroll 1
+  while (j + 1 < g.nj && id >= g.job[j + 1].start) ++j;
+  const RbPackJob& jb = g.job[j];
+  const long long c = id - jb.start;
+  const int lane = (int)(c & 63);
+  const long long frag = c >> 6;
+  const int KH = jb.KC >> 5;
+  const int n = (int)(frag / KH) * 16 + (lane & 15);
+  const int k0 = (int)(frag % KH) * 32 + 8 * (lane >> 4);
+  bf16x8 v;
+  if (!jb.trans) {
+    v = *reinterpret_cast<const bf16x8*>(jb.W + (long long)n * jb.ld + k0);
+  } else {
+#pragma unroll
+    for (int e = 0; e < 8; ++e) v[e] = jb.W[(long long)(k0 + e) * jb.ld + n];
+  }
+  *reinterpret_cast<bf16x8*>(jb.dst + c * 8) = v;
+}
+
+hipError_t rowband_pack(const RowbandArgs& p, hipStream_t s) {
+  RbPackParams g{};
+  long long n = 0;
+  auto add = [&](const bf16* W, const bf16* dst, int ld, int NR, int KC, int trans) {
+    if (!dst) return;
+    g.job[g.nj] = RbPackJob{W, const_cast<bf16*>(dst), ld, KC, trans, n};
+    n += (long long)NR * KC / 8;
+    ++g.nj;
+  };
+  for (int l = 0; l < p.nh; ++l) {
+    const int K = l == 0 ? p.in : p.H;
+    add(p.W[l], p.Pf[l], K, p.H, K, 0);        // forward: W_l [H][K]
+    if (l >= 1) add(p.W[l], p.Pd[l], K, K, p.H, 1);   // dgrad: W_l^T [K][H]
+  }
+  g.total = n;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(rb_pack_kernel, dim3((unsigned)((n + 255) / 256)), dim3(256), 0, s, g);
+  return hipGetLastError();
+}
+
+int rowband_blocks(int rows) { return (rows + RB_ROWS - 1) / RB_ROWS; }
+
+bool rowband_ok(int rows, int H, int in, int nh, int out, int loss, int act) {
+  return rows > 0 && H == 512 && in == H && nh >= 1 && nh <= RB_MAXL && out == 1 &&
+         loss == LOSS_MSE && (act == ACT_RELU || act == ACT_TANH || act == ACT_NONE);
+}
+
+bool rowband2_ok(int rows, int H, int in, int nh, int out, int loss, int act) {
+  return rows > 0 && nh >= 1 && nh <= RB_MAXL && out == 1 && loss == LOSS_MSE &&
+         (act == ACT_RELU || act == ACT_TANH || act == ACT_NONE) && rowband2_shape_ok(H, in, nh);
+}
+
+size_t rowband_packed_elems(int H, int in, int nh) {
+  // forward images of every layer + dgrad images of layers 1 .. nh-1
+  return (size_t)H * in + (size_t)(nh - 1) * H * H * 2;
+}
+
+
 hipError_t rowband_fwd_bwd(const RowbandArgs& p0, hipStream_t s) {
   RowbandArgs p = p0;
+  if (p.Pf[0]) {   // v2: packed weight images
+    if (!rowband2_ok(p.rows, p.H, p.in, p.nh, 1, LOSS_MSE, p.act)) return hipErrorInvalidValue;
+    for (int l = 0; l < p.nh; ++l)
+      if (!p.Pf[l] || (l >= 1 && !p.Pd[l])) return hipErrorInvalidValue;
+    switch (p.H) {
+      case 256: return rowband2_launch<256>(p, s);
+      case 384: return rowband2_launch<384>(p, s);
+      case 512: return rowband2_launch<512>(p, s);
+      case 768: return rowband2_launch<768>(p, s);
+      case 1024: return rowband2_launch<1024>(p, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
   if (!rowband_ok(p.rows, p.H, p.H, p.nh, 1, LOSS_MSE, p.act)) return hipErrorInvalidValue;
 
   using G = RbGeom<512>;
@@ -426,17 +883,20 @@ static int rb_splits(int splits, int nh, int H, int rows) {
   return env > 0 ? env : wgrad_multi_splits(nh, H, H, rows);
 }
 
-size_t rowband_workspace_bytes(int rows, int H, int nh, int splits) {
+size_t rowband_workspace_bytes(int rows, int H, int in, int nh, int splits) {
   const size_t G = (size_t)rowband_blocks(rows);
   const int S = rb_splits(splits, nh, H, rows);
   const size_t head = G * H + rb_pad4(G) + rb_pad4(G);
-  return (head + (size_t)nh * S * ((size_t)H * H + H)) * sizeof(float);
+  return (head + (size_t)nh * S * ((size_t)H * std::max(H, in) + H)) * sizeof(float);
 }
 
 hipError_t rowband_step(const RowbandStep& st0, hipStream_t s) {
   RowbandStep st = st0;
   RowbandArgs& p = st.fb;
-  if (!rowband_ok(p.rows, p.H, p.H, p.nh, 1, LOSS_MSE, p.act) || !st.ws) return hipErrorInvalidValue;
+  if (!p.Pf[0]) p.in = p.H;
+  const bool ok = p.Pf[0] ? rowband2_ok(p.rows, p.H, p.in, p.nh, 1, LOSS_MSE, p.act)
+                          : rowband_ok(p.rows, p.H, p.H, p.nh, 1, LOSS_MSE, p.act);
+  if (!ok || !st.ws) return hipErrorInvalidValue;
   const int H = p.H, nh = p.nh;
   const size_t G = (size_t)rowband_blocks(p.rows);
   float* ws = st.ws;
@@ -449,12 +909,21 @@ hipError_t rowband_step(const RowbandStep& st0, hipStream_t s) {
   const int S = rb_splits(st.splits, nh, H, p.rows);
   WgradArgs jobs[RB_MAXL];
   SlabReduce red[RB_MAXL + 1];
+  const size_t per = (size_t)S * ((size_t)H * std::max(H, p.in) + H);
   for (int l = 0; l < nh; ++l) {
     jobs[l] = WgradArgs{p.dz[l], H, l == 0 ? p.X : p.a[l - 1], l == 0 ? p.ldx : H, st.gW[l],
-                        st.gb[l], H, H, p.rows, slabs + (size_t)l * S * ((size_t)H * H + H), st.sg};
+                        st.gb[l], H, l == 0 ? p.in : H, p.rows, slabs + (size_t)l * per, st.sg};
   }
   e = wgrad_multi(jobs, nh, S, red, s);
   if (e != hipSuccess) return e;
+  if (st.sg.g_base && p.Pf[0]) {
+    // one rank: the combines apply the update, and write the v2 weight images of the NEW weights
+    // for the next step's row-band launch
+    for (int l = 0; l < nh; ++l) {
+      red[l].pkf = const_cast<bf16*>(p.Pf[l]);
+      red[l].pkd = l >= 1 ? const_cast<bf16*>(p.Pd[l]) : nullptr;
+    }
+  }
   red[nh] = SlabReduce{p.wslab, (int)G, H, 1, H, st.gWh, H, p.bslab, 1, st.gbh, p.loss_part, (int)G,
                        st.loss_scale, st.loss_out, st.sg};
   return slab_reduce_multi(red, nh + 1, s);

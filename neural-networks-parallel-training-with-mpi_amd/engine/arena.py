@@ -84,6 +84,7 @@ class Arena:
         ``chunk_layers``: cut layers larger than a bucket into output-row chunk buckets."""
         self.layer_shapes = list(layer_shapes)
         self.n_layers = len(layer_shapes)
+        self.version = 0
         self.device = torch.device(device)
         slots: List[Slot] = []
         off = 0
@@ -155,6 +156,10 @@ class Arena:
             lin.bias.data = self.bias(li)
 
     def sync_shadow(self) -> None:
+        """Refresh the bf16 shadow after the master weights were written outside an optimizer
+        step (model binding, state_dict load, broadcast).  Bumps ``version``: derived weight
+        copies (the row-band v2 images, engine.py) are rebuilt before their next use."""
+        self.version += 1
         if self.shadow is not None:
             self.shadow.copy_(self.master)
 

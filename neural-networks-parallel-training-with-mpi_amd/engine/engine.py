@@ -123,8 +123,20 @@ class MLPEngine:
         self.rowband = (self.overlap and dtype == torch.bfloat16 and inline_sync and
                         hasattr(ops, "rowband_ok") and os.environ.get("NNMPI_ROWBAND", "1") != "0"
                         and ops.rowband_ok(self.R, w, self.act, spec.loss))
-        self.ws_rb = (torch.zeros(ops.rowband_workspace_bytes(self.R, w[1], L - 1) // 4 + 64,
+        self.ws_rb = (torch.zeros(ops.rowband_workspace_bytes(self.R, w[1], L - 1, in_=w[0]) // 4 + 64,
                                   dtype=torch.float32, device=dev) if self.rowband else None)
+        # v2 row-band kernel: the weights also live in fragment-major images (one global load per
+        # MFMA operand, no LDS staging -- rowband.hip).  The images must hold the CURRENT weights:
+        # the single-rank fused combine rewrites them from the updated weights; every other
+        # update path (the multi-rank SGD pass, ZeRO-1, other schedules, a reload of the arena
+        # -- Arena.version) leaves them stale and the next row-band step rebuilds them first.
+        self.rb_version = (ops.rowband_version(self.R, w, self.act, spec.loss) if self.rowband
+                           and hasattr(ops, "rowband_version") else (1 if self.rowband else 0))
+        self.rb_packed = None
+        if self.rb_version == 2:
+            self._rb_buf, self.rb_packed = ops.rowband_packed(w[1], w[0], L - 1, dev)
+        self._rb_fresh = False
+        self._rb_ver = -1
         # A band's passes cost the same whatever the number of bands (per-CU bound: 47 us at
         # 1,024 rows as at 8,192, profiles/r3s2_rowband_pmc.txt), so small batches (strong-scaling
         # shards, mini-batches) keep the grouped schedule: 0.053 vs ~0.064 ms at 1,024 rows.
@@ -386,8 +398,20 @@ class MLPEngine:
                       ar.grad_weight(last), ar.grad_bias(last), self.dlogits[:rows], self.loss_out,
                       self.loss_scale, ws=self.ws, **kw)
 
+    def _rb_current(self) -> bool:
+        """The v2 row-band weight images hold the current weights."""
+        return self._rb_fresh and self._rb_ver == self.arena.version
+
+    def _rb_pack(self):
+        """Rebuild the v2 weight images from the bf16 shadow (one launch, on the engine's stream)."""
+        self.ops.rowband_pack([self.arena.compute_weight(i) for i in range(self.L - 1)],
+                              self.rb_packed)
+        self._rb_fresh, self._rb_ver = True, self.arena.version
+
     def _step_body(self, first: bool):
         self._mark("start")
+        if not (self.overlap and self.rows > 0 and self.uses_rowband(self.rows)):
+            self._rb_fresh = False        # this step updates the weights without the images
         if self.overlap and self.rows > 0:
             self._step_body_overlap(first)
         else:
@@ -559,9 +583,17 @@ class MLPEngine:
         last = L - 1
         layers = [(ar.compute_weight(i), ar.bias(i), self.acts[i][:rows], self._dzl(i, rows),
                    ar.grad_weight(i), ar.grad_bias(i)) for i in range(L - 1)]
+        kw = {}
+        if self.rb_packed is not None:
+            if not self._rb_current():
+                self._rb_pack()
+            kw["packed"] = self.rb_packed
         ops.rowband_step(self.X[:rows], layers, ar.weight(last), ar.bias(last), self.Y[:rows],
                          self.inv_count, ar.grad_weight(last), ar.grad_bias(last), self.ws_rb,
-                         self.loss_scale, self.loss_out, self.act, sgd=fz)
+                         self.loss_scale, self.loss_out, self.act, sgd=fz, **kw)
+        # the fused combine rewrote the images from the updated weights; the multi-rank update
+        # below does not
+        self._rb_fresh = fz is not None
         self._mark("bwd")
         if fz is not None:
             return
@@ -890,6 +922,8 @@ class MLPEngine:
         """Capture ``body()`` (work on the engine's streams) as one replayable graph."""
         from .. import native
         g = native.lib().GraphRunner()
+        # the row-band image state the captured body assumes at its start, and leaves behind
+        rb_pre = (self._rb_fresh, self._rb_ver)
         origin = self.sync.capture_origin()
         if origin is None:
             origin = self.stream
@@ -906,13 +940,17 @@ class MLPEngine:
         except Exception:
             self.sync.record(False)
             g.cancel()    # leave the stream out of capture mode, drop the partial graph
+            self._rb_fresh, self._rb_ver = rb_pre
             raise
         notes = self.sync.record(False)
         g.end()
         # the capture issued these collectives once, but every launch runs them: the launch
         # adds them to the collective signature (utils/seqcheck.py), the capture does not
         self.sync.seq -= len(notes)
-        return _Graph(g, self.sync, notes)
+        rb_post = self._rb_fresh
+        self._rb_fresh, self._rb_ver = rb_pre     # nothing ran yet
+        return _Graph(g, self.sync, notes, self,
+                      rb_pre[0] and rb_pre[1] == self.arena.version, rb_post)
 
     # ---------------- gradient accumulation ----------------------------------------------------
     # Not in the reference (one backward per step, SURVEY.md §2.3 "optional").  A step over more
@@ -963,6 +1001,7 @@ class MLPEngine:
                 self.sync.ready(i)
             self.sync.finish()
             self._update(first)
+        self._rb_fresh = False
         self._n_acc = 0
         self.steps_done += 1
 
@@ -1028,14 +1067,24 @@ class MLPEngine:
 
 
 class _Graph:
-    """A captured graph plus the collectives it issues per launch (for the signature)."""
+    """A captured graph plus the collectives it issues per launch (for the signature) and the
+    row-band weight-image state it was captured under: a body captured with current images
+    skips their rebuild, so before it replays on stale images they are rebuilt eagerly."""
 
-    def __init__(self, runner, sync, notes):
+    def __init__(self, runner, sync, notes, engine=None, rb_pre: bool = False,
+                 rb_post: bool = False):
         self.runner, self.sync, self.notes = runner, sync, notes
+        self.engine, self.rb_pre, self.rb_post = engine, rb_pre, rb_post
 
     def launch(self, stream_handle: int):
+        eng = self.engine
+        if eng is not None and eng.rb_packed is not None and self.rb_pre and not eng._rb_current():
+            with torch.cuda.stream(eng.stream):
+                eng._rb_pack()
         self.runner.launch(stream_handle)
         self.sync.replay(self.notes)
+        if eng is not None:
+            eng._rb_fresh, eng._rb_ver = self.rb_post, eng.arena.version
 
 
 class _SilentSync:

@@ -6,6 +6,9 @@ captured into a hipGraph).  Workspaces are provided by the caller (the engine si
 """
 from __future__ import annotations
 
+import os
+from typing import Optional, Tuple
+
 import torch
 
 from .. import native
@@ -291,44 +294,95 @@ class HipOps:
             self.lib.slab_reduce(pending, self.stream)
 
     # ---------------- row-band step (rowband.hip) ----------------
-    def rowband_ok(self, rows: int, widths, act: str, loss: str) -> bool:
-        """Input and hidden widths all equal (512), out == 1, MSE: the whole forward + head +
-        activation-gradient chain runs as one launch per step (see rowband.hip)."""
+    def rowband_version(self, rows: int, widths, act: str, loss: str) -> int:
+        """2: the v2 row-band step (fragment-major weight images) runs this model -- hidden
+        widths all equal (H % 128 == 0, 256..1024), input width % 128 == 0, out == 1, MSE;
+        1: only the v1 kernel (H == in == 512); 0: neither."""
         widths = list(widths)
-        if len(widths) < 3 or any(w != widths[0] for w in widths[:-1]):
-            return False
-        return bool(self.lib.rowband_ok(int(rows), widths[1], widths[0], len(widths) - 2,
-                                        widths[-1], LOSS_CODES.get(loss, -1), ACT_CODES[act]))
+        if len(widths) < 3 or any(w != widths[1] for w in widths[1:-1]):
+            return 0
+        H, in_, nh, out = widths[1], widths[0], len(widths) - 2, widths[-1]
+        lc, ac = LOSS_CODES.get(loss, -1), ACT_CODES[act]
+        if os.environ.get("NNMPI_RB_V2", "1") != "0" and \
+                self.lib.rowband2_ok(int(rows), H, in_, nh, out, lc, ac):
+            return 2
+        if in_ == H and self.lib.rowband_ok(int(rows), H, in_, nh, out, lc, ac):
+            return 1
+        return 0
 
-    def rowband_workspace_bytes(self, rows: int, H: int, nh: int, splits: int = 0) -> int:
-        return int(self.lib.rowband_workspace_bytes(int(rows), int(H), int(nh), int(splits)))
+    def rowband_ok(self, rows: int, widths, act: str, loss: str) -> bool:
+        """The whole forward + head + activation-gradient chain runs as one launch per step
+        (see rowband.hip)."""
+        return self.rowband_version(rows, widths, act, loss) > 0
+
+    def rowband_workspace_bytes(self, rows: int, H: int, nh: int, splits: int = 0,
+                                in_: Optional[int] = None) -> int:
+        return int(self.lib.rowband_workspace_bytes(int(rows), int(H), int(H if in_ is None else in_),
+                                                    int(nh), int(splits)))
+
+    def rowband_packed(self, H: int, in_: int, nh: int, device) -> Tuple[torch.Tensor, list]:
+        """The v2 weight images of one model: one bf16 buffer and, per hidden layer, the
+        (forward image, dgrad image) views (layer 0 has no dgrad image)."""
+        buf = torch.zeros(int(self.lib.rowband_packed_elems(H, in_, nh)), dtype=torch.bfloat16,
+                          device=device)
+        views, o = [], 0
+        for l in range(nh):
+            k = in_ if l == 0 else H
+            pf = buf[o:o + H * k]
+            o += H * k
+            pd = None
+            if l >= 1:
+                pd = buf[o:o + H * H]
+                o += H * H
+            views.append((pf, pd))
+        return buf, views
+
+    @staticmethod
+    def _packed_ptrs(packed):
+        return None if packed is None else [(_p(pf), _p(pd) if pd is not None else 0)
+                                            for pf, pd in packed]
+
+    def rowband_pack(self, weights, packed):
+        """Rebuild the v2 weight images from the row-major bf16 weights (one launch)."""
+        H, in_ = weights[0].shape
+        self.lib.rowband_pack(int(H), int(in_), [_p(W) for W in weights], self._packed_ptrs(packed),
+                              self.stream)
 
     def rowband_step(self, X, layers, wh, bh, y, inv_count: float, gWh, gbh, ws, loss_scale: float,
-                     loss_out, act: str, sgd=None, splits: int = 0):
-        """One step body of a narrow square MSE regressor in three launches.  ``layers``: per
-        hidden layer ``(W16, b, a_out, dz_out, gW, gb)``.  Writes every activation and dZ, the
-        gradients (or, with ``sgd``, applies the fused update at their arena positions) and
-        ``loss_out[0] = loss_scale * sum of squared errors``."""
-        rows, H = X.shape
+                     loss_out, act: str, sgd=None, splits: int = 0, packed=None):
+        """One step body of a narrow MSE regressor in three launches.  ``layers``: per hidden
+        layer ``(W16, b, a_out, dz_out, gW, gb)``.  Writes every activation and dZ, the
+        gradients (or, with ``sgd``, applies the fused update at their arena positions -- and
+        rewrites the ``packed`` v2 weight images from the new weights) and
+        ``loss_out[0] = loss_scale * sum of squared errors``.  ``packed``: the v2 weight images
+        (must match the weights); None runs the v1 kernel."""
+        rows, in_ = X.shape
         nh = len(layers)
+        H = layers[0][0].shape[0]
         _check(X.dtype == torch.bfloat16 and X.stride(1) == 1, "rowband: bf16 rows")
-        _check(self.lib.rowband_ok(rows, H, H, nh, 1, LOSS_CODES["mse"], ACT_CODES[act]),
-               "rowband: shape")
-        self._check_ws(ws, self.rowband_workspace_bytes(rows, H, nh, splits), "rowband")
+        ok = (self.lib.rowband2_ok(rows, H, in_, nh, 1, LOSS_CODES["mse"], ACT_CODES[act])
+              if packed is not None else
+              in_ == H and self.lib.rowband_ok(rows, H, H, nh, 1, LOSS_CODES["mse"], ACT_CODES[act]))
+        _check(ok, "rowband: shape")
+        self._check_ws(ws, self.rowband_workspace_bytes(rows, H, nh, splits, in_), "rowband")
         lay = []
-        for W, b, a, dz, gW, gb in layers:
-            _check(tuple(W.shape) == (H, H) and W.is_contiguous() and W.dtype == torch.bfloat16,
-                   "rowband: bf16 [H, H] weights")
+        for l, (W, b, a, dz, gW, gb) in enumerate(layers):
+            k = in_ if l == 0 else H
+            _check(tuple(W.shape) == (H, k) and W.is_contiguous() and W.dtype == torch.bfloat16,
+                   "rowband: bf16 [H, in] weights")
             _check(a.shape[0] >= rows and dz.shape[0] >= rows and a.stride(0) == H and
                    dz.stride(0) == H and a.dtype == dz.dtype == torch.bfloat16,
                    "rowband: dense bf16 activation buffers")
-            _check(gW.is_contiguous() and gW.numel() == H * H and gb.numel() == H and
+            _check(gW.is_contiguous() and gW.numel() == H * k and gb.numel() == H and
                    b.numel() == H, "rowband: gradient / bias shapes")
             lay.append((_p(W), _p(b), _p(a), _p(dz), _p(gW), _p(gb)))
         _check(y.numel() >= rows and wh.numel() == H, "rowband: head shapes")
-        self.lib.rowband_step(_p(X), X.stride(0), rows, H, ACT_CODES[act], lay, _p(wh), _p(bh),
-                              _p(y), float(inv_count), _p(gWh), _p(gbh), _p(ws),
-                              float(loss_scale), _p(loss_out), sgd, int(splits), self.stream)
+        if packed is not None:
+            _check(len(packed) == nh, "rowband: one (forward, dgrad) image pair per hidden layer")
+        self.lib.rowband_step(_p(X), X.stride(0), rows, H, in_, ACT_CODES[act], lay, _p(wh),
+                              _p(bh), _p(y), float(inv_count), _p(gWh), _p(gbh), _p(ws),
+                              float(loss_scale), _p(loss_out), sgd, int(splits),
+                              self._packed_ptrs(packed), self.stream)
 
     # ---------------- tiny fused MLP ----------------
     def tiny_workspace_bytes(self, rows, numel) -> int:

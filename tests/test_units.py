@@ -282,17 +282,52 @@ def test_rowband_host_sizing_invariants():
     assert lib.wgrad_multi_splits(3, 512, 512, 512) == 2          # 8 k-steps: >= 4 per split
     assert lib.rowband_blocks(8192) == 256 and lib.rowband_blocks(8191) == 256
     assert lib.rowband_blocks(37) == 2
-    cap = lib.rowband_workspace_bytes(8192, 512, 3, 0)
+    cap = lib.rowband_workspace_bytes(8192, 512, 512, 3, 0)
     prev = 0
     for rows in (1, 31, 32, 33, 1000, 4096, 6144, 8000, 8191, 8192):
-        need = lib.rowband_workspace_bytes(rows, 512, 3, 0)
+        need = lib.rowband_workspace_bytes(rows, 512, 512, 3, 0)
         assert prev <= need <= cap, rows
         prev = need
+    # a wider input layer needs a larger first-layer slab
+    assert lib.rowband_workspace_bytes(8192, 512, 1024, 3, 0) > cap
     assert lib.rowband_ok(8192, 512, 512, 3, 1, 0, 1)
-    assert not lib.rowband_ok(8192, 1024, 1024, 3, 1, 0, 1)      # H = 512 only
-    assert not lib.rowband_ok(8192, 512, 784, 3, 1, 0, 1)        # input width = H
+    assert not lib.rowband_ok(8192, 1024, 1024, 3, 1, 0, 1)      # v1: H = 512 only
+    assert not lib.rowband_ok(8192, 512, 784, 3, 1, 0, 1)        # v1: input width = H
     assert not lib.rowband_ok(8192, 512, 512, 3, 10, 1, 1)       # MSE regression head only
     assert not lib.rowband_ok(0, 512, 512, 3, 1, 0, 1)
+    # v2 (fragment-major weight images): H in {256, 384, 512, 768, 1024}, input width % 128 == 0,
+    # every activation slot + the parameter block in the 160 KiB LDS
+    for H, in_, nh in ((512, 512, 3), (512, 512, 4), (256, 256, 4), (384, 128, 2),
+                       (768, 768, 3), (1024, 1024, 2), (512, 1024, 2), (256, 512, 1)):
+        assert lib.rowband2_ok(8192, H, in_, nh, 1, 0, 1), (H, in_, nh)
+        k = [in_] + [H] * (nh - 1)
+        assert lib.rowband_packed_elems(H, in_, nh) == sum(H * x for x in k) + H * H * (nh - 1)
+    assert not lib.rowband2_ok(8192, 1024, 1024, 3, 1, 0, 1)     # 3 x 64 KiB slots
+    assert not lib.rowband2_ok(8192, 512, 784, 3, 1, 0, 1)       # input width % 128
+    assert not lib.rowband2_ok(8192, 640, 640, 2, 1, 0, 1)       # H in {256, 384, 512, 768, 1024}
+    assert not lib.rowband2_ok(8192, 512, 576, 2, 1, 0, 1)       # in % 128 (ring: k-steps % 2)
+    assert not lib.rowband2_ok(8192, 2048, 2048, 1, 1, 0, 1)     # H <= 1024
+    assert not lib.rowband2_ok(8192, 512, 512, 3, 10, 1, 1)      # MSE regression head only
+
+
+def test_rowband_fragment_major_offsets():
+    """rb_pk_off (common.h) is a bijection of a [N][K] matrix onto its fragment-major image: 1 KiB
+    per 16 x 32 fragment, lane (n & 15) + 16 * ((k >> 3) & 3) holding 8 consecutive k.  Checked
+    against the v_mfma_f32_16x16x32_bf16 operand map (cdna_hip_programming.md §3)."""
+    N, K = 48, 96
+    seen = set()
+    for n in range(N):
+        for k in range(K):
+            frag, rem = divmod(_rb_pk_off(n, k, K), 512)
+            lane, e = divmod(rem, 8)
+            assert frag == (n // 16) * (K // 32) + k // 32
+            assert (lane & 15) == n % 16 and 8 * (lane >> 4) + e == k % 32
+            seen.add((frag, lane, e))
+    assert len(seen) == N * K
+
+
+def _rb_pk_off(n, k, K):
+    return (((n >> 4) * (K >> 5) + (k >> 5)) * 64 + ((n & 15) + 16 * ((k >> 3) & 3))) * 8 + (k & 7)
 
 
 def test_shm_allreduce_sums_in_rank_order_and_times_out():
