@@ -223,7 +223,11 @@ def main(argv=None):
             _fail(f"{job.local_world} local ranks need as many GPUs; {have} visible "
                   "(one rank per GPU: RCCL refuses two ranks on one device)")
     from nnmpi_amd.parallel import supervisor as sup
-    if job.world > 1 and not sup.supervised() and os.environ.get("NNMPI_BENCH_SUPERVISE", "1") != "0":
+    # (supervise only where the supervisors' rendezvous is shared by every rank: a TCP store at
+    # MASTER_ADDR, or -- for a plain mpiexec -- all ranks on this node, which share the
+    # launcher's FileStore; a multi-node mpiexec without MASTER_* runs unsupervised)
+    if (job.world > 1 and not sup.supervised() and sup.rendezvous_shared(job.world, job.local_world)
+            and os.environ.get("NNMPI_BENCH_SUPERVISE", "1") != "0"):
         # this process never touches the GPU: it runs the rank as a child and retries the whole
         # job in fresh processes with a more conservative schedule if any rank dies or hangs
         sys.exit(supervise(a, argv, job))
@@ -275,8 +279,8 @@ def run(a, job):
     from nnmpi_amd.engine.trainer import loss_scales
     from nnmpi_amd.models.mlp import MLPSpec, reference_init
     from nnmpi_amd.parallel import dist as pdist
-    from nnmpi_amd.parallel.sync import (NativeRcclSync, NoSync, ShardedSync, ShmSync,
-                                         TorchDistSync, shm_sync_ok)
+    from nnmpi_amd.parallel.sync import (NativeRcclSync, NoSync, ShardedSync, TorchDistSync,
+                                         make_shm_sync, shm_sync_ok)
     from nnmpi_amd.parallel.supervisor import supervised, write_result
     from nnmpi_amd.utils.config import TrainConfig
     from nnmpi_amd.utils.metrics import comm_volume, scaling_report
@@ -370,10 +374,11 @@ def run(a, job):
             arena.sync_shadow()
             if zero1:
                 sync = ShardedSync(arena, world, rank, group=comm_group)
-            elif shm_sync_ok(dev.type, world, job.local_world, grad_dtype):
-                sync = ShmSync(arena, comm_group, world, rank)
             else:
-                sync = TorchDistSync(arena, comm_group, world, grad_dtype=grad_dtype)
+                sync = (make_shm_sync(arena, comm_group, world, rank)
+                        if shm_sync_ok(dev.type, world, job.local_world, grad_dtype) else None)
+                if sync is None:
+                    sync = TorchDistSync(arena, comm_group, world, grad_dtype=grad_dtype)
         eng = MLPEngine(spec, arena, make_ops(), sync, device=dev, dtype=dtype,
                         rows_capacity=max(rows, 1), lr=a.lr, momentum=0.9,
                         use_graph=not a.no_graph, overlap=not a.no_overlap,

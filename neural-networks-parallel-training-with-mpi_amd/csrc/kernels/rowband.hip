@@ -494,7 +494,7 @@ __device__ __forceinline__ Rb2Mat rb2_mat(const RowbandArgs& p, int q, int cg) {
 // do-while: every matrix has >= D k-steps, and a loop the compiler must assume can be skipped
 // makes it wait for the refills at the loop exit -- rule: no global load between the ring
 // refills and their use, or vmcnt drains the ring.)
-template <int H, int D, int ABL = 0>
+template <int H, int D>
 __device__ __forceinline__ void rb2_mainloop(bf16x8 (&ring)[D][Rb2Geom<H>::NF],
                                              f32x4 (&acc)[2][Rb2Geom<H>::NJ], const char* img,
                                              const Rb2Mat& cur, const Rb2Mat& nxt, int lane) {
@@ -512,45 +512,56 @@ __device__ __forceinline__ void rb2_mainloop(bf16x8 (&ring)[D][Rb2Geom<H>::NF],
 #pragma unroll
         for (int i = 0; i < 2; ++i) af[i][kk] = read_frag<64, KMAJ>(kb, 16 * i, kk, lane);
       // slot d: every later slot (D - 1 k-steps) may stay in flight, and the second k-half
-      if (ABL != 2) rb2_wait<(D - 1) * G::NF + G::NJ, G::NJ>(ring[d], 0);
+      rb2_wait<(D - 1) * G::NF + G::NJ, G::NJ>(ring[d], 0);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < G::NJ; ++j) {
-          if (ABL == 1) asm volatile("" ::"v"(ring[d][2 * j]), "v"(af[i][0]));
-          else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[d][2 * j], af[i][0], acc[i][j], 0, 0, 0);
-        }
+        for (int j = 0; j < G::NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[d][2 * j], af[i][0], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);   // (the first half's MFMAs stay ahead of the second wait)
-      if (ABL != 2) rb2_wait<(D - 1) * G::NF, G::NJ>(ring[d], 1);
+      rb2_wait<(D - 1) * G::NF, G::NJ>(ring[d], 1);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < G::NJ; ++j) {
-          if (ABL == 1) asm volatile("" ::"v"(ring[d][2 * j + 1]), "v"(af[i][1]));
-          else acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[d][2 * j + 1], af[i][1], acc[i][j], 0, 0, 0);
-        }
+        for (int j = 0; j < G::NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[d][2 * j + 1], af[i][1], acc[i][j], 0, 0, 0);
       // (sched_barrier: the refill stays behind this sub-step's MFMAs, which read the slot)
       __builtin_amdgcn_sched_barrier(0);
       const int sn = s + D;
       const bool inc = sn < cur.ks;
-      if (ABL != 2) rb2_issue<G::NJ>(ring[d], inc ? cur.b : nxt.b, inc ? cur.ts : nxt.ts, inc ? sn : sn - cur.ks, voff);
+      rb2_issue<G::NJ>(ring[d], inc ? cur.b : nxt.b, inc ? cur.ts : nxt.ts, inc ? sn : sn - cur.ks, voff);
       __builtin_amdgcn_sched_barrier(0);
     }
     s0 += D;
   } while (s0 < cur.ks);
 }
 
-// Runtime-width row-contiguous copy between an image of `width` columns and [rows][ld] memory.
+// The band's input rows into the image (runtime width, a multiple of 128 up to 1024): all of a
+// thread's loads are issued before any LDS write, so they are in flight together.  Every load
+// issues unconditionally (past the width: the chunk of iteration 0 again, an L1 hit) -- a load
+// guarded by the runtime width made hipcc wait for each one separately.
 __device__ __forceinline__ void rb2_load_in(char* img, const bf16* src, int ld, int width, int nvalid, int tid) {
-  const int nch = RB_ROWS * width / 8;
-  for (int id = tid; id < nch; id += RB_THREADS) {
-    const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
-    bf16x8 v = *reinterpret_cast<const bf16x8*>(src + (long long)min(r, nvalid - 1) * ld + kb * 64 + k8 * 8);
-    if (r >= nvalid) {
+  constexpr int MAXIT = 1024 * RB_ROWS / 8 / RB_THREADS;   // 8
+  const int nit = width * RB_ROWS / 8 / RB_THREADS;
+  bf16x8 v[MAXIT];
 #pragma unroll
-      for (int e = 0; e < 8; ++e) v[e] = (bf16)0.f;
+  for (int it = 0; it < MAXIT; ++it) {
+    const int id = tid + min(it, nit - 1) * RB_THREADS;
+    const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
+    v[it] = *reinterpret_cast<const bf16x8*>(src + (long long)min(r, nvalid - 1) * ld + kb * 64 + k8 * 8);
+  }
+#pragma unroll
+  for (int it = 0; it < MAXIT; ++it) {
+    if (it < nit) {
+      const int id = tid + it * RB_THREADS;
+      const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
+      bf16x8 x = v[it];
+      if (r >= nvalid) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = (bf16)0.f;
+      }
+      *reinterpret_cast<bf16x8*>(img + kb * (RB_ROWS * 128) + kmaj_off(r, k8)) = x;
     }
-    *reinterpret_cast<bf16x8*>(img + kb * (RB_ROWS * 128) + kmaj_off(r, k8)) = v;
   }
 }
 
@@ -628,7 +639,7 @@ __device__ __forceinline__ void rb2_head(const RowbandArgs& p, char* z, const Rb
   }
 }
 
-template <int H, int ACT, int D, int ABL = 0>
+template <int H, int ACT, int D>
 __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
   using G = Rb2Geom<H>;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
@@ -647,21 +658,33 @@ __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
   auto slot = [&](int i) { return smem + i * SL; };
   const Rb2Par q = rb2_par(smem + nslot * SL, H, nh);
 
-  // the band's rows and the small operands first, then the ring: every global load the
-  // compiler waits for precedes the ring refills, so its vmcnt bookkeeping sees the same D
-  // ring slots in flight on every path into the main loops
-  rb2_load_in(slot(0), p.X + (long long)row0 * p.ldx, p.ldx, IN, nvalid, tid);
-  for (int i = tid; i < nh * (H / 4); i += RB_THREADS) {
-    const int l = i / (H / 4), c = i % (H / 4);
-    reinterpret_cast<f32x4*>(q.bias)[i] = reinterpret_cast<const f32x4*>(p.b[l])[c];
-  }
-  for (int i = tid; i < H / 4; i += RB_THREADS) reinterpret_cast<f32x4*>(q.wh)[i] = reinterpret_cast<const f32x4*>(p.wh)[i];
-  if (tid < RB_ROWS) q.y[tid] = p.y[row0 + min(tid, nvalid - 1)];
-  if (tid == 0) q.bh[0] = p.bh[0];
+  // Startup: the ring's first D k-steps, the band's rows and the small operands are all issued
+  // before the first wait, so the launch pays one memory round trip, not one per operand.
   bf16x8 ring[D][G::NF];
   Rb2Mat cur = rb2_mat<H>(p, 0, cg);
 #pragma unroll
   for (int d = 0; d < D; ++d) rb2_issue<G::NJ>(ring[d], cur.b, cur.ts, d, lane * 16);
+  {
+    // (thread t < H / 4 loads float4 t of every layer's bias and of the head weight; the layer
+    // index is unrolled so each bias pointer is a kernel-argument load, not a memory load of
+    // the pointer array that hipcc would wait for)
+    f32x4 bq[RB_MAXL], wq;
+    const int tq = min(tid, H / 4 - 1);
+#pragma unroll
+    for (int l = 0; l < RB_MAXL; ++l) bq[l] = reinterpret_cast<const f32x4*>(p.b[l < nh ? l : 0])[tq];
+    wq = reinterpret_cast<const f32x4*>(p.wh)[tq];
+    const float yq = p.y[row0 + min(tid & (RB_ROWS - 1), nvalid - 1)];
+    const float bhq = p.bh[0];
+    rb2_load_in(slot(0), p.X + (long long)row0 * p.ldx, p.ldx, IN, nvalid, tid);
+    if (tid < H / 4) {
+#pragma unroll
+      for (int l = 0; l < RB_MAXL; ++l)
+        if (l < nh) reinterpret_cast<f32x4*>(q.bias)[l * (H / 4) + tid] = bq[l];
+      reinterpret_cast<f32x4*>(q.wh)[tid] = wq;
+    }
+    if (tid < RB_ROWS) q.y[tid] = yq;
+    if (tid == 0) q.bh[0] = bhq;
+  }
   __syncthreads();
 
   f32x4 acc[2][G::NJ];
@@ -674,7 +697,7 @@ __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
       for (int j = 0; j < G::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const char* in = slot(l == 0 ? 0 : l);
     char* out = l < nh - 1 ? slot(l + 1) : slot(nh >= 2 ? 0 : 1);
-    rb2_mainloop<H, D, ABL>(ring, acc, in, cur, nxt, lane);
+    rb2_mainloop<H, D>(ring, acc, in, cur, nxt, lane);
     // lane holds out[16i + (lane & 15)][n0 + 16j + 4(lane >> 4) .. +3]
     const float* bl = q.bias + l * H + n0 + 4 * (lane >> 4);
 #pragma unroll
@@ -690,7 +713,7 @@ __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
       }
     }
     __syncthreads();
-    if (ABL != 3) rb_copy_out<H>(out, p.a[l] + (long long)row0 * H, H, nvalid, tid);
+    rb_copy_out<H>(out, p.a[l] + (long long)row0 * H, H, nvalid, tid);
     cur = nxt;
   }
   // ---- head (in place on a_{nh-1}) ----
@@ -706,7 +729,7 @@ __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
 #pragma unroll
       for (int j = 0; j < G::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     char* out = slot(l);   // holds a_{l-1}
-    rb2_mainloop<H, D, ABL>(ring, acc, z, cur, nxt, lane);
+    rb2_mainloop<H, D>(ring, acc, z, cur, nxt, lane);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
@@ -719,7 +742,7 @@ __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
         *po = o;
       }
     __syncthreads();
-    if (ABL != 3) rb_copy_out<H>(out, p.dz[l - 1] + (long long)row0 * H, H, nvalid, tid);
+    rb_copy_out<H>(out, p.dz[l - 1] + (long long)row0 * H, H, nvalid, tid);
     z = out;
     cur = nxt;
   }
@@ -754,14 +777,7 @@ static hipError_t rowband2_launch(const RowbandArgs& p, hipStream_t s) {
       (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  Fn f = fns[p.act == ACT_RELU ? 1 : p.act == ACT_TANH ? 2 : 0];
-  static const int abl = rb_env("NNMPI_RB2_ABL", 0);   // TEMPORARY ablation (measurement only)
-  if (abl > 0 && H == 512 && p.act == ACT_RELU) {
-    static const Fn ab[4] = {nullptr, rowband2_kernel<512, ACT_RELU, 4, 1>, rowband2_kernel<512, ACT_RELU, 4, 2>,
-                             rowband2_kernel<512, ACT_RELU, 4, 3>};
-    f = ab[abl & 3];
-    (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
-  }
+  const Fn f = fns[p.act == ACT_RELU ? 1 : p.act == ACT_TANH ? 2 : 0];
   hipLaunchKernelGGL(f, dim3(rowband_blocks(p.rows)), dim3(RB_THREADS), rb2_smem(H, p.in, p.nh), s, p);
   return hipGetLastError();
 }

@@ -942,11 +942,11 @@ class MLPEngine:
             g.cancel()    # leave the stream out of capture mode, drop the partial graph
             self._rb_fresh, self._rb_ver = rb_pre
             raise
+        # (record(False) rolls the sequence number and the signature back: the capture issued
+        # these collectives once, but every launch runs them, and the launch adds them to the
+        # collective signature -- utils/seqcheck.py)
         notes = self.sync.record(False)
         g.end()
-        # the capture issued these collectives once, but every launch runs them: the launch
-        # adds them to the collective signature (utils/seqcheck.py), the capture does not
-        self.sync.seq -= len(notes)
         rb_post = self._rb_fresh
         self._rb_fresh, self._rb_ver = rb_pre     # nothing ran yet
         return _Graph(g, self.sync, notes, self,

@@ -30,7 +30,7 @@ from ..data.dataset import RegressionDataset, scale_features
 from ..data.partition import partition_rows
 from ..models.mlp import MLP, MLPSpec, reference_init
 from ..parallel import dist as pdist
-from ..parallel.sync import (NativeRcclSync, NoSync, ShardedSync, ShmSync, TorchDistSync,
+from ..parallel.sync import (NativeRcclSync, NoSync, ShardedSync, TorchDistSync, make_shm_sync,
                              shm_sync_ok)
 from ..utils import checkpoint as ckpt
 from ..utils.config import TrainConfig, config_from_args, resolve_device
@@ -257,7 +257,9 @@ def make_sync(j: Job, arena: Arena):
         return ShardedSync(arena, j.world, j.rank, group=group)
     if (j.comm_kind in ("torch", "gloo") and
             shm_sync_ok(j.device.type, j.world, j.job.local_world, grad_dtype, cfg.sync)):
-        return ShmSync(arena, j.pg.gloo, j.world, j.rank, timeout_s=cfg.timeout_s)
+        shm = make_shm_sync(arena, j.pg.gloo, j.world, j.rank, timeout_s=cfg.timeout_s)
+        if shm is not None:
+            return shm
     if j.comm_kind == "native":
         inline = (cfg.comm_mode == "inline" or
                   (cfg.comm_mode == "auto" and arena.numel * 4 <= INLINE_MAX_GRAD_BYTES))

@@ -48,9 +48,12 @@ def _load():
 
 
 def lib():
-    """The loaded extension module (raises if it cannot be built/loaded)."""
+    """The loaded extension module (raises if it cannot be built/loaded).  NNMPI_NATIVE=0
+    refuses to load it (a host without the library: the CPU paths fall back to PyTorch)."""
     global _lib
     if _lib is None:
+        if os.environ.get("NNMPI_NATIVE", "1") == "0":
+            raise RuntimeError("native library disabled (NNMPI_NATIVE=0)")
         _lib = _load()
     return _lib
 

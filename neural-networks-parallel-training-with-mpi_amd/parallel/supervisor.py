@@ -80,6 +80,32 @@ def _describe(rc: int) -> str:
     return f"exit code {rc}"
 
 
+def rendezvous_shared(world: int, local_world: int) -> bool:
+    """The supervisors of every rank can meet: a TCP store (MASTER_ADDR / MASTER_PORT), or all
+    ranks on this node (the FileStore of their common launcher)."""
+    env = os.environ
+    return ("MASTER_ADDR" in env and "MASTER_PORT" in env) or local_world == world
+
+
+def _launcher_key() -> str:
+    """A per-job key for the FileStore path when there is no MASTER_*: the launcher's pid plus its
+    start time (a pid reused by a later launcher gets a different key, so a file left behind by
+    a crashed job is never picked up), or the launcher's job id when it exports one."""
+    env = os.environ
+    for k in ("NNMPI_RDZV_KEY", "PMIX_NAMESPACE", "OMPI_MCA_ess_base_jobid", "PMI_KVSNAME",
+              "SLURM_JOB_ID"):
+        if env.get(k):
+            return "".join(c if c.isalnum() else "_" for c in f"{k}_{env[k]}")[:96]
+    ppid = os.getppid()
+    start = "0"
+    try:
+        with open(f"/proc/{ppid}/stat") as f:
+            start = f.read().rsplit(")", 1)[1].split()[19]   # field 22: starttime
+    except (OSError, IndexError):
+        pass
+    return f"{ppid}_{start}"
+
+
 def _make_store(rank: int, world: int, timeout_s: float):
     import torch.distributed as dist
     env = os.environ
@@ -91,9 +117,9 @@ def _make_store(rank: int, world: int, timeout_s: float):
         st = dist.TCPStore(env["MASTER_ADDR"], int(env["MASTER_PORT"]), world,
                            is_master=(rank == 0 and not agent), timeout=timeout,
                            wait_for_workers=False)
-    else:   # plain mpiexec on one node: the ranks share their launcher's pid
-        key = env.get("NNMPI_RDZV_KEY", str(os.getppid()))
-        st = dist.FileStore(os.path.join(tempfile.gettempdir(), f"nnmpi_sup_{key}"), world)
+    else:   # plain mpiexec on one node: the ranks share their launcher (rendezvous_shared)
+        st = dist.FileStore(os.path.join(tempfile.gettempdir(), f"nnmpi_sup_{_launcher_key()}"),
+                            world)
         st.set_timeout(timeout)
     restart = env.get("TORCHELASTIC_RESTART_COUNT", "0")
     return dist.PrefixStore(f"nnmpi_supervisor/{restart}", st)
@@ -201,8 +227,10 @@ class Supervisor:
                 pass
             st.set(f"a{k}/result", state)
         self._count(f"a{k}/ended", 1)
-        # every peer either finishes or is killed within stall_s + the kill grace
-        self._wait_count(f"a{k}/ended", self.world, self.stall_s + 4 * self.kill_grace_s + 60)
+        # every peer either finishes or is killed within stall_s + the kill grace; a peer that
+        # never reports fails the attempt (its result key may never be written)
+        if not self._wait_count(f"a{k}/ended", self.world, self.stall_s + 4 * self.kill_grace_s + 60):
+            return "none", own, [f"rank {r}: peers did not end attempt {k} in time"], res
         state = st.get(f"a{k}/result").decode()
         fails = []
         if self._count(f"a{k}/nfail") > 0:

@@ -73,11 +73,18 @@ class GradSync:
     def record(self, on: bool):
         """Start (on) / stop (returns the notes) recording the collectives issued meanwhile: the
         engine records a graph capture's collectives and replays them into the signature at
-        every launch of that graph."""
+        every launch of that graph.  A capture issues nothing: stopping restores the sequence
+        number AND the signature to their values at the start (also when the capture failed),
+        so only the launches count -- a rank that captures an extra graph (e.g. a partial last
+        mini-batch of its own) keeps the same signature as its peers."""
         if on:
             self._recording = []
+            self._rec_saved = (self.seq, self.sig)
             return None
         out, self._recording = self._recording or [], None
+        saved, self._rec_saved = getattr(self, "_rec_saved", None), None
+        if saved is not None:
+            self.seq, self.sig = saved
         return out
 
     def replay(self, notes):
@@ -450,6 +457,35 @@ def shm_sync_ok(device_type: str, world: int, local_world: int, grad_dtype: str 
             and mode == "allreduce" and os.environ.get("NNMPI_SHM", "1") != "0")
 
 
+def make_shm_sync(arena, group, world: int, rank: int, timeout_s: float = 120.0):
+    """A :class:`ShmSync` when EVERY rank can use it, else None (the caller keeps gloo).  Each
+    rank first tries to load the native library and the ranks agree on the outcome (a MIN
+    all-reduce of an ok flag over ``group``), so a rank that cannot load it never leaves the
+    others waiting in the segment setup's barriers; the segment setup agrees the same way."""
+    try:
+        from .. import native
+        native.lib()
+        ok = 1
+    except Exception:
+        ok = 0
+    if not _agree(ok, group):
+        return None
+    try:
+        return ShmSync(arena, group, world, rank, timeout_s=timeout_s)
+    except _ShmSetupFailed:
+        return None
+
+
+def _agree(ok: int, group) -> bool:
+    t = torch.tensor([int(ok)], dtype=torch.int32)
+    dist.all_reduce(t, op=dist.ReduceOp.MIN, group=group)
+    return bool(int(t.item()))
+
+
+class _ShmSetupFailed(RuntimeError):
+    pass
+
+
 class ShmSync(GradSync):
     """Gradient all-reduce of CPU ranks on one machine through shared memory.
 
@@ -475,12 +511,20 @@ class ShmSync(GradSync):
         self.name = obj[0]
         cap = max(b.numel for b in arena.buckets)
         lib = native.lib()
-        if rank == 0:
-            self.comm = lib.ShmComm(self.name, rank, world, cap, True)
-        dist.barrier(group=group)
-        if rank != 0:
-            self.comm = lib.ShmComm(self.name, rank, world, cap, False)
-        dist.barrier(group=group)
+        # create on rank 0, then attach on the others; every step agreed over gloo, so a failure
+        # on any rank fails the setup on all of them (make_shm_sync falls back to gloo)
+        self.comm = None
+        for creator in (True, False):
+            ok = 1
+            if (rank == 0) == creator:
+                try:
+                    self.comm = lib.ShmComm(self.name, rank, world, cap, creator)
+                except Exception:
+                    ok = 0
+            if not _agree(ok, group):
+                if rank == 0 and self.comm is not None:
+                    self.comm.unlink()
+                raise _ShmSetupFailed("shared-memory all-reduce setup failed on some rank")
         if rank == 0:
             self.comm.unlink()
 

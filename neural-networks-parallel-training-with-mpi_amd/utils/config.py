@@ -75,8 +75,9 @@ class TrainConfig:
     overlap: bool = True
     graph: bool = True                # capture the steady-state step in a HIP graph
     fast_epochs: bool = True          # full-batch GPU epochs replayed 64 per graph (same output)
-    grad_dtype: str = "auto"          # auto | fp32 | bf16 (all-reduce payload dtype; auto: bf16
-                                      # above 64 MB of fp32 gradient on the GPU, as bench.py)
+    grad_dtype: str = "fp32"          # fp32 | bf16 | auto (all-reduce payload dtype; fp32 as the
+                                      # reference averages fp32 gradients, ref.py:185-208; auto:
+                                      # bf16 above 64 MB of fp32 gradient on the GPU, as bench.py)
     shard_optimizer: bool = False     # ZeRO-1: reduce-scatter grads, SGD on own 1/P, all-gather
     deterministic: bool = True
     # --- IO / observability ---
@@ -162,9 +163,10 @@ def build_parser() -> argparse.ArgumentParser:
     p.add_argument("--no_fast_epochs", dest="fast_epochs", action="store_false",
                    help="one graph replay + loss readback per epoch (default: 64 epochs per "
                         "replay, losses recorded on the device; identical output)")
-    p.add_argument("--grad_dtype", choices=["auto", "fp32", "bf16"], default="auto",
-                   help="all-reduce payload: auto = bf16 above 64 MB of fp32 gradient on the GPU "
-                        "(one-rounding reduction, see parallel/sync.py), fp32 otherwise")
+    p.add_argument("--grad_dtype", choices=["auto", "fp32", "bf16"], default="fp32",
+                   help="all-reduce payload (default fp32, the reference's gradients); auto = "
+                        "bf16 above 64 MB of fp32 gradient on the GPU (one-rounding reduction, "
+                        "see parallel/sync.py) -- the bench's choice")
     p.add_argument("--shard_optimizer", "--zero1", dest="shard_optimizer", action="store_true",
                    help="sharded optimizer state (ZeRO-1): reduce-scatter gradients, SGD on this "
                         "rank's 1/P of the parameters, all-gather the updated parameters")

@@ -701,12 +701,15 @@ def test_minibatch_epoch_graph_same_as_per_step(comm):
 
 
 def test_compat_cli_wide_preset_takes_the_bench_schedule():
-    """``--preset wide8192 --comm native`` through the compat trainer picks what bench.py picks:
-    the bf16 payload (auto: > 64 MB of fp32 gradient) and the overlapped chunk buckets whose
-    updates ride in the next weight-gradient epilogue (deferred updates)."""
+    """``--preset wide8192 --comm native --grad_dtype auto`` through the compat trainer picks what
+    bench.py picks: the bf16 payload (auto: > 64 MB of fp32 gradient) and the overlapped chunk
+    buckets whose updates ride in the next weight-gradient epilogue (deferred updates).  Without
+    ``--grad_dtype`` the CLI keeps the reference's fp32 gradients."""
     from nnmpi_amd.utils.config import build_parser, config_from_args
+    assert config_from_args(build_parser().parse_args(["--preset", "wide8192"])).grad_dtype == "fp32"
     cfg = config_from_args(build_parser().parse_args(
-        ["--preset", "wide8192", "--comm", "native", "--nepochs", "2", "--print_rank", "none",
+        ["--preset", "wide8192", "--comm", "native", "--grad_dtype", "auto", "--nepochs", "2",
+         "--print_rank", "none",
          "--data_gen", "device", "--data_dist", "local", "--scaling", "none", "--lr", "1e-5"]))
     res = trainer.run_worker(cfg)
     sch = res.schedule

@@ -32,6 +32,12 @@ GOLDEN_PARAMS = {
     8: [0.017505, 0.369685, -0.637966, -0.498654, -0.295752, 0.192411, -0.023648, 0.582469,
         -0.039345, 0.129082, -0.344731, -0.159964, -0.616460],
 }
+# P = 12 (uneven: ranks 0-3 get 2 rows, ranks 4-11 one) runs in the reference only by accident
+# (its int8 counts broadcast as MPI.INT happen to carry whole ints at P % 4 == 0);
+# captured for ranks 0 and 11 with the final parameters
+GOLDEN_P12 = {0: [3440.1406, 3442.9797, 3448.4126], 11: [13.9438, 14.1968, 14.6891]}
+GOLDEN_P12_PARAMS = [-0.001211, 0.384259, -0.598219, -0.522632, -0.277418, 0.183917, -0.009074,
+                     0.587691, -0.057679, 0.164367, -0.307603, -0.113446, -0.661263]
 INIT = [-0.00529, 0.37932, -0.58198, -0.52039, -0.27235, 0.18962, -0.01401, 0.56066, -0.06275,
         0.15277, -0.17448, -0.11349, -0.55157]
 
@@ -59,4 +65,17 @@ def test_golden_multirank(world):
     for r in range(world):
         assert torch.allclose(out[r]["final"], torch.tensor(GOLDEN_PARAMS[world]), atol=5e-6), r
         # replicas stay bitwise identical
+        assert torch.equal(out[r]["final"], out[0]["final"])
+
+
+def test_golden_p12_uneven_scatterv():
+    """The reference's only uneven split that runs (P = 12, 16 rows: Bcast(counts) + Scatterv,
+    ref.py:110-143): rank 0 and rank 11 losses and the final parameters of SURVEY.md §4.2, every
+    replica bitwise equal.  12 spawned CPU ranks over gloo / the shared-memory all-reduce."""
+    out = run_ranks(TrainConfig(device="cpu", print_rank="none"), 12)
+    assert [o["rows"] for o in out] == [2] * 4 + [1] * 8
+    for r, want in GOLDEN_P12.items():
+        assert out[r]["losses"] == pytest.approx(want, rel=1e-5), r
+    for r in range(12):
+        assert torch.allclose(out[r]["final"], torch.tensor(GOLDEN_P12_PARAMS), atol=5e-6), r
         assert torch.equal(out[r]["final"], out[0]["final"])

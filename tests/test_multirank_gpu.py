@@ -17,7 +17,7 @@ import pytest
 import torch
 
 from _mp import run_ranks_proc
-from test_golden import GOLDEN_LOSSES, GOLDEN_PARAMS
+from test_golden import GOLDEN_LOSSES, GOLDEN_P12, GOLDEN_P12_PARAMS, GOLDEN_PARAMS
 
 pytestmark = pytest.mark.gpu
 
@@ -155,6 +155,30 @@ def test_rccl_reference_golden_p2_scatterv():
         assert out[r]["losses"] == pytest.approx(GOLDEN_LOSSES[2][r], rel=1e-5), r
         assert torch.allclose(out[r]["final"], torch.tensor(GOLDEN_PARAMS[2]), atol=5e-6)
     _replicas_equal(out)
+
+
+@pytest.mark.parametrize("world", [3, 12])
+def test_rccl_reference_uneven_scatterv_matches_cpu(world):
+    """The reference config with an UNEVEN split over RCCL (BASELINE config 3's "uneven dataset
+    split"): rank 0 generates the 16 rows and scatters them with grouped ncclSend/Recv of
+    per-rank counts (the reference's Bcast(counts) + Scatterv, ref.py:110-143; it crashes at P=3,
+    D2), the model is broadcast, the tiny kernel steps, the gradient is all-reduced.  Every rank
+    matches the CPU (gloo) run of the same job to rtol 1e-5, replicas are bitwise equal, and at
+    P = 12 ranks 0 and 11 match the reference's own output."""
+    cfg = dict(print_rank="none", data_dist="scatter")
+    gpu = run_ranks_proc(dict(cfg, device="cuda", comm="native"), world, env_per_rank=rccl_env,
+                         timeout=420.0)
+    cpu = run_ranks_proc(dict(cfg, device="cpu"), world, timeout=300.0)
+    rows = [o["rows"] for o in gpu]
+    assert sum(rows) == 16 and rows == [o["rows"] for o in cpu] and len(set(rows)) == 2
+    for r in range(world):
+        assert gpu[r]["losses"] == pytest.approx(cpu[r]["losses"], rel=1e-5), r
+        assert torch.allclose(gpu[r]["final"], cpu[r]["final"], rtol=1e-5, atol=1e-6), r
+    _replicas_equal(gpu)
+    if world == 12:
+        for r, want in GOLDEN_P12.items():
+            assert gpu[r]["losses"] == pytest.approx(want, rel=1e-5), r
+        assert torch.allclose(gpu[0]["final"], torch.tensor(GOLDEN_P12_PARAMS), atol=5e-6)
 
 
 def test_rccl_grouped_overlap_two_ranks_bitwise():

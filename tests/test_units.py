@@ -375,3 +375,45 @@ def test_shm_sync_matches_gloo_at_two_ranks():
     assert torch.equal(a[0]["final"], a[1]["final"])
     assert torch.equal(a[0]["final"], b[0]["final"])
     assert a[0]["losses"] == b[0]["losses"]
+
+
+def test_capture_rollback_keeps_the_collective_signature():
+    """A graph capture issues no collective: stopping the recording restores the sequence number
+    AND the running signature, so a rank that captures one more graph than its peers
+    (a partial last mini-batch of its own) still matches them; the failed-capture path too.
+    Only the launches (replay) add the recorded notes."""
+    from nnmpi_amd.parallel.sync import GradSync
+    ar = Arena([(8, 8), (1, 8)], "cpu")
+    a, b = GradSync(ar), GradSync(ar)
+    for s in (a, b):
+        s.note(1, 0, 0, 64, 0)
+    # rank a captures an extra graph that holds two collectives, rank b does not
+    a.record(True)
+    a.note(1, 0, 0, 64, 0)
+    a.note(1, 1, 64, 8, 0)
+    notes = a.record(False)
+    assert len(notes) == 2 and (a.seq, a.sig) == (b.seq, b.sig)
+    # a capture that raised: record(False) from the except branch restores the same way
+    a.record(True)
+    a.note(3, 0, 0, 72, 1)
+    a.record(False)
+    assert (a.seq, a.sig) == (b.seq, b.sig)
+    # one launch of the captured graph on both ranks keeps them equal
+    a.replay(notes)
+    b.note(1, 0, 0, 64, 0)
+    b.note(1, 1, 64, 8, 0)
+    assert (a.seq, a.sig) == (b.seq, b.sig)
+
+
+def test_shm_sync_falls_back_to_gloo_when_one_rank_cannot_load_the_library():
+    """the shared-memory all-reduce needs the native library on EVERY rank.  With it
+    hidden on rank 1 (NNMPI_NATIVE=0) the ranks agree over gloo and both keep the gloo all-reduce
+    (no rank waits in the segment setup); training proceeds and matches the plain-gloo run."""
+    from _mp import run_ranks_proc
+    cfg = dict(device="cpu", print_rank="none", nepochs=4)
+    a = run_ranks_proc(cfg, 2, env_per_rank=lambda r: {"NNMPI_NATIVE": "0"} if r == 1 else {})
+    assert a[0]["schedule"]["sync"] == a[1]["schedule"]["sync"] == "TorchDistSync"
+    b = run_ranks_proc(cfg, 2, env_per_rank=lambda r: {"NNMPI_SHM": "0"})
+    for r in range(2):
+        assert a[r]["losses"] == pytest.approx(b[r]["losses"], rel=1e-5)
+        assert torch.allclose(a[r]["final"], b[r]["final"], rtol=1e-5, atol=1e-6)
