@@ -128,7 +128,7 @@ def parse(argv=None):
     p.add_argument("--fwd_variant", type=int, default=-1, help="forward GEMM variant (experiments)")
     p.add_argument("--gemm_variant", type=int, default=0,
                    help="GEMM main-loop variant of every launch (experiments; 19..24 = deep-ring "
-                        "256x256, needs an NNMPI_EXPERIMENTS=1 build)")
+                        "256x256, needs an NNMPI_BUILD_EXPERIMENTS=1 build)")
     p.add_argument("--pp_order", default="",
                    help="256x256 GEMM kernel for fwd,dgrad,wgrad (0 GM4, 1 row-major, 2 GM4 + one "
                         "DMA half per phase, 3 row-major + one half per phase; experiments)")
@@ -139,6 +139,23 @@ def parse(argv=None):
     p.add_argument("--group_async", type=int, default=-1,
                    help="grouped-backward LDS read mode (experiments)")
     return p.parse_args(argv)
+
+
+EXPERIMENT_FLAGS = {"fwd_variant": -1, "gemm_variant": 0, "pp_order": "", "head_xcd_rows": 0,
+                    "store_policy": 0, "group_async": -1}
+
+
+def knobs_report(a) -> dict:
+    """What could make this run differ from the default configuration: every NNMPI_* variable in
+    the environment and every non-default experiment flag, each with whether it took effect
+    (experiment knobs count only with NNMPI_EXPERIMENTS=1, nnmpi_amd/utils/knobs.py)."""
+    from nnmpi_amd.utils import knobs
+    out = {"experiments": knobs.experiments(), "env": knobs.seen(), "flags": {}}
+    for k, d in EXPERIMENT_FLAGS.items():
+        v = getattr(a, k)
+        if v != d:
+            out["flags"][k] = {"value": v, "honoured": knobs.experiments()}
+    return out
 
 
 def _free_port() -> int:
@@ -290,6 +307,8 @@ def run(a, job):
     gpu = a.device == "cuda"
     if gpu:
         from nnmpi_amd import native
+        # kernel-selection experiment flags: honoured only with NNMPI_EXPERIMENTS=1 (the native
+        # knobs ignore them otherwise); the JSON line reports them either way
         native.lib().set_fwd_variant(a.fwd_variant)
         native.lib().set_gemm_variant(a.gemm_variant)
         for epi, idx in enumerate(a.pp_order.split(",") if a.pp_order else []):
@@ -693,6 +712,7 @@ def run(a, job):
             "extras_error": extras_error,
             "loss_after_warmup": loss0,
             "final_loss": loss,
+            "knobs": knobs_report(a),
         }
 
     if rank == 0 and supervised():

@@ -1,4 +1,5 @@
 #include <cstdlib>
+#include "knobs.h"
 #include "rccl_comm.h"
 #include "kernels/kernels.h"
 
@@ -253,7 +254,7 @@ void GraphRunner::end() {
   // replay -- often inside a timed region -- does not pay for it.  NNMPI_GRAPH_UPLOAD=0 skips
   // it (A/B).
   static const bool upload = [] {
-    const char* v = std::getenv("NNMPI_GRAPH_UPLOAD");
+    const char* v = knob_env("NNMPI_GRAPH_UPLOAD");
     return !(v && v[0] == '0');
   }();
   if (upload) HIP_THROW(hipGraphUpload(exec_, s));

@@ -9,6 +9,7 @@
 //                                     (scripts/stamp_fwd.py).
 // The production file reaches them through the weak references declared in gemm_tiles.h.
 #include "kernels/gemm_tiles.h"
+#include "knobs.h"
 
 namespace nnmpi {
 
@@ -290,7 +291,7 @@ static int g_pair = -1;   // 1 on, 0 off (default; NNMPI_PAIR=1 / set_wide_pair)
 void exp_set_wide_pair(int on) { g_pair = on; }
 static bool pair_enabled() {
   if (g_pair < 0) {
-    const char* e = std::getenv("NNMPI_PAIR");
+    const char* e = knob_env("NNMPI_PAIR");
     g_pair = (e && e[0] == '1') ? 1 : 0;
   }
   return g_pair == 1 && gemm_host::default_path();

@@ -23,6 +23,7 @@
 // gradient (row sums of dZ^T) rides on the same A fragments through one extra MFMA against a
 // ones operand in the n-tile-0 blocks.
 #include "gemm_tiles.h"
+#include "knobs.h"
 
 namespace nnmpi {
 
@@ -30,7 +31,7 @@ static int g_stage_epi = -1;   // NNMPI_STAGE_EPI=1: LDS-staged 256x256 forward 
 void set_stage_epi(int on) { g_stage_epi = on; }   // -1: re-read the environment
 static int stage_epi() {
   if (g_stage_epi < 0) {
-    const char* e = std::getenv("NNMPI_STAGE_EPI");
+    const char* e = knob_env("NNMPI_STAGE_EPI");
     g_stage_epi = (e && e[0] == '1') ? 1 : 0;
   }
   return g_stage_epi;
@@ -39,7 +40,7 @@ static int g_sgd_serial = -1;   // NNMPI_SGD_SERIAL=<form> (experiments)
 void set_sgd_epilogue(int form) { g_sgd_serial = form; }   // -1: re-read the environment
 static int sgd_serial() {
   if (g_sgd_serial < 0) {
-    const char* e = std::getenv("NNMPI_SGD_SERIAL");
+    const char* e = knob_env("NNMPI_SGD_SERIAL");
     g_sgd_serial = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : 0;
   }
   return g_sgd_serial;
@@ -218,7 +219,7 @@ static int g_gemm_impl = -1;
 
 static int gemm_impl() {
   if (g_gemm_impl < 0) {
-    const char* e = getenv("NNMPI_GEMM");
+    const char* e = knob_env("NNMPI_GEMM");
     g_gemm_impl = (e && e[0] == '1') ? 1 : 2;   // 2 = LDS-DMA ring (default), 1 = register-staged
   }
   return g_gemm_impl;
@@ -273,7 +274,7 @@ static int g_slab_store_pol = -2;
 void set_slab_store_policy(int p) { g_slab_store_pol = p; }
 static int slab_store_pol() {
   if (g_slab_store_pol == -2) {
-    const char* e = std::getenv("NNMPI_SLAB_STORE");
+    const char* e = knob_env("NNMPI_SLAB_STORE");
     g_slab_store_pol = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : -1;
   }
   return g_slab_store_pol >= 0 ? g_slab_store_pol : g_store_pol;
@@ -304,7 +305,7 @@ static hipError_t launch_t(GemmParams p, int splits, hipStream_t s, int variant 
       attr = true;
     }
     if (variant >= 19 && variant <= 24) {
-      // the deep-ring twin lives in csrc/experiments (NNMPI_EXPERIMENTS=1 builds)
+      // the deep-ring twin lives in csrc/experiments (NNMPI_BUILD_EXPERIMENTS=1 builds)
       if (!exp_pp256_ring) return hipErrorNotSupported;
       return exp_pp256_ring(variant, LA, LB, EPI, ACT, BG, p, grid, s);
     }
@@ -605,7 +606,7 @@ static int g_group = -1;   // grouped backward launch: 1 on (default), 0 off (NN
 void set_bwd_group(int on) { g_group = on; }
 static bool group_enabled() {
   if (g_group < 0) {
-    const char* e = getenv("NNMPI_GROUP");
+    const char* e = knob_env("NNMPI_GROUP");
     g_group = (e && e[0] == '0') ? 0 : 1;
   }
   return g_group == 1;

@@ -1,7 +1,7 @@
 // Device-side building blocks of the bf16 MFMA GEMMs (gemm_bf16.hip): operand layouts, LDS
 // images, the LDS-DMA plan, the 128x128 DMA main loop and the 256x256 ping-pong tile with their
 // fused epilogues.  Shared by the production launchers (gemm_bf16.hip) and the experiment
-// kernels (csrc/experiments/, built only with NNMPI_EXPERIMENTS=1).  See gemm_bf16.hip for the
+// kernels (csrc/experiments/, built only with NNMPI_BUILD_EXPERIMENTS=1).  See gemm_bf16.hip for the
 // design notes.
 #pragma once
 #include "common.h"

@@ -25,6 +25,7 @@
 // fragment reads of the current k-step are not using.  After each pass the image is copied out
 // row-contiguously (activations and dZ are needed by the weight gradients).
 #include "gemm_tiles.h"
+#include "knobs.h"
 
 namespace nnmpi {
 
@@ -761,7 +762,7 @@ static bool rowband2_shape_ok(int H, int in, int nh) {
 }
 
 static int rb_env(const char* name, int dflt) {
-  const char* e = std::getenv(name);
+  const char* e = knob_env(name);
   return (e && e[0] >= '0' && e[0] <= '9') ? std::atoi(e) : dflt;
 }
 

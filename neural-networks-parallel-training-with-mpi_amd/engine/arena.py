@@ -18,6 +18,7 @@ from dataclasses import dataclass
 from typing import Dict, List, Optional, Tuple
 
 import torch
+from ..utils.knobs import knob
 
 ALIGN = 64  # elements
 
@@ -67,7 +68,7 @@ def row_chunks(out_f: int, in_f: int, grad_bytes: int, bucket_bytes: float,
     # min_tiles: tiles per chunk at least (0: NNMPI_CHUNK_MIN_TILES, else CHUNK_MIN_TILES; tests
     # exercise the chunked schedule on small layers, bench.py tunes 2 vs 4 chunks per layer)
     if min_tiles <= 0:
-        min_tiles = int(os.environ.get("NNMPI_CHUNK_MIN_TILES", CHUNK_MIN_TILES))
+        min_tiles = int(knob("NNMPI_CHUNK_MIN_TILES", CHUNK_MIN_TILES))
     c = 1
     while (out_f % (2 * c * CHUNK_TILE) == 0 and
            (out_f // (2 * c * CHUNK_TILE)) * (in_f // CHUNK_TILE) >= min_tiles):

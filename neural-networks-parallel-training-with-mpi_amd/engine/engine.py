@@ -26,6 +26,7 @@ import os
 from typing import Dict, List, Optional, Tuple
 
 import torch
+from ..utils.knobs import knob
 
 from ..models.mlp import MLPSpec
 from .arena import Arena
@@ -121,7 +122,7 @@ class MLPEngine:
         # per-bucket overlapped schedule to hide.  NNMPI_ROWBAND=0 keeps the grouped schedule
         # (proxy step 0.082 vs 0.094 ms, profiles/r3s2_rowband_*).
         self.rowband = (self.overlap and dtype == torch.bfloat16 and inline_sync and
-                        hasattr(ops, "rowband_ok") and os.environ.get("NNMPI_ROWBAND", "1") != "0"
+                        hasattr(ops, "rowband_ok") and knob("NNMPI_ROWBAND", "1") != "0"
                         and ops.rowband_ok(self.R, w, self.act, spec.loss))
         self.ws_rb = (torch.zeros(ops.rowband_workspace_bytes(self.R, w[1], L - 1, in_=w[0]) // 4 + 64,
                                   dtype=torch.float32, device=dev) if self.rowband else None)
@@ -140,7 +141,7 @@ class MLPEngine:
         # A band's passes cost the same whatever the number of bands (per-CU bound: 47 us at
         # 1,024 rows as at 8,192, profiles/r3s2_rowband_pmc.txt), so small batches (strong-scaling
         # shards, mini-batches) keep the grouped schedule: 0.053 vs ~0.064 ms at 1,024 rows.
-        self.rowband_min_rows = int(os.environ.get("NNMPI_ROWBAND_MIN_ROWS", "6144"))
+        self.rowband_min_rows = int(knob("NNMPI_ROWBAND_MIN_ROWS", "6144"))
         if self.is_cuda:
             self.ev_wfree = [torch.cuda.Event(enable_timing=False) for _ in range(L)]
         # bf16-payload overlapped schedule: per-bucket updates read the bf16 payload
@@ -158,7 +159,7 @@ class MLPEngine:
         # index -> the partner bucket it updates.
         self._defer_plan: Dict[int, object] = {}
         if (self._w16 and hasattr(ops, "linear_wgrad_defer") and not self.sharded
-                and os.environ.get("NNMPI_DEFER", "1") != "0"):
+                and knob("NNMPI_DEFER", "1") != "0"):
             for i in range(L - 2):
                 if spec.layer_shape(i) != spec.layer_shape(i + 1):
                     continue
@@ -169,7 +170,7 @@ class MLPEngine:
         self._defer_targets = {b.index for b in self._defer_plan.values()}
         # NNMPI_DEFER_WAIT=chunk: every deferred update waits on its own partner's collective
         # (default: one wait per partner layer, see _defer_update)
-        self._defer_wait_layer = os.environ.get("NNMPI_DEFER_WAIT", "layer") != "chunk"
+        self._defer_wait_layer = knob("NNMPI_DEFER_WAIT", "layer") != "chunk"
         self._waited = set()
         self.ev_ar = ({b.index: torch.cuda.Event(enable_timing=False)
                        for b in self._defer_plan.values()} if self._defer_plan else {})
@@ -1073,11 +1074,16 @@ class _Graph:
 
     def __init__(self, runner, sync, notes, engine=None, rb_pre: bool = False,
                  rb_post: bool = False):
+        import weakref
         self.runner, self.sync, self.notes = runner, sync, notes
-        self.engine, self.rb_pre, self.rb_post = engine, rb_pre, rb_post
+        # (a weak reference: engine -> _graphs -> graph -> engine would be a cycle, freed by the
+        # garbage collector in arbitrary order at teardown -- a graph holding RCCL kernels then
+        # outlives its communicator, and the teardown of the two hung a 2-rank RCCL job)
+        self._eng = weakref.ref(engine) if engine is not None else (lambda: None)
+        self.rb_pre, self.rb_post = rb_pre, rb_post
 
     def launch(self, stream_handle: int):
-        eng = self.engine
+        eng = self._eng()
         if eng is not None and eng.rb_packed is not None and self.rb_pre and not eng._rb_current():
             with torch.cuda.stream(eng.stream):
                 eng._rb_pack()

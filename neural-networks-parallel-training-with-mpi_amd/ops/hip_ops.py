@@ -10,6 +10,7 @@ import os
 from typing import Optional, Tuple
 
 import torch
+from ..utils.knobs import knob
 
 from .. import native
 from .torch_ops import ACT_CODES
@@ -303,7 +304,7 @@ class HipOps:
             return 0
         H, in_, nh, out = widths[1], widths[0], len(widths) - 2, widths[-1]
         lc, ac = LOSS_CODES.get(loss, -1), ACT_CODES[act]
-        if os.environ.get("NNMPI_RB_V2", "1") != "0" and \
+        if knob("NNMPI_RB_V2", "1") != "0" and \
                 self.lib.rowband2_ok(int(rows), H, in_, nh, out, lc, ac):
             return 2
         if in_ == H and self.lib.rowband_ok(int(rows), H, in_, nh, out, lc, ac):

@@ -11,6 +11,7 @@ numerics oracle (``NNMPI_CPU_NATIVE=0`` selects it for tiny models too).
 """
 from __future__ import annotations
 
+from ..utils.knobs import knob
 import os
 
 from .. import native
@@ -23,7 +24,7 @@ def _p(t):
 
 
 def host_ops_enabled() -> bool:
-    return os.environ.get("NNMPI_CPU_NATIVE", "1") != "0"
+    return knob("NNMPI_CPU_NATIVE", "1") != "0"
 
 
 class HostOps(TorchOps):

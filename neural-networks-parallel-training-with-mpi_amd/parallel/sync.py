@@ -29,6 +29,7 @@ from __future__ import annotations
 from typing import List, Optional
 
 import torch
+from ..utils.knobs import knob
 import torch.distributed as dist
 
 
@@ -230,7 +231,7 @@ class NativeRcclSync(GradSync):
                      if self.bf16 else None)
         self._comm_stream = torch.cuda.ExternalStream(self.gs.comm_stream)
         import os
-        self.bf16_reduce = bf16_reduce or os.environ.get("NNMPI_BF16_REDUCE", "acc32")
+        self.bf16_reduce = bf16_reduce or knob("NNMPI_BF16_REDUCE", "acc32")
         if self.bf16_reduce not in ("acc32", "rccl"):
             raise ValueError(f"bf16_reduce must be acc32 or rccl, not {self.bf16_reduce!r}")
         self.scratch = None
@@ -454,7 +455,7 @@ def shm_sync_ok(device_type: str, world: int, local_world: int, grad_dtype: str 
     applies (NNMPI_SHM=0 keeps gloo)."""
     import os
     return (device_type == "cpu" and world > 1 and local_world == world and grad_dtype == "fp32"
-            and mode == "allreduce" and os.environ.get("NNMPI_SHM", "1") != "0")
+            and mode == "allreduce" and knob("NNMPI_SHM", "1") != "0")
 
 
 def make_shm_sync(arena, group, world: int, rank: int, timeout_s: float = 120.0):

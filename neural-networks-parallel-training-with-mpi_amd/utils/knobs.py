@@ -1,0 +1,66 @@
+"""Experiment knobs: one switch decides whether they count.
+
+Every ``NNMPI_*`` environment variable that changes WHAT runs -- a kernel variant, a schedule, a
+transport, a split count -- is an experiment knob: honoured only when ``NNMPI_EXPERIMENTS=1``
+(the native library checks the same switch, ``csrc/knobs.h``).  Without it a stray variable on
+a benchmark box cannot silently change what is timed; ``bench.py`` reports every ``NNMPI_*``
+variable it sees (and whether it was honoured) in its JSON line.
+
+Operational variables (launcher plumbing, the supervisor's files, the native-library switch,
+test fault injection) are not knobs: they do not select a code path of the training step.
+"""
+from __future__ import annotations
+
+import os
+from typing import Dict, Optional
+
+EXPERIMENTS = "NNMPI_EXPERIMENTS"
+
+# variables that select code paths of the step (Python side and csrc/knobs.h)
+KNOBS = {
+    "NNMPI_ROWBAND": "row-band step schedule (0 off)",
+    "NNMPI_ROWBAND_MIN_ROWS": "smallest batch that takes the row-band step",
+    "NNMPI_RB_V2": "row-band v2 kernel with fragment-major weight images (0: v1)",
+    "NNMPI_RB_SPLITS": "row-band weight-gradient split-K slabs",
+    "NNMPI_DEFER": "deferred bucket updates in weight-gradient epilogues (0 off)",
+    "NNMPI_DEFER_WAIT": "deferred update waits per chunk / per layer",
+    "NNMPI_CHUNK_MIN_TILES": "tiles per output-row chunk bucket",
+    "NNMPI_BF16_REDUCE": "bf16 all-reduce algorithm (acc32 | rccl)",
+    "NNMPI_SHM": "shared-memory all-reduce of CPU ranks (0: gloo)",
+    "NNMPI_CPU_NATIVE": "native host step of tiny CPU models (0: PyTorch)",
+    "NNMPI_STAGE_EPI": "LDS-staged 256x256 forward epilogue",
+    "NNMPI_SGD_SERIAL": "SGD epilogue form",
+    "NNMPI_GEMM": "GEMM main loop (1 register-staged, 2 LDS-DMA)",
+    "NNMPI_SLAB_STORE": "split-K slab store policy",
+    "NNMPI_GROUP": "grouped backward launch (0 off)",
+    "NNMPI_GRAPH_UPLOAD": "hipGraphUpload after instantiation (0 off)",
+    "NNMPI_PAIR": "wide backward pair launches (experiments build)",
+}
+
+# plumbing, not knobs (never reported)
+INTERNAL = {"NNMPI_SUPERVISED", "NNMPI_ATTEMPT", "NNMPI_PROGRESS_FILE", "NNMPI_RESULT_FILE",
+            "NNMPI_LAUNCHER", "NNMPI_RDZV_KEY"}
+
+
+def experiments() -> bool:
+    return os.environ.get(EXPERIMENTS) == "1"
+
+
+def knob(name: str, default: Optional[str] = None) -> Optional[str]:
+    """The value of experiment knob ``name`` -- its default unless NNMPI_EXPERIMENTS=1."""
+    assert name in KNOBS, name
+    if not experiments():
+        return default
+    return os.environ.get(name, default)
+
+
+def seen() -> Dict[str, dict]:
+    """Every NNMPI_* variable in the environment (plumbing excluded): value and whether it took
+    effect (knobs only with NNMPI_EXPERIMENTS=1; operational variables always)."""
+    on = experiments()
+    out = {}
+    for k, v in sorted(os.environ.items()):
+        if not k.startswith("NNMPI_") or k in INTERNAL:
+            continue
+        out[k] = {"value": v, "honoured": (on if k in KNOBS else True)}
+    return out

@@ -72,6 +72,15 @@ def run_ranks_proc(cfg: dict, world: int, env_per_rank=None, timeout: float = 15
             if failed is None and any(p.returncode != 0 for p in procs):
                 failed = f"rank exit codes {[p.returncode for p in procs]}"
         finally:
+            live = [p for p in procs if p.poll() is None]
+            if live and failed:
+                import signal
+                for p in live:          # stack dump (faulthandler, _rank_entry.py), then kill
+                    try:
+                        p.send_signal(signal.SIGUSR1)
+                    except OSError:
+                        pass
+                time.sleep(3)
             for p in procs:
                 if p.poll() is None:
                     p.kill()
@@ -80,7 +89,10 @@ def run_ranks_proc(cfg: dict, world: int, env_per_rank=None, timeout: float = 15
             out = []
             for r, log in enumerate(logs):
                 log.seek(0)
-                out.append(f"--- rank {r} ---\n" + log.read()[-3000:])
+                txt = log.read()
+                # (RCCL's warning lines crowd out the stack dump: keep the Python frames)
+                txt = "\n".join(l for l in txt.splitlines() if "NCCL WARN" not in l and l.strip())
+                out.append(f"--- rank {r} ---\n" + txt[-6000:])
             raise AssertionError(failed + "\n" + "\n".join(out))
         for log in logs:
             log.close()

@@ -7,6 +7,13 @@ import sys
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
+import faulthandler  # noqa: E402
+import signal  # noqa: E402
+
+# _mp.run_ranks_proc sends SIGUSR1 to a rank that hangs past its time limit before killing it:
+# every thread's Python stack lands in the rank's log
+faulthandler.register(signal.SIGUSR1, all_threads=True)
+
 import torch  # noqa: E402
 
 torch.set_num_threads(1)

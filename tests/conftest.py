@@ -7,6 +7,10 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 if ROOT not in sys.path:
     sys.path.insert(0, ROOT)
 
+# The tests pin schedules and kernel variants through the experiment knobs (utils/knobs.py),
+# which only count with this switch (production runs -- smoke(), bench.py -- leave it unset)
+os.environ["NNMPI_EXPERIMENTS"] = "1"
+
 
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (gfx950) GPU")

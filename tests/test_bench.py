@@ -150,6 +150,21 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
 
 @pytest.mark.gpu
 @pytest.mark.rowband
+def test_bench_three_rank_rowband_uneven_rehearsal():
+    """The bench's N > 1 shape at P = 3: 8192 * 3 - 1 rows split unevenly (8192, 8192, 8191), the
+    row-band step (v2 images rebuilt after every multi-rank update) with the inline RCCL
+    all-reduce, 3 RCCL ranks sharing the GPU: replicas bitwise equal."""
+    r = _run(["--gpus", "3", "--shared_gpu_rehearsal", "--steps", "6", "--warmup", "2",
+              "--comm_mode", "inline", "--no_extras"], timeout=300)
+    d = _line(r)
+    assert d["n_gpus"] == 3 and d["rccl_ranks"] == 3
+    assert d["config"]["schedule"] == "rowband" and d["config"]["uneven_split"] is True
+    assert d["config"]["global_batch"] == 8192 * 3 - 1
+    assert d["replicas_bitwise_equal"] is True and d["final_loss"] == d["final_loss"]
+
+
+@pytest.mark.gpu
+@pytest.mark.rowband
 def test_bench_driver_torchrun_form_on_one_gpu():
     """The driver's exact N-GPU launch (torch.distributed.run ... bench.py --gpus N) with the GPU
     ranks sharing the one device: per-rank supervisors under torchrun's agent store, RCCL ranks,
@@ -205,3 +220,41 @@ def test_bench_under_torchrun_sigsegv_falls_back():
     d = _line(_torchrun(["--steps", "6", "--warmup", "2"], n=3,
                         env={"NNMPI_BENCH_CRASH": "2:0:warm-up"}))
     assert "rank 2 killed by SIGSEGV" == d["fallback"] and d["n_gpus"] == 3
+
+
+def test_bench_reports_and_ignores_a_stray_knob():
+    """An experiment knob in the environment of a production run (no NNMPI_EXPERIMENTS=1) does
+    not change what is timed -- the native library and the engine ignore it -- and the JSON line
+    records it as not honoured; with NNMPI_EXPERIMENTS=1 it is recorded as honoured."""
+    env = dict(os.environ, NNMPI_RB_SPLITS="7", NNMPI_ROWBAND="0")
+    env.pop("NNMPI_EXPERIMENTS", None)
+    r = subprocess.run([sys.executable, BENCH, "--device", "cpu", "--config", "ref", "--steps", "2",
+                        "--warmup", "1", "--no_extras"], capture_output=True, text=True,
+                       timeout=300, env=env)
+    d = _line(r)
+    k = d["knobs"]
+    assert k["experiments"] is False
+    assert k["env"]["NNMPI_RB_SPLITS"] == {"value": "7", "honoured": False}
+    assert k["env"]["NNMPI_ROWBAND"]["honoured"] is False
+    env["NNMPI_EXPERIMENTS"] = "1"
+    r = subprocess.run([sys.executable, BENCH, "--device", "cpu", "--config", "ref", "--steps", "2",
+                        "--warmup", "1", "--no_extras"], capture_output=True, text=True,
+                       timeout=300, env=env)
+    k = _line(r)["knobs"]
+    assert k["experiments"] is True and k["env"]["NNMPI_RB_SPLITS"]["honoured"] is True
+
+
+def test_native_set_knobs_need_the_experiments_switch():
+    """The bindings' set_* kernel-selection knobs are ignored (return False) unless
+    NNMPI_EXPERIMENTS=1 (csrc/knobs.h)."""
+    code = ("from nnmpi_amd import native; l = native.lib(); "
+            "print(l.experiments_on(), l.set_gemm_tile(64), l.set_pp256_order(0, 1))")
+    env = dict(os.environ)
+    env.pop("NNMPI_EXPERIMENTS", None)
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                         env=env, cwd=os.path.dirname(BENCH)).stdout.split()
+    assert out == ["False", "False", "False"]
+    env["NNMPI_EXPERIMENTS"] = "1"
+    out = subprocess.run([sys.executable, "-c", code], capture_output=True, text=True, timeout=120,
+                         env=env, cwd=os.path.dirname(BENCH)).stdout.split()
+    assert out == ["True", "True", "True"]

@@ -437,7 +437,7 @@ def test_wide_pair_launches_bitwise_equal(width, rows):
     if not lib.experiments_built():
         # production build: the pair kernel is not linked and every pair is refused
         assert not lib.wide_pair_wgrad_ok(rows, width, width)
-        pytest.skip("experiment kernels not built (NNMPI_EXPERIMENTS=1)")
+        pytest.skip("experiment kernels not built (NNMPI_BUILD_EXPERIMENTS=1)")
     cfg = _wide_cfg(widths=[width] * 4 + [1], n_features=width, n_samples=rows)
     try:
         lib.set_wide_pair(1)

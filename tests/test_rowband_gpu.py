@@ -210,3 +210,21 @@ def test_small_batches_keep_the_grouped_schedule(monkeypatch):
     eng.step()
     assert l_small == l_small and eng.loss() == eng.loss()
 
+
+
+def test_rowband_checkpoint_resume_is_exact(tmp_path):
+    """Checkpoint / resume through the row-band schedule: 3 epochs + resume to 6 == 6 epochs bit
+    for bit (the resumed arena bumps Arena.version, so the v2 weight images are rebuilt from the
+    loaded weights before the first resumed step; the momentum is restored by name)."""
+    from nnmpi_amd.engine import trainer
+    from nnmpi_amd.utils.config import TrainConfig
+    base = dict(device="cuda", print_rank="none", widths=[512, 512, 512, 512, 1], n_features=512,
+                n_samples=8192, dtype="bf16", lr=1e-4, data_gen="device", data_dist="local",
+                scaling="none")
+    ck = str(tmp_path / "rb.pt")
+    full = trainer.run_worker(TrainConfig(nepochs=6, **base))
+    trainer.run_worker(TrainConfig(nepochs=3, checkpoint=ck, **base))
+    res = trainer.run_worker(TrainConfig(nepochs=6, resume=ck, **base))
+    assert full.schedule["rowband"] and res.schedule["rowband"]
+    assert torch.equal(res.final_params, full.final_params)
+    assert res.losses[-3:] == full.losses[-3:]
