@@ -108,7 +108,8 @@ def parse(argv=None):
                    help="steps per replayed hipGraph (1 = one graph launch per step; 0 = auto: "
                         "each run of n steps as few graphs as possible, at most 128 steps each)")
     p.add_argument("--lr", type=float, default=1e-5)
-    p.add_argument("--comm_mode", choices=["auto", "tune", "overlap", "inline", "zero1"],
+    p.add_argument("--comm_mode", choices=["auto", "tune", "overlap", "inline", "zero1",
+                                           "overlap_rowband"],
                    default="auto",
                    help="overlap: per-bucket all-reduce on a comm stream + per-bucket SGD; "
                         "inline: one all-reduce on the compute stream; zero1: reduce-scatter + "
@@ -401,7 +402,7 @@ def run(a, job):
         eng = MLPEngine(spec, arena, make_ops(), sync, device=dev, dtype=dtype,
                         rows_capacity=max(rows, 1), lr=a.lr, momentum=0.9,
                         use_graph=not a.no_graph, overlap=not a.no_overlap,
-                        grouped=not a.no_group)
+                        grouped=not a.no_group, rowband_overlap=(mode == "overlap_rowband"))
         eng.load_batch(X, Y, labels)
         cfg = TrainConfig(widths=list(widths), loss=c["loss"], n_features=widths[0], device="cpu")
         eng.set_scales(*loss_scales(cfg, rows, list(part.counts), widths[-1]))
@@ -512,6 +513,10 @@ def run(a, job):
             cands = [("inline", None), ("zero1", None), ("overlap", a.bucket_mb)]
             if half_mb > a.bucket_mb:
                 cands.append(("overlap", half_mb))
+            if gpu and c["loss"] == "mse":
+                # the row-band step with its last layer's bucket reduced during the other
+                # layers' weight gradients (engine._step_body_rowband_overlap)
+                cands.append(("overlap_rowband", a.bucket_mb))
         for m, bmb in cands:
             milestone(f"tune {m}")
             e = build(m.split("_c")[0], data, bucket_mb=bmb, chunk_tiles=512 if m.endswith("_c2") else 0)

@@ -746,7 +746,8 @@ int wgrad_multi_splits(int nj, int M, int N, int K) {
   return s;
 }
 
-hipError_t wgrad_multi(const WgradArgs* jobs, int nj, int splits, SlabReduce* pending, hipStream_t s) {
+hipError_t wgrad_multi(const WgradArgs* jobs, int nj, const int* splits, SlabReduce* pending,
+                       hipStream_t s) {
   if (nj < 1 || nj > RB_MAXL) return hipErrorInvalidValue;
   WgradMultiParams g{};
   g.nj = nj;
@@ -755,7 +756,7 @@ hipError_t wgrad_multi(const WgradArgs* jobs, int nj, int splits, SlabReduce* pe
     const WgradArgs& a = jobs[j];
     if (wgrad_tile(a.M, a.N) != 128 || a.db == nullptr || a.ws == nullptr || a.dW16 != nullptr)
       return hipErrorInvalidValue;
-    const int want = splits > 0 ? splits : wgrad_multi_splits(nj, a.M, a.N, a.K);
+    const int want = (splits && splits[j] > 0) ? splits[j] : wgrad_multi_splits(nj, a.M, a.N, a.K);
     GemmParams p;
     const int sp = make_wgrad_s(a, p, pending[j], want);
     if (sp == 1) {   // un-split: the combine would have nothing to do -- keep the slab form

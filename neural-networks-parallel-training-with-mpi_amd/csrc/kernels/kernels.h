@@ -9,6 +9,8 @@ namespace nnmpi {
 
 typedef __bf16 bf16;
 
+constexpr int RB_MAXL_PK = 4;   // == RB_MAXL (row-band hidden layers), see below
+
 // Optional optimizer fusion for kernels that produce final (already reduced) gradients: the
 // parameter / momentum / bf16-shadow arrays share the gradient arena's layout, so an element's
 // position is found from its offset to g_base.  g_base == nullptr disables the fusion.
@@ -180,13 +182,22 @@ struct RowbandStep {
   float loss_scale; float* loss_out;
   SgdFuse sg;
   int splits;         // weight-gradient split-K slabs (0 = fill the chip)
+  // 0: the whole step; 1: the band launch + the LAST hidden layer's and the head's weight
+  // gradients (their bucket's all-reduce can start); 2: every other layer's weight gradients.
+  int phase = 0;
+  // split-K plan: 0 every layer `splits` (0: the count that fills the chip with all layers in one
+  // launch); 1 the phased plan -- the last layer filling the chip alone, the others together.
+  // Phases 1 + 2 of a plan == phase 0 of the same plan, bitwise.
+  int plan = 0;
 };
 size_t rowband_workspace_bytes(int rows, int H, int in, int nh, int splits);
 hipError_t rowband_step(const RowbandStep& st, hipStream_t s);
 // Weight gradients of several layers in ONE grouped launch (128x128 tiles, split-K with
 // `splits` slabs each, 0 = fill the chip); pending[j] receives job j's combine.
 int wgrad_multi_splits(int nj, int M, int N, int K);
-hipError_t wgrad_multi(const WgradArgs* jobs, int nj, int splits, SlabReduce* pending, hipStream_t s);
+// (splits: one count per job, or null = fill the chip)
+hipError_t wgrad_multi(const WgradArgs* jobs, int nj, const int* splits, SlabReduce* pending,
+                       hipStream_t s);
 // Several independent combines in ONE launch (same per-block body as slab_reduce).
 hipError_t slab_reduce_multi(const SlabReduce* r, int nr, hipStream_t s);
 
@@ -267,16 +278,29 @@ void sgd_momentum_host(float* p, float* g, float* buf, long long n, const float*
                        int first, int zero_grad);
 
 // ---- optimizer / elementwise (optim.hip) ----
+// Row-band v2 weight images refreshed by the optimizer pass itself (rowband.hip): matrix t
+// ([M][N] row-major, starting `start` elements after the pass's first element -- may be
+// negative when the pass begins inside it) is also written into its fragment-major image pkf
+// and that of its transpose pkd (either may be null).
+struct SgdPack {
+  int n;
+  long long start[RB_MAXL_PK];
+  int M[RB_MAXL_PK], N[RB_MAXL_PK];
+  bf16* pkf[RB_MAXL_PK];
+  bf16* pkd[RB_MAXL_PK];
+};
 // hp = {lr, momentum, dampening, weight_decay, grad_scale}
 hipError_t sgd_momentum(float* p, float* g, float* buf, bf16* shadow, long long n,
-                        const float* hp, int nesterov, int first, int zero_grad, hipStream_t s);
+                        const float* hp, int nesterov, int first, int zero_grad, hipStream_t s,
+                        const SgdPack* pack = nullptr);
 // the same update on a fixed grid of `blocks` blocks (runs beside a GEMM, see optim.hip)
 hipError_t sgd_momentum_bg(float* p, float* g, float* buf, bf16* shadow, long long n,
                            const float* hp, int nesterov, int first, int zero_grad, int blocks,
                            hipStream_t s);
 // the same update with the gradient read from a bf16 buffer (the bf16 all-reduce payload)
 hipError_t sgd_momentum_bf16grad(float* p, const bf16* g, float* buf, bf16* shadow, long long n,
-                                 const float* hp, int nesterov, int first, hipStream_t s);
+                                 const float* hp, int nesterov, int first, hipStream_t s,
+                                 const SgdPack* pack = nullptr);
 hipError_t cast_f32_bf16(const float* x, bf16* y, long long n, hipStream_t s);
 hipError_t scale_f32(float* x, long long n, float a, hipStream_t s);
 hipError_t cast_bf16_f32(const bf16* x, float* y, long long n, hipStream_t s);

@@ -30,7 +30,7 @@ template <typename TG>
 __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, TG* __restrict__ g,
                                                   float* __restrict__ buf, bf16* __restrict__ shadow,
                                                   long long n4, const float* __restrict__ hp,
-                                                  int nesterov, int first, int zero_grad) {
+                                                  int nesterov, int first, int zero_grad, SgdPack pk) {
   const float lr = hp[0], mom = hp[1], damp = hp[2], wd = hp[3], gs = hp[4];
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
@@ -54,6 +54,13 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, TG* __r
     if constexpr (sizeof(TG) == 4) {
       if (zero_grad) reinterpret_cast<f32x4*>(g)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
     }
+    for (int t = 0; t < pk.n; ++t) {   // row-band v2 weight images of the updated weights
+      const long long loc = i * 4 - pk.start[t];
+      if (loc >= 0 && loc < (long long)pk.M[t] * pk.N[t]) {
+        const int m = (int)(loc / pk.N[t]), c = (int)(loc % pk.N[t]);
+        rb_pack_store4(pk.pkf[t], pk.pkd[t], m, c, pk.M[t], pk.N[t], pv);
+      }
+    }
   }
 }
 
@@ -62,11 +69,21 @@ static int grid_for(long long n, int per_thread = 1) {
   return (int)std::max<long long>(1, std::min<long long>(b, 2048));
 }
 
+static bool pack_ok(const SgdPack* pk) {
+  if (!pk) return true;
+  if (pk->n < 0 || pk->n > RB_MAXL_PK) return false;
+  for (int t = 0; t < pk->n; ++t)   // whole float4 groups inside one matrix row, 16x32 tiles
+    if (pk->start[t] % 4 || pk->N[t] % 32 || pk->M[t] % 32) return false;
+  return true;
+}
+
 hipError_t sgd_momentum(float* p, float* g, float* buf, bf16* shadow, long long n,
-                        const float* hp, int nesterov, int first, int zero_grad, hipStream_t s) {
-  if (n % 4 != 0) return hipErrorInvalidValue;
+                        const float* hp, int nesterov, int first, int zero_grad, hipStream_t s,
+                        const SgdPack* pack) {
+  if (n % 4 != 0 || !pack_ok(pack)) return hipErrorInvalidValue;
+  const SgdPack pk = pack ? *pack : SgdPack{};
   hipLaunchKernelGGL(sgd_kernel<float>, dim3(grid_for(n / 4)), dim3(256), 0, s, p, g, buf, shadow,
-                     n / 4, hp, nesterov, first, zero_grad);
+                     n / 4, hp, nesterov, first, zero_grad, pk);
   return hipGetLastError();
 }
 
@@ -78,15 +95,17 @@ hipError_t sgd_momentum_bg(float* p, float* g, float* buf, bf16* shadow, long lo
                            hipStream_t s) {
   if (n % 4 != 0 || blocks < 1) return hipErrorInvalidValue;
   hipLaunchKernelGGL(sgd_kernel<float>, dim3(blocks), dim3(256), 0, s, p, g, buf, shadow, n / 4,
-                     hp, nesterov, first, zero_grad);
+                     hp, nesterov, first, zero_grad, SgdPack{});
   return hipGetLastError();
 }
 
 hipError_t sgd_momentum_bf16grad(float* p, const bf16* g, float* buf, bf16* shadow, long long n,
-                                 const float* hp, int nesterov, int first, hipStream_t s) {
-  if (n % 4 != 0) return hipErrorInvalidValue;
+                                 const float* hp, int nesterov, int first, hipStream_t s,
+                                 const SgdPack* pack) {
+  if (n % 4 != 0 || !pack_ok(pack)) return hipErrorInvalidValue;
+  const SgdPack pk = pack ? *pack : SgdPack{};
   hipLaunchKernelGGL(sgd_kernel<const bf16>, dim3(grid_for(n / 4)), dim3(256), 0, s, p, g, buf,
-                     shadow, n / 4, hp, nesterov, first, 0);
+                     shadow, n / 4, hp, nesterov, first, 0, pk);
   return hipGetLastError();
 }
 

@@ -900,9 +900,22 @@ static int rb_splits(int splits, int nh, int H, int rows) {
   return env > 0 ? env : wgrad_multi_splits(nh, H, H, rows);
 }
 
+// Split-K slabs of layer l's weight gradient under plan 0 / 1 (RowbandStep::plan).  A layer's
+// gradient sums its slabs in a fixed order, so the phases of one plan are bitwise equal to its
+// single launch.
+static int rb_layer_splits(int plan, int splits, int nh, int H, int rows, int l) {
+  if (plan == 0) return rb_splits(splits, nh, H, rows);
+  return rb_splits(0, l == nh - 1 ? 1 : std::max(1, nh - 1), H, rows);
+}
+
+// slab capacity per layer: the largest count of either plan
+static int rb_max_splits(int splits, int nh, int H, int rows) {
+  return std::max(rb_splits(splits, nh, H, rows), rb_splits(0, 1, H, rows));
+}
+
 size_t rowband_workspace_bytes(int rows, int H, int in, int nh, int splits) {
   const size_t G = (size_t)rowband_blocks(rows);
-  const int S = rb_splits(splits, nh, H, rows);
+  const int S = rb_max_splits(splits, nh, H, rows);
   const size_t head = G * H + rb_pad4(G) + rb_pad4(G);
   return (head + (size_t)nh * S * ((size_t)H * std::max(H, in) + H)) * sizeof(float);
 }
@@ -913,7 +926,7 @@ hipError_t rowband_step(const RowbandStep& st0, hipStream_t s) {
   if (!p.Pf[0]) p.in = p.H;
   const bool ok = p.Pf[0] ? rowband2_ok(p.rows, p.H, p.in, p.nh, 1, LOSS_MSE, p.act)
                           : rowband_ok(p.rows, p.H, p.H, p.nh, 1, LOSS_MSE, p.act);
-  if (!ok || !st.ws) return hipErrorInvalidValue;
+  if (!ok || !st.ws || st.phase < 0 || st.phase > 2) return hipErrorInvalidValue;
   const int H = p.H, nh = p.nh;
   const size_t G = (size_t)rowband_blocks(p.rows);
   float* ws = st.ws;
@@ -921,29 +934,45 @@ hipError_t rowband_step(const RowbandStep& st0, hipStream_t s) {
   p.bslab = ws + G * H;
   p.loss_part = p.bslab + rb_pad4(G);
   float* slabs = p.loss_part + rb_pad4(G);
-  hipError_t e = rowband_fwd_bwd(p, s);
-  if (e != hipSuccess) return e;
-  const int S = rb_splits(st.splits, nh, H, p.rows);
+  hipError_t e = hipSuccess;
+  if (st.phase <= 1) {
+    e = rowband_fwd_bwd(p, s);
+    if (e != hipSuccess) return e;
+  }
+  const size_t per = (size_t)rb_max_splits(st.splits, nh, H, p.rows) * ((size_t)H * std::max(H, p.in) + H);
+  if (st.plan < 0 || st.plan > 1) return hipErrorInvalidValue;
+  // the layers of this phase: [l0, l1); phase 1 also combines the head
+  const int l0 = st.phase == 1 ? nh - 1 : 0;
+  const int l1 = st.phase == 2 ? nh - 1 : nh;
+  const bool head = st.phase != 2;
   WgradArgs jobs[RB_MAXL];
   SlabReduce red[RB_MAXL + 1];
-  const size_t per = (size_t)S * ((size_t)H * std::max(H, p.in) + H);
-  for (int l = 0; l < nh; ++l) {
-    jobs[l] = WgradArgs{p.dz[l], H, l == 0 ? p.X : p.a[l - 1], l == 0 ? p.ldx : H, st.gW[l],
-                        st.gb[l], H, l == 0 ? p.in : H, p.rows, slabs + (size_t)l * per, st.sg};
+  int sp[RB_MAXL];
+  const int nj = l1 - l0;
+  for (int l = l0; l < l1; ++l) {
+    jobs[l - l0] = WgradArgs{p.dz[l], H, l == 0 ? p.X : p.a[l - 1], l == 0 ? p.ldx : H, st.gW[l],
+                             st.gb[l], H, l == 0 ? p.in : H, p.rows, slabs + (size_t)l * per, st.sg};
+    sp[l - l0] = rb_layer_splits(st.plan, st.splits, nh, H, p.rows, l);
   }
-  e = wgrad_multi(jobs, nh, S, red, s);
-  if (e != hipSuccess) return e;
-  if (st.sg.g_base && p.Pf[0]) {
-    // one rank: the combines apply the update, and write the v2 weight images of the NEW weights
-    // for the next step's row-band launch
-    for (int l = 0; l < nh; ++l) {
-      red[l].pkf = const_cast<bf16*>(p.Pf[l]);
-      red[l].pkd = l >= 1 ? const_cast<bf16*>(p.Pd[l]) : nullptr;
+  if (nj > 0) {
+    e = wgrad_multi(jobs, nj, sp, red, s);
+    if (e != hipSuccess) return e;
+    if (st.sg.g_base && p.Pf[0]) {
+      // one rank: the combines apply the update, and write the v2 weight images of the NEW
+      // weights for the next step's row-band launch
+      for (int l = l0; l < l1; ++l) {
+        red[l - l0].pkf = const_cast<bf16*>(p.Pf[l]);
+        red[l - l0].pkd = l >= 1 ? const_cast<bf16*>(p.Pd[l]) : nullptr;
+      }
     }
   }
-  red[nh] = SlabReduce{p.wslab, (int)G, H, 1, H, st.gWh, H, p.bslab, 1, st.gbh, p.loss_part, (int)G,
-                       st.loss_scale, st.loss_out, st.sg};
-  return slab_reduce_multi(red, nh + 1, s);
+  int nr = nj;
+  if (head) {
+    red[nr++] = SlabReduce{p.wslab, (int)G, H, 1, H, st.gWh, H, p.bslab, 1, st.gbh, p.loss_part,
+                           (int)G, st.loss_scale, st.loss_out, st.sg};
+  }
+  if (nr == 0) return hipSuccess;
+  return slab_reduce_multi(red, nr, s);
 }
 
 }  // namespace nnmpi

@@ -43,7 +43,8 @@ class MLPEngine:
                  rows_capacity: int, lr: float, momentum: float, dampening: float = 0.0,
                  weight_decay: float = 0.0, nesterov: bool = False, use_graph: bool = True,
                  use_tiny: Optional[bool] = None, overlap: bool = True, fuse_sgd: bool = True,
-                 grouped: bool = True):
+                 grouped: bool = True, rowband_overlap: bool = False,
+                 rowband_plan: Optional[int] = None):
         self.spec = spec
         self.arena = arena
         self.ops = ops
@@ -121,9 +122,19 @@ class MLPEngine:
         # ZeRO-1): it produces every layer's gradient at once, so there is nothing for a
         # per-bucket overlapped schedule to hide.  NNMPI_ROWBAND=0 keeps the grouped schedule
         # (proxy step 0.082 vs 0.094 ms, profiles/r3s2_rowband_*).
-        self.rowband = (self.overlap and dtype == torch.bfloat16 and inline_sync and
+        # rowband_overlap: also with per-bucket collectives on the comm stream -- the band launch
+        # and the last hidden layer's + the head's weight gradients first, their bucket's
+        # all-reduce overlapping the other layers' weight gradients (_step_body_rowband_overlap)
+        self.rb_overlap = bool(rowband_overlap) and self.comm_overlap
+        self.rowband = (self.overlap and dtype == torch.bfloat16 and
+                        (inline_sync or self.rb_overlap) and
                         hasattr(ops, "rowband_ok") and knob("NNMPI_ROWBAND", "1") != "0"
                         and ops.rowband_ok(self.R, w, self.act, spec.loss))
+        # split-K plan of the weight gradients (RowbandStep::plan): the overlapped schedule's
+        # phased plan, else one launch filling the chip with every layer
+        if rowband_plan is None:
+            rowband_plan = int(knob("NNMPI_RB_PLAN", "1" if self.rb_overlap else "0"))
+        self.rb_plan = int(rowband_plan)
         self.ws_rb = (torch.zeros(ops.rowband_workspace_bytes(self.R, w[1], L - 1, in_=w[0]) // 4 + 64,
                                   dtype=torch.float32, device=dev) if self.rowband else None)
         # v2 row-band kernel: the weights also live in fragment-major images (one global load per
@@ -570,7 +581,7 @@ class MLPEngine:
     def schedule_name(self) -> str:
         """The step schedule a batch of the loaded size runs (bench / result reports)."""
         if self.uses_rowband():
-            return "rowband"
+            return "rowband_overlap" if self.rb_overlap else "rowband"
         if self.grouped:
             return "grouped"
         return "overlap" if self.overlap else "sequential"
@@ -578,20 +589,69 @@ class MLPEngine:
     # Row-band schedule (see rowband.hip): three launches per step.  One rank: the combine
     # applies the SGD update; several ranks: the combine writes the gradient, then the inline
     # all-reduce (or ZeRO-1's reduce-scatter / all-gather) and the update follow.
-    def _step_body_rowband(self, first: bool):
-        rows, ops, ar, L = self.rows, self.ops, self.arena, self.L
-        fz = ops.sgd_fusion(ar, self.hp, self.nesterov, first) if self.fuse_sgd else None
-        last = L - 1
-        layers = [(ar.compute_weight(i), ar.bias(i), self.acts[i][:rows], self._dzl(i, rows),
-                   ar.grad_weight(i), ar.grad_bias(i)) for i in range(L - 1)]
+    def _rb_images(self):
+        """{layer: (forward image, dgrad image)} for an optimizer pass of a row-band step (the
+        pass refreshes the v2 images it covers), else None."""
+        if self.rb_packed is None or not self.uses_rowband():
+            return None
+        return dict(enumerate(self.rb_packed))
+
+    def _rb_layers(self):
+        rows, ar = self.rows, self.arena
+        return [(ar.compute_weight(i), ar.bias(i), self.acts[i][:rows], self._dzl(i, rows),
+                 ar.grad_weight(i), ar.grad_bias(i)) for i in range(self.L - 1)]
+
+    def _rb_launch(self, sgd=None, phase: int = 0):
+        rows, ar, last = self.rows, self.arena, self.L - 1
         kw = {}
         if self.rb_packed is not None:
-            if not self._rb_current():
+            if phase <= 1 and not self._rb_current():
                 self._rb_pack()
             kw["packed"] = self.rb_packed
-        ops.rowband_step(self.X[:rows], layers, ar.weight(last), ar.bias(last), self.Y[:rows],
-                         self.inv_count, ar.grad_weight(last), ar.grad_bias(last), self.ws_rb,
-                         self.loss_scale, self.loss_out, self.act, sgd=fz, **kw)
+        self.ops.rowband_step(self.X[:rows], self._rb_layers(), ar.weight(last), ar.bias(last),
+                              self.Y[:rows], self.inv_count, ar.grad_weight(last),
+                              ar.grad_bias(last), self.ws_rb, self.loss_scale, self.loss_out,
+                              self.act, sgd=sgd, phase=phase, plan=self.rb_plan, **kw)
+
+    # Row-band step with per-bucket collectives on the comm stream (several ranks): the band
+    # launch and the last hidden layer's + the head's weight gradients first (phase 1); their
+    # bucket's all-reduce -- and its SGD, which also refreshes that layer's v2 images -- run on
+    # the comm stream while the other layers' weight gradients compute (phase 2); the buckets
+    # those complete follow.  Every weight's last reader is the band launch.
+    def _step_body_rowband_overlap(self, first: bool):
+        ar, L, main = self.arena, self.L, self.stream
+        self.sync.begin()
+        self._sgd_done = set()
+        self._reduced = {}
+        self._pending_sgd = []
+        self._written16 = []
+        self._waited = set()
+        self._first = first
+        self._rb_launch(phase=1)
+        for l in range(L):
+            main.record_event(self.ev_wfree[l])
+        self._mark("bwd_tail")
+        self._layer_done(L - 1, main)
+        self._layer_done(L - 2, main)
+        if L > 2:
+            self._rb_launch(phase=2)
+            for i in range(L - 3, -1, -1):
+                self._layer_done(i, main)
+        self._mark("bwd")
+        self._join_comm()
+        self._mark("comm")
+        for b in ar.buckets:
+            if b.index not in self._sgd_done:
+                self.ops.sgd(ar, self.hp, self.nesterov, first, offset=b.offset, numel=b.numel,
+                             **self._upd_kw())
+        self._rb_fresh = self.rb_packed is not None
+
+    def _step_body_rowband(self, first: bool):
+        rows, ops, ar, L = self.rows, self.ops, self.arena, self.L
+        if self.rb_overlap:
+            return self._step_body_rowband_overlap(first)
+        fz = ops.sgd_fusion(ar, self.hp, self.nesterov, first) if self.fuse_sgd else None
+        self._rb_launch(sgd=fz)
         # the fused combine rewrote the images from the updated weights; the multi-rank update
         # below does not
         self._rb_fresh = fz is not None
@@ -606,7 +666,12 @@ class MLPEngine:
             self.sync.launch_bucket(b, self.stream)
         self.sync.finish()
         self._mark("comm")
-        ops.sgd(ar, self.hp, self.nesterov, first)
+        if self.rb_packed is not None:
+            # the optimizer pass also rewrites the v2 weight images from the updated weights
+            ops.sgd(ar, self.hp, self.nesterov, first, images=dict(enumerate(self.rb_packed)))
+            self._rb_fresh = True
+        else:
+            ops.sgd(ar, self.hp, self.nesterov, first)
 
     # Grouped schedule: the backward of layer i is ONE launch holding three independent jobs —
     # dgrad_i, wgrad_i (split-K partial slabs) and the slab combine of layer i+1 (with the SGD
@@ -746,7 +811,11 @@ class MLPEngine:
                 n -= 1
 
     def _upd_kw(self):
-        return {} if self._upd_grad is None else {"grad_bf16": self._upd_grad}
+        kw = {} if self._upd_grad is None else {"grad_bf16": self._upd_grad}
+        img = self._rb_images()
+        if img is not None:
+            kw["images"] = img
+        return kw
 
     def _join_comm(self):
         """Join the comm stream into the compute stream.  Updates still queued at this point

@@ -394,6 +394,7 @@ def _run(j: Job) -> TrainResult:
     mb = bs if bs else (max(1, math.ceil(max_rows / K)) if K > 1 else None)
     cap = min(mb, max_rows) if mb else max_rows
     eng = MLPEngine(spec, arena, ops, sync, device=j.device, dtype=dtype,
+                    rowband_overlap=cfg.comm_mode == "overlap_rowband",
                     rows_capacity=max(cap, 1), lr=cfg.lr, momentum=cfg.momentum,
                     dampening=cfg.dampening, weight_decay=cfg.weight_decay,
                     nesterov=cfg.nesterov, use_graph=cfg.graph, overlap=cfg.overlap)

@@ -350,13 +350,16 @@ class HipOps:
                               self.stream)
 
     def rowband_step(self, X, layers, wh, bh, y, inv_count: float, gWh, gbh, ws, loss_scale: float,
-                     loss_out, act: str, sgd=None, splits: int = 0, packed=None):
+                     loss_out, act: str, sgd=None, splits: int = 0, packed=None, phase: int = 0,
+                     plan: int = 0):
         """One step body of a narrow MSE regressor in three launches.  ``layers``: per hidden
         layer ``(W16, b, a_out, dz_out, gW, gb)``.  Writes every activation and dZ, the
         gradients (or, with ``sgd``, applies the fused update at their arena positions -- and
         rewrites the ``packed`` v2 weight images from the new weights) and
         ``loss_out[0] = loss_scale * sum of squared errors``.  ``packed``: the v2 weight images
-        (must match the weights); None runs the v1 kernel."""
+        (must match the weights); None runs the v1 kernel.  ``phase`` 1 / 2: the band launch with
+        the last hidden layer's and the head's gradients / the other layers' gradients (the
+        overlapped multi-rank schedule); ``plan``: the split-K plan (RowbandStep, kernels.h)."""
         rows, in_ = X.shape
         nh = len(layers)
         H = layers[0][0].shape[0]
@@ -383,7 +386,7 @@ class HipOps:
         self.lib.rowband_step(_p(X), X.stride(0), rows, H, in_, ACT_CODES[act], lay, _p(wh),
                               _p(bh), _p(y), float(inv_count), _p(gWh), _p(gbh), _p(ws),
                               float(loss_scale), _p(loss_out), sgd, int(splits),
-                              self._packed_ptrs(packed), self.stream)
+                              self._packed_ptrs(packed), int(phase), int(plan), self.stream)
 
     # ---------------- tiny fused MLP ----------------
     def tiny_workspace_bytes(self, rows, numel) -> int:
@@ -416,19 +419,29 @@ class HipOps:
 
     # ---------------- optimizer ----------------
     def sgd(self, arena, hp, nesterov: bool, first: bool, zero_grad: bool = True, offset: int = 0,
-            numel: int = None, grad_bf16=None):
+            numel: int = None, grad_bf16=None, images=None):
         """``grad_bf16``: read the gradient from this bf16 buffer (same layout as the arena)
-        instead of ``arena.grad`` -- the bf16 all-reduce payload, updated from directly."""
+        instead of ``arena.grad`` -- the bf16 all-reduce payload, updated from directly.
+        ``images``: {layer: (pkf, pkd)} row-band v2 weight images to refresh from the updated
+        weights of those layers (the parts inside this pass's range)."""
         n = arena.numel - offset if numel is None else numel
         e = 4  # bytes per fp32 element
         sh = _p(arena.shadow) + 2 * offset if arena.shadow is not None else 0
+        pack = None
+        if images:
+            pack = []
+            for li, (pf, pd) in images.items():
+                slot = arena.by_name[f"layers.{2 * li}.weight"]
+                M, N = slot.shape
+                if slot.offset < offset + n and slot.offset + M * N > offset:
+                    pack.append((slot.offset - offset, M, N, _p(pf), _p(pd) if pd is not None else 0))
         if grad_bf16 is not None:
             _check(grad_bf16.dtype == torch.bfloat16 and grad_bf16.numel() >= offset + n,
                    "sgd: bf16 gradient buffer too small")
             self.lib.sgd_momentum_bf16grad(_p(arena.master) + e * offset, _p(grad_bf16) + 2 * offset,
                                            _p(arena.momentum) + e * offset, sh, n, _p(hp),
-                                           int(nesterov), int(first), self.stream)
+                                           int(nesterov), int(first), self.stream, pack)
             return
         self.lib.sgd_momentum(_p(arena.master) + e * offset, _p(arena.grad) + e * offset,
                               _p(arena.momentum) + e * offset, sh, n, _p(hp), int(nesterov),
-                              int(first), int(zero_grad), self.stream)
+                              int(first), int(zero_grad), self.stream, pack)

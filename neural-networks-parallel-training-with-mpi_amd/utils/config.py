@@ -70,7 +70,8 @@ class TrainConfig:
     comm: str = "auto"                # auto | native (RCCL) | torch (torch.distributed) |
                                       # gloo (gloo even for device tensors) | none
     sync: str = "allreduce"           # allreduce | root (reference-style reduce+bcast)
-    comm_mode: str = "auto"           # auto | overlap (comm stream) | inline (compute stream)
+    comm_mode: str = "auto"           # auto | overlap (comm stream) | inline (compute stream) |
+                                      # overlap_rowband (the row-band step, comm stream)
     bucket_mb: float = 1.0
     overlap: bool = True
     graph: bool = True                # capture the steady-state step in a HIP graph
@@ -156,7 +157,8 @@ def build_parser() -> argparse.ArgumentParser:
                         "torch.distributed (nccl on GPU, gloo on CPU), gloo = gloo also for "
                         "device tensors (several ranks sharing one GPU)")
     p.add_argument("--sync", choices=["allreduce", "root"], default="allreduce")
-    p.add_argument("--comm_mode", choices=["auto", "overlap", "inline"], default="auto")
+    p.add_argument("--comm_mode", choices=["auto", "overlap", "inline", "overlap_rowband"],
+                   default="auto")
     p.add_argument("--bucket_mb", type=float, default=1.0)
     p.add_argument("--no_overlap", dest="overlap", action="store_false")
     p.add_argument("--no_graph", dest="graph", action="store_false")

@@ -22,6 +22,7 @@ KNOBS = {
     "NNMPI_ROWBAND_MIN_ROWS": "smallest batch that takes the row-band step",
     "NNMPI_RB_V2": "row-band v2 kernel with fragment-major weight images (0: v1)",
     "NNMPI_RB_SPLITS": "row-band weight-gradient split-K slabs",
+    "NNMPI_RB_PLAN": "row-band split-K plan (0 one launch, 1 phased; RowbandStep::plan)",
     "NNMPI_DEFER": "deferred bucket updates in weight-gradient epilogues (0 off)",
     "NNMPI_DEFER_WAIT": "deferred update waits per chunk / per layer",
     "NNMPI_CHUNK_MIN_TILES": "tiles per output-row chunk bucket",

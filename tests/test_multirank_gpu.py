@@ -355,3 +355,27 @@ def test_rowband_rccl_two_ranks_inline_and_zero1_match_one_rank():
     assert torch.equal(a[0]["final"], b[0]["final"])
     torch.testing.assert_close(a[0]["final"], one[0]["final"], rtol=2e-2, atol=2e-3)
 
+
+
+@pytest.mark.rowband
+@pytest.mark.parametrize("world", [2, 3])
+def test_rowband_overlap_matches_inline_bitwise(world):
+    """The overlapped row-band schedule (--comm_mode overlap_rowband: the last hidden layer's and
+    the head's bucket all-reduced on the comm stream while the other layers' weight gradients
+    compute, each bucket's SGD -- which also refreshes its layers' v2 images -- behind its
+    collective) against the inline row-band sync with the same split-K plan
+    (NNMPI_RB_PLAN=1): RCCL ranks sharing the GPU, an uneven split at P=3, bitwise-equal
+    parameters and losses, replicas bitwise equal."""
+    kw = dict(widths=[512, 512, 512, 512, 1], n_features=512, n_samples=2048 * world - 1,
+              lr=1e-4, nepochs=4)
+    a = run_ranks_proc(_cfg(comm="native", comm_mode="overlap_rowband", **kw), world,
+                       env_per_rank=rccl_env, timeout=300.0)
+    b = run_ranks_proc(_cfg(comm="native", comm_mode="inline", **kw), world,
+                       env_per_rank=lambda r: dict(rccl_env(r), NNMPI_RB_PLAN="1"), timeout=300.0)
+    for o in a + b:
+        assert o["schedule"]["rowband"], o["schedule"]
+    _replicas_equal(a)
+    _replicas_equal(b)
+    assert torch.equal(a[0]["final"], b[0]["final"])
+    for r in range(world):
+        assert a[r]["losses"] == b[r]["losses"], r
