@@ -73,6 +73,10 @@ CONFIGS = {
                      model="mlp_512x3_regression(512-512-512-1)"),
     "wide8192": dict(widths=[8192] * 5 + [1], loss="mse", rows=4096,
                      model="mlp_8192x4_regression(8192x4-1)"),
+    # mid-size: a bf16 all-reduce payload (> 64 MB of fp32 gradient) on a model small enough
+    # for multi-rank rehearsals on one GPU
+    "wide2048": dict(widths=[2048] * 5 + [1], loss="mse", rows=2048,
+                     model="mlp_2048x4_regression(2048x4-1)"),
     "mnist": dict(widths=[784, 1024, 1024, 10], loss="xent", rows=8192,
                   model="mlp_mnist_shape(784-1024-1024-10,xent)"),
     # the reference config itself: fp32 like the reference (whole step in one tiny-MLP kernel)
@@ -363,10 +367,11 @@ def run(a, job):
             labels = None
         return part, X.to(dtype), Y, labels
 
-    def build(mode, data, comm=True, bucket_mb=None, chunk_tiles=0):
+    def build(mode, data, comm=True, bucket_mb=None, chunk_tiles=0, bf16_reduce=None):
         """One arena + gradient-sync strategy + engine over ``data`` (a shard()).
-        mode: inline | overlap | zero1 | none (no gradient synchronisation at all);
-        chunk_tiles: 256x256 tiles per output-row chunk bucket at least (0: the default)."""
+        mode: inline | overlap | overlap_rowband | zero1 | none (no gradient synchronisation);
+        chunk_tiles: 256x256 tiles per output-row chunk bucket at least (0: the default);
+        bf16_reduce: the bf16-payload all-reduce algorithm (acc32 | rccl; None: the default)."""
         part, X, Y, labels = data
         rows = part.rows(rank)
         model = reference_init(widths, "relu", seed=0, device=dev if (big and gpu) else None)
@@ -388,7 +393,7 @@ def run(a, job):
                 sync = ShardedSync(arena, world, rank, native_comm=native_comm)
             else:
                 sync = NativeRcclSync(arena, native_comm, world, inline=(mode == "inline"),
-                                      grad_dtype=grad_dtype)
+                                      grad_dtype=grad_dtype, bf16_reduce=bf16_reduce)
         else:
             dist.broadcast(arena.master, src=0, group=comm_group)
             arena.sync_shadow()
@@ -497,38 +502,52 @@ def run(a, job):
     tune = None
     bucket_mb = a.bucket_mb
     chunk_tiles = a.chunk_tiles
+    bf16_reduce = None
+    best_t = None
+    best = None
     if mode == "tune":
         tune = {}
         eng = None
         # overlap candidates: --bucket_mb buckets, and ~two buckets (the first all-reduce
         # larger, the exposed last one smaller than the whole gradient)
         half_mb = round(grad_bytes / 2 ** 20 * 0.6, 3)
+        ct0 = a.chunk_tiles
         if grad_bytes > INLINE_MAX_GRAD_BYTES:
             # overlap with 4 chunk buckets per 8192-wide layer (one 256-tile wave each: the
             # earliest collective start) and with 2 (half the launches and cross-queue waits,
             # twice the exposed last collective); measured at one rank: docs/PERF.md
-            cands = [("overlap", a.bucket_mb), ("overlap_c2", a.bucket_mb), ("inline", None),
-                     ("zero1", None)]
+            cands = [("overlap", "overlap", a.bucket_mb, ct0), ("overlap_c2", "overlap", a.bucket_mb, 512),
+                     ("inline", "inline", None, ct0), ("zero1", "zero1", None, ct0)]
         else:
-            cands = [("inline", None), ("zero1", None), ("overlap", a.bucket_mb)]
+            cands = [("inline", "inline", None, ct0), ("zero1", "zero1", None, ct0),
+                     ("overlap", "overlap", a.bucket_mb, ct0)]
             if half_mb > a.bucket_mb:
-                cands.append(("overlap", half_mb))
+                cands.append((f"overlap_{half_mb}mb", "overlap", half_mb, ct0))
             if gpu and c["loss"] == "mse":
                 # the row-band step with its last layer's bucket reduced during the other
                 # layers' weight gradients (engine._step_body_rowband_overlap)
-                cands.append(("overlap_rowband", a.bucket_mb))
-        for m, bmb in cands:
-            milestone(f"tune {m}")
-            e = build(m.split("_c")[0], data, bucket_mb=bmb, chunk_tiles=512 if m.endswith("_c2") else 0)
+                cands.append(("overlap_rowband", "overlap_rowband", a.bucket_mb, ct0))
+
+        def try_cand(key, m, bmb, ct, red=None):
+            nonlocal eng, best_t, mode, bucket_mb, chunk_tiles, bf16_reduce, best
+            milestone(f"tune {key}")
+            e = build(m, data, bucket_mb=bmb, chunk_tiles=ct, bf16_reduce=red)
             e.run_steps(a.warmup, chunk_for(a.warmup))
             tm = min(timed(e, a.tune_steps, chunk_for(a.tune_steps)) for _ in range(2))
-            key = m if bmb in (None, a.bucket_mb) else f"{m}_{bmb}mb"
             tune[key] = round(tm / a.tune_steps * 1e3, 5)
             # every rank sees the same max-over-ranks times, so every rank keeps the same mode
             if eng is None or tm < best_t:
-                eng, best_t, mode, bucket_mb = e, tm, m, (bmb or a.bucket_mb)
-                chunk_tiles = 512 if m.endswith("_c2") else 0
+                eng, best_t, mode, bucket_mb, chunk_tiles = e, tm, key, (bmb or a.bucket_mb), ct
+                bf16_reduce, best = red, (key, m, bmb, ct)
             del e
+
+        for key, m, bmb, ct in cands:
+            try_cand(key, m, bmb, ct)
+        if grad_dtype == "bf16" and native_comm is not None and best[1] != "zero1":
+            # the bf16 all-reduce algorithm is tuned too, under the chosen schedule: the
+            # one-rounding all-to-all (acc32, the default) vs RCCL's own ring / tree algorithms
+            key, m, bmb, ct = best
+            try_cand(f"{key}+rccl", m, bmb, ct, red="rccl")
         if gpu:
             torch.cuda.empty_cache()
         # the chosen engine idled while the other candidates ran: warm it again (untimed, like
@@ -558,9 +577,10 @@ def run(a, job):
     loss = eng.loss()
     ms = elapsed / a.steps * 1e3
     value = n_global * a.steps / elapsed
-    sharded = mode == "zero1"
     mode_name = mode
-    mode = mode.split("_c")[0]
+    # (the tuner's key names the candidate; best[1] is its schedule)
+    mode = best[1] if best is not None else mode
+    sharded = mode == "zero1"
     n_buckets = len(eng.arena.buckets)
     wire = comm_volume(eng.arena.numel, world, grad_dtype, sharded=sharded,
                        shadow=eng.arena.shadow is not None)["wire_bytes_per_rank"]
@@ -631,7 +651,7 @@ def run(a, job):
             nonlocal strong
             sdata = shard(rows_pg)
             e = build(mode if mode != "none" else "inline", sdata, bucket_mb=bucket_mb,
-                      chunk_tiles=chunk_tiles)
+                      chunk_tiles=chunk_tiles, bf16_reduce=bf16_reduce)
             e.run_steps(min(a.warmup, 10) + 1, chunk_for(min(a.warmup, 10)))
             s_ms = timed(e, n_ex, chunk_for(n_ex)) / n_ex * 1e3
             comp_ms = res["comp_ms"]
@@ -698,6 +718,9 @@ def run(a, job):
                        "comm_mode": mode_name if use_comm else None,
                        "comm_tune_ms_per_step": tune,
                        "grad_dtype": grad_dtype if use_comm else None,
+                       "bf16_reduce": ((bf16_reduce or eng.sync.bf16_reduce)
+                                       if use_comm and grad_dtype == "bf16"
+                                       and hasattr(eng.sync, "bf16_reduce") else None),
                        "grad_wire_bytes_per_rank": wire,
                        "bucket_mb": bucket_mb,
                        "n_buckets": n_buckets},
