@@ -216,6 +216,11 @@ void GradSync::bucket_ready(int b, void* ptr, size_t count, int dtype, hipStream
     comm_->allreduce_bf16_acc32(ptr, acc32_scratch_, count, comm_stream_);
   else
     comm_->allreduce(ptr, count, dtype, 0, comm_stream_);
+  if (standin_blocks_ > 0 && standin_gbps_ > 0.0) {
+    // a ring all-reduce moves 2 (P-1)/P of the bytes per rank; at P = 8: 1.75
+    const double bytes = 1.75 * (double)count * (dtype == 1 ? 2.0 : 4.0);
+    HIP_THROW(cu_hold(standin_blocks_, bytes / (standin_gbps_ * 1e9), comm_stream_));
+  }
 }
 
 void GradSync::join(hipStream_t compute) {

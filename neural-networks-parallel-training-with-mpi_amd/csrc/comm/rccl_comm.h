@@ -77,6 +77,9 @@ class GradSync {
   void bucket_ready(int b, void* ptr, size_t count, int dtype, hipStream_t compute);
   // bf16 buckets use RcclComm::allreduce_bf16_acc32 with this scratch (nullptr: ncclAllReduce)
   void set_acc32_scratch(void* scratch) { acc32_scratch_ = scratch; }
+  // diagnostic: after each bucket's collective, hold `blocks` CUs on the comm stream for the
+  // time the bucket would take at `gbps` bus bandwidth (kernels.h cu_hold; 0 blocks: off)
+  void set_standin(int blocks, double gbps) { standin_blocks_ = blocks; standin_gbps_ = gbps; }
   // comm stream -> (event) -> compute stream: everything launched so far is complete.
   void join(hipStream_t compute);
   hipStream_t comm_stream() const { return comm_stream_; }
@@ -84,6 +87,8 @@ class GradSync {
  private:
   RcclComm* comm_;
   void* acc32_scratch_ = nullptr;
+  int standin_blocks_ = 0;
+  double standin_gbps_ = 0.0;
   hipStream_t comm_stream_ = nullptr;
   std::vector<hipEvent_t> ready_;
   hipEvent_t done_ = nullptr;

@@ -309,6 +309,9 @@ hipError_t checksum_f32(const float* x, long long n, double* out, hipStream_t s)
 // for j < n, accumulated in fp32 (the owner step of RcclComm::allreduce_bf16_acc32)
 hipError_t sum_slices_bf16(bf16* out, const bf16* scratch, int P, int me, long long stride,
                            long long n, hipStream_t s);
+// diagnostic: `blocks` 256-thread blocks holding their CUs (and a full wave's VGPRs) for
+// `seconds` of wall time, then exiting (standin.hip; the collective stand-in)
+hipError_t cu_hold(int blocks, double seconds, hipStream_t s);
 // bitwise replica hash of n 32-bit words; out: 1025 uint64, result at out[1024]
 hipError_t hash_u32(const unsigned* x, long long n, unsigned long long* out, hipStream_t s);
 

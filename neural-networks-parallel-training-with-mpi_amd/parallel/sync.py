@@ -234,6 +234,12 @@ class NativeRcclSync(GradSync):
         self.bf16_reduce = bf16_reduce or knob("NNMPI_BF16_REDUCE", "acc32")
         if self.bf16_reduce not in ("acc32", "rccl"):
             raise ValueError(f"bf16_reduce must be acc32 or rccl, not {self.bf16_reduce!r}")
+        # collective stand-in (measurement only): "k:gbps" holds k CUs on the comm stream after
+        # each bucket's collective for its bytes at gbps (csrc/kernels/standin.hip)
+        st = knob("NNMPI_COMM_STANDIN", "")
+        if st:
+            k, gbps = st.split(":")
+            self.gs.set_standin(int(k), float(gbps))
         self.scratch = None
         if self.bf16 and self.bf16_reduce == "acc32" and mode != "root":
             # one bucket reduces at a time on its stream: scratch for the largest

@@ -36,6 +36,7 @@ KNOBS = {
     "NNMPI_GROUP": "grouped backward launch (0 off)",
     "NNMPI_GRAPH_UPLOAD": "hipGraphUpload after instantiation (0 off)",
     "NNMPI_PAIR": "wide backward pair launches (experiments build)",
+    "NNMPI_COMM_STANDIN": "k:gbps -- k CUs held after every bucket collective (standin.hip)",
 }
 
 # plumbing, not knobs (never reported)
