@@ -150,12 +150,87 @@ __device__ __forceinline__ void slab_reduce_block(const SlabReduce& r, int b, in
   }
 }
 
+// Deep combine (S > 64 partials: one per row band / per head block): a block sums DEEP_COLS
+// columns over DEEP_Q lane groups (group q sums z = q, q + DEEP_Q, ... in order; the groups are
+// then combined in order through LDS).  A block reads S x 16 x 16 B (64 KiB at S = 256) instead
+// of the 64-column form's 256 KiB, so the combine spreads over 16x more blocks (the 256-slab
+// head combine ran on 40 blocks).  Selected by slab_ws() == SLAB_DEEP; bitwise reproducible.
+constexpr int SLAB_DEEP = 32, DEEP_COLS = 16, DEEP_Q = SLAB_THREADS / DEEP_COLS;
+
+__device__ __forceinline__ void slab_reduce_deep_block(const SlabReduce& r, int b, int nb_main,
+                                                       int nb_bias, f32x4* part) {
+  const int c = threadIdx.x % DEEP_COLS, q = threadIdx.x / DEEP_COLS;
+  if (b < nb_main) {
+    const int nv = r.N >> 2;
+    const long long nvec = (long long)r.M * nv;
+    const long long v = (long long)b * DEEP_COLS + c;
+    const bool live = v < nvec;
+    const long long m = live ? v / nv : 0, n = live ? (v % nv) * 4 : 0;
+    const float* p = r.ws + m * r.N + n;
+    float* o = r.out + m * r.ldo + n;
+    const bool upd = q == 0 && live && r.sg.g_base;
+    SgdPre4 pre{};
+    if (upd) pre = sgd_pre4(r.sg, o);
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    if (live) {
+#pragma unroll 8
+      for (int z = q; z < r.S; z += DEEP_Q) acc += *reinterpret_cast<const f32x4*>(p + z * r.stride);
+    }
+    part[q * DEEP_COLS + c] = acc;
+    __syncthreads();
+    if (q == 0 && live) {
+      f32x4 t = part[c];
+#pragma unroll 8
+      for (int k = 1; k < DEEP_Q; ++k) t += part[k * DEEP_COLS + c];
+      if (upd) {
+        const f32x4 pn = sgd_apply4(r.sg, pre, t);
+        if (r.pkf || r.pkd) rb_pack_store4(r.pkf, r.pkd, (int)m, (int)n, r.M, r.N, pn);
+      } else {
+        *reinterpret_cast<f32x4*>(o) = t;
+      }
+    }
+    return;
+  }
+  float* ps = reinterpret_cast<float*>(part);
+  if (b < nb_main + nb_bias) {
+    const long long m = (long long)(b - nb_main) * DEEP_COLS + c;
+    float acc = 0.f;
+    if (m < r.M) {
+#pragma unroll 8
+      for (int z = q; z < r.S; z += DEEP_Q) acc += r.bws[z * r.bstride + m];
+    }
+    ps[q * DEEP_COLS + c] = acc;
+    __syncthreads();
+    if (q == 0 && m < r.M) {
+      float t = ps[c];
+#pragma unroll 8
+      for (int k = 1; k < DEEP_Q; ++k) t += ps[k * DEEP_COLS + c];
+      if (r.sg.g_base) sgd_fused_store(r.sg, r.bout + m, t);
+      else r.bout[m] = t;
+    }
+    return;
+  }
+  // loss partials: the same fixed-order form as slab_reduce_block's
+  const int lane = threadIdx.x & 63, w = threadIdx.x >> 6;
+  float acc = 0.f;
+  for (int i = threadIdx.x; i < r.n_loss_part; i += SLAB_THREADS) acc += r.loss_part[i];
+  acc = wave_sum(acc);
+  if (lane == 0) ps[w] = acc;
+  __syncthreads();
+  if (threadIdx.x == 0) {
+    float t = 0.f;
+    for (int k = 0; k < SLAB_NW; ++k) t += ps[k];
+    *r.loss_out = t * r.loss_scale;
+  }
+}
+
 constexpr int SLAB_PART_BYTES = 16 * 64 * 16;   // max(WS, NW) x 64 lanes x f32x4
 
 template <int WS>
 __global__ void __launch_bounds__(SLAB_THREADS) slab_reduce_kernel(SlabReduce r, int nb_main, int nb_bias) {
   __shared__ f32x4 part[SLAB_PART_BYTES / 16];
-  slab_reduce_block<WS>(r, blockIdx.x, nb_main, nb_bias, part);
+  if constexpr (WS == SLAB_DEEP) slab_reduce_deep_block(r, blockIdx.x, nb_main, nb_bias, part);
+  else slab_reduce_block<WS>(r, blockIdx.x, nb_main, nb_bias, part);
 }
 
 __device__ __forceinline__ void slab_reduce_any(int ws, const SlabReduce& r, int b, int nb_main,
@@ -165,7 +240,8 @@ __device__ __forceinline__ void slab_reduce_any(int ws, const SlabReduce& r, int
     case 2: slab_reduce_block<2>(r, b, nb_main, nb_bias, part); break;
     case 4: slab_reduce_block<4>(r, b, nb_main, nb_bias, part); break;
     case 8: slab_reduce_block<8>(r, b, nb_main, nb_bias, part); break;
-    default: slab_reduce_block<16>(r, b, nb_main, nb_bias, part); break;
+    case 16: slab_reduce_block<16>(r, b, nb_main, nb_bias, part); break;
+    default: slab_reduce_deep_block(r, b, nb_main, nb_bias, part); break;
   }
 }
 
@@ -559,13 +635,17 @@ hipError_t gemm_bf16_generic(const bf16* A, int lda, int la, const bf16* B, int 
 }
 
 static int slab_ws(const SlabReduce& r) {
+  // more than 64 partials: the deep 16-column form
+  if (r.S > 64) return SLAB_DEEP;
   // ~8 independent loads per lane: WS = S / 8 rounded up to a power of two, in [1, 16]
   int ws = 1;
   while (ws < 16 && ws * 8 < r.S) ws *= 2;
   return ws;
 }
 
-static int slab_cols(int ws) { return ws >= SLAB_NW ? 64 : 64 * (SLAB_NW / ws); }
+static int slab_cols(int ws) {
+  return ws == SLAB_DEEP ? DEEP_COLS : ws >= SLAB_NW ? 64 : 64 * (SLAB_NW / ws);
+}
 
 static void slab_blocks(const SlabReduce& r, int& nb_main, int& nb_bias, int& nb) {
   const int cols = slab_cols(slab_ws(r));
@@ -587,7 +667,8 @@ hipError_t slab_reduce(const SlabReduce& r0, hipStream_t s) {
     case 2: hipLaunchKernelGGL(slab_reduce_kernel<2>, g, t, 0, s, r, nb_main, nb_bias); break;
     case 4: hipLaunchKernelGGL(slab_reduce_kernel<4>, g, t, 0, s, r, nb_main, nb_bias); break;
     case 8: hipLaunchKernelGGL(slab_reduce_kernel<8>, g, t, 0, s, r, nb_main, nb_bias); break;
-    default: hipLaunchKernelGGL(slab_reduce_kernel<16>, g, t, 0, s, r, nb_main, nb_bias); break;
+    case 16: hipLaunchKernelGGL(slab_reduce_kernel<16>, g, t, 0, s, r, nb_main, nb_bias); break;
+    default: hipLaunchKernelGGL(slab_reduce_kernel<SLAB_DEEP>, g, t, 0, s, r, nb_main, nb_bias); break;
   }
   return hipGetLastError();
 }

@@ -226,6 +226,16 @@ hipError_t head_fused(const void* a, int a_bf16, int rows, int in, const float* 
                       float* gb, float* ws, float* loss_part, float loss_scale, float* loss_out,
                       hipStream_t s, const SgdFuse* sgd = nullptr, SlabReduce* pending = nullptr);
 size_t head_wgrad_workspace_bytes(int rows, int in, int out);
+// Multi-output head (1 < out <= 16, in 512 / 1024, bf16) with its weight gradient in one
+// kernel + the deferred/immediate combine (head.hip head_mo_fused_kernel)
+bool head_mo_fused_ok(int a_bf16, int rows, int in, int out, int loss);
+void set_head_fused(int on);   // 0: two launches (A/B), 1: fused, -1: environment
+size_t head_mo_workspace_bytes(int rows, int in, int out);
+hipError_t head_mo_fused(const bf16* a, int rows, int in, const float* W, const float* b, int out,
+                         const float* y, const int64_t* labels, int loss, float inv_count,
+                         int act_prev, void* dz_prev, float* gW, float* gb, float* ws,
+                         float* loss_part, float loss_scale, float* loss_out, hipStream_t s,
+                         const SgdFuse* sgd = nullptr, SlabReduce* pending = nullptr);
 // General head on the matrix cores (head.hip): bf16 activations, in % 256 == 0, out <= 128
 bool head_general_mfma_ok(int a_bf16, int in, int out);
 void set_head_general_valu(int on);   // 1: the VALU general head for bf16 heads too (A/B)

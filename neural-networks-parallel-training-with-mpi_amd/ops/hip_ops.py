@@ -139,7 +139,25 @@ class HipOps:
             return int(self.lib.head_general_workspace_bytes(max(rows, 1), in_f, out_f))
         _, off = self._head_split(rows, in_f, out_f)
         return max(int(self.lib.head_wgrad_workspace_bytes(rows, in_f, out_f)),
-                   int(self.lib.head_fused_workspace_bytes(rows, in_f))) + 4 * off
+                   int(self.lib.head_fused_workspace_bytes(rows, in_f)),
+                   int(self.lib.head_mo_workspace_bytes(rows, in_f, out_f))) + 4 * off
+
+    def _head_mo(self, a, W, b, y, labels, loss, inv_count, act_prev, dz_out, gW, gb, loss_out,
+                 loss_scale, ws, sgd, deferred):
+        """Multi-output head with its weight gradient in one kernel (head.hip
+        head_mo_fused_kernel); None when the shape is not one it takes."""
+        rows, in_f = a.shape
+        out_f = W.shape[0]
+        if a.dtype != torch.bfloat16 or not self.lib.head_mo_fused_ok(1, rows, in_f, out_f,
+                                                                      LOSS_CODES[loss]):
+            return None
+        _check(a.is_contiguous() and (dz_out is None or dz_out.is_contiguous()),
+               "fused head needs contiguous activations")
+        parts, off = self._head_split(rows, in_f, out_f)
+        return self.lib.head_mo_fused(_p(a), rows, in_f, _p(W), _p(b), out_f, _p(y), _p(labels),
+                                      LOSS_CODES[loss], float(inv_count), ACT_CODES[act_prev],
+                                      _p(dz_out), _p(gW), _p(gb), _p(ws[off:]), _p(ws[:parts]),
+                                      float(loss_scale), _p(loss_out), self.stream, sgd, deferred)
 
     def head_can_fuse_sgd(self, out_f, in_f, loss) -> bool:
         # both skinny head forms end in a slab combine that can apply the update: the fused
@@ -168,6 +186,9 @@ class HipOps:
         lp = ws[:parts]
         wws = ws[off:]
         a_bf16 = 1 if a.dtype == torch.bfloat16 else 0
+        if self._head_mo(a, W, b, y, labels, loss, inv_count, act_prev, dz_out, gW, gb, loss_out,
+                         loss_scale, ws, sgd, False) is not None:
+            return
         if self.lib.head_can_fuse(out_f, in_f, LOSS_CODES[loss]):
             # regression head: fwd + loss + dZ + wgrad partials in one kernel, then one reduce
             self.lib.head_fused(_p(a), a_bf16, rows, in_f, _p(W), _p(b), _p(y), float(inv_count),
@@ -197,6 +218,10 @@ class HipOps:
                                                 float(inv_count), ACT_CODES[act_prev], _p(dz_out),
                                                 _p(gW), _p(gb), _p(ws[off:]), _p(ws[:parts]),
                                                 float(loss_scale), _p(loss_out), self.stream, sgd)
+        r = self._head_mo(a, W, b, y, labels, loss, inv_count, act_prev, dz_out, gW, gb, loss_out,
+                          loss_scale, ws, sgd, True)
+        if r is not None:
+            return r
         _check(dlogits is not None, "multi-output head needs a dlogits buffer")
         self.lib.head_fwd(_p(a), a_bf16, rows, in_f, _p(W), _p(b), out_f, _p(y), _p(labels),
                           LOSS_CODES[loss], float(inv_count), ACT_CODES[act_prev], _p(dz_out),
