@@ -796,7 +796,22 @@ struct WgradMultiParams {
   int nj;
 };
 
-template <int GA>
+// NS: LDS stages of the DMA ring.  The launch holds about one block per CU (3 jobs x 16 tiles x 5
+// splits = 240 blocks on the proxy step), so no second block hides a k-step's DMA wait: with 2
+// stages a block keeps ONE 32 KiB stage in flight and runs at the L2 round trip, not the per-CU
+// feed (25.5 us for 3 x 512 x 512 x 8192).  4 stages (128 KiB) keep three in flight.
+constexpr int WGM_NS = 4;
+constexpr int WGM_SMEM = WGM_NS * (GRP_BM + GRP_BN) * GEMM_BK * 2;
+static int g_wgm_ns = -1;   // NNMPI_WG_STAGES=2: the 2-stage ring (A/B)
+static int wgm_stages() {
+  if (g_wgm_ns < 0) {
+    const char* e = knob_env("NNMPI_WG_STAGES");
+    g_wgm_ns = (e && e[0] == '2') ? 2 : WGM_NS;
+  }
+  return g_wgm_ns;
+}
+
+template <int GA, int NS>
 __global__ void __launch_bounds__(GRP_THREADS, 4) wgrad_multi_kernel(WgradMultiParams g) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   int bid = blockIdx.x;
@@ -807,7 +822,7 @@ __global__ void __launch_bounds__(GRP_THREADS, 4) wgrad_multi_kernel(WgradMultiP
       const int l = xcd_remap(bid, g.blocks[j]);
       if (l >= g.n[j]) return;
       const int split = l / g.tiles[j], t = l % g.tiles[j];
-      dma_gemm_tile<GRP_BM, GRP_BN, GRP_WGM, GRP_WGN, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, GRP_NS, GA>(
+      dma_gemm_tile<GRP_BM, GRP_BN, GRP_WGM, GRP_WGN, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, NS, GA>(
           g.wg[j], smem, t % g.gx[j], t / g.gx[j], split);
       return;
     }
@@ -857,14 +872,18 @@ hipError_t wgrad_multi(const WgradArgs* jobs, int nj, const int* splits, SlabRed
     nb += g.blocks[j];
   }
   const int ga = g_group_async >= 0 ? std::min(g_group_async, 2) : GROUP_ASYNC_DEFAULT;
+  const int si = wgm_stages() == 2 ? 0 : 1;
   using Fn = void (*)(WgradMultiParams);
-  static const Fn fns[3] = {wgrad_multi_kernel<0>, wgrad_multi_kernel<1>, wgrad_multi_kernel<2>};
-  static bool attr[3] = {};
-  if (!attr[ga]) {
-    (void)hipFuncSetAttribute((const void*)fns[ga], hipFuncAttributeMaxDynamicSharedMemorySize, GRP_SMEM);
-    attr[ga] = true;
+  static const Fn fns[2][3] = {
+      {wgrad_multi_kernel<0, 2>, wgrad_multi_kernel<1, 2>, wgrad_multi_kernel<2, 2>},
+      {wgrad_multi_kernel<0, WGM_NS>, wgrad_multi_kernel<1, WGM_NS>, wgrad_multi_kernel<2, WGM_NS>}};
+  static bool attr[2][3] = {};
+  const int smem = si ? WGM_SMEM : GRP_SMEM;
+  if (!attr[si][ga]) {
+    (void)hipFuncSetAttribute((const void*)fns[si][ga], hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+    attr[si][ga] = true;
   }
-  hipLaunchKernelGGL(fns[ga], dim3(nb), dim3(GRP_THREADS), GRP_SMEM, s, g);
+  hipLaunchKernelGGL(fns[si][ga], dim3(nb), dim3(GRP_THREADS), smem, s, g);
   return hipGetLastError();
 }
 
