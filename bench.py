@@ -371,7 +371,8 @@ def run(a, job):
         """One arena + gradient-sync strategy + engine over ``data`` (a shard()).
         mode: inline | overlap | overlap_rowband | zero1 | none (no gradient synchronisation);
         chunk_tiles: 256x256 tiles per output-row chunk bucket at least (0: the default);
-        bf16_reduce: the bf16-payload all-reduce algorithm (acc32 | rccl; None: the default)."""
+        bf16_reduce: the all-reduce algorithm, "rccl" for RCCL's own ring / tree (None: the
+        default -- acc32 for a bf16 payload, ordered for an fp32 one)."""
         part, X, Y, labels = data
         rows = part.rows(rank)
         model = reference_init(widths, "relu", seed=0, device=dev if (big and gpu) else None)
@@ -392,8 +393,11 @@ def run(a, job):
             if zero1:
                 sync = ShardedSync(arena, world, rank, native_comm=native_comm)
             else:
+                bf16 = grad_dtype == "bf16"
                 sync = NativeRcclSync(arena, native_comm, world, inline=(mode == "inline"),
-                                      grad_dtype=grad_dtype, bf16_reduce=bf16_reduce)
+                                      grad_dtype=grad_dtype,
+                                      bf16_reduce=bf16_reduce if bf16 else None,
+                                      f32_reduce=None if bf16 else bf16_reduce)
         else:
             dist.broadcast(arena.master, src=0, group=comm_group)
             arena.sync_shadow()
@@ -543,9 +547,10 @@ def run(a, job):
 
         for key, m, bmb, ct in cands:
             try_cand(key, m, bmb, ct)
-        if grad_dtype == "bf16" and native_comm is not None and best[1] != "zero1":
-            # the bf16 all-reduce algorithm is tuned too, under the chosen schedule: the
-            # one-rounding all-to-all (acc32, the default) vs RCCL's own ring / tree algorithms
+        if native_comm is not None and best[1] != "zero1":
+            # the all-reduce algorithm is tuned too, under the chosen schedule: the all-to-all
+            # with the owner's rank-order sum (bf16: acc32, one rounding; fp32: ordered -- the
+            # defaults) vs RCCL's own ring / tree algorithms
             key, m, bmb, ct = best
             try_cand(f"{key}+rccl", m, bmb, ct, red="rccl")
         if gpu:
@@ -721,6 +726,9 @@ def run(a, job):
                        "bf16_reduce": ((bf16_reduce or eng.sync.bf16_reduce)
                                        if use_comm and grad_dtype == "bf16"
                                        and hasattr(eng.sync, "bf16_reduce") else None),
+                       "f32_reduce": ((bf16_reduce or eng.sync.f32_reduce)
+                                      if use_comm and grad_dtype != "bf16"
+                                      and hasattr(eng.sync, "f32_reduce") else None),
                        "grad_wire_bytes_per_rank": wire,
                        "bucket_mb": bucket_mb,
                        "n_buckets": n_buckets},

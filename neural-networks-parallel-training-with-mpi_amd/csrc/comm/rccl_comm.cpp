@@ -158,6 +158,31 @@ void RcclComm::allreduce_bf16_acc32(void* buf, void* scratch, size_t count, hipS
   NCCL_THROW(ncclGroupEnd());
 }
 
+void RcclComm::allreduce_f32_ordered(void* buf, void* scratch, size_t count, hipStream_t s) {
+  if (nranks_ == 1) return;
+  const size_t c = acc32_slice(count);
+  auto off = [&](int r) { return std::min(count, (size_t)r * c); };
+  auto cnt = [&](int r) { return std::min(count, (size_t)(r + 1) * c) - off(r); };
+  float* b = static_cast<float*>(buf);
+  float* sc = static_cast<float*>(scratch);
+  NCCL_THROW(ncclGroupStart());
+  for (int q = 0; q < nranks_; ++q) {
+    if (q == rank_) continue;
+    if (cnt(q) > 0) NCCL_THROW(ncclSend(b + off(q), cnt(q), ncclFloat32, q, comm_, s));
+    if (cnt(rank_) > 0) NCCL_THROW(ncclRecv(sc + (size_t)q * c, cnt(rank_), ncclFloat32, q, comm_, s));
+  }
+  NCCL_THROW(ncclGroupEnd());
+  if (cnt(rank_) > 0)
+    HIP_THROW(sum_slices_f32(b + off(rank_), sc, nranks_, rank_, (long long)c, (long long)cnt(rank_), s));
+  NCCL_THROW(ncclGroupStart());
+  for (int q = 0; q < nranks_; ++q) {
+    if (q == rank_) continue;
+    if (cnt(rank_) > 0) NCCL_THROW(ncclSend(b + off(rank_), cnt(rank_), ncclFloat32, q, comm_, s));
+    if (cnt(q) > 0) NCCL_THROW(ncclRecv(b + off(q), cnt(q), ncclFloat32, q, comm_, s));
+  }
+  NCCL_THROW(ncclGroupEnd());
+}
+
 int RcclComm::poll_error(bool abort_on_error) {
   if (aborted_) return (int)ncclInvalidUsage;
   ncclResult_t r = ncclSuccess;
@@ -214,6 +239,8 @@ void GradSync::bucket_ready(int b, void* ptr, size_t count, int dtype, hipStream
   HIP_THROW(hipStreamWaitEvent(comm_stream_, ready_[b], 0));
   if (dtype == 1 && acc32_scratch_)
     comm_->allreduce_bf16_acc32(ptr, acc32_scratch_, count, comm_stream_);
+  else if (dtype == 0 && f32_scratch_)
+    comm_->allreduce_f32_ordered(ptr, f32_scratch_, count, comm_stream_);
   else
     comm_->allreduce(ptr, count, dtype, 0, comm_stream_);
   if (standin_blocks_ > 0 && standin_gbps_ > 0.0) {

@@ -57,6 +57,11 @@ class RcclComm {
   // with P -- and every transfer takes the direct xGMI link between the two GPUs.
   void allreduce_bf16_acc32(void* buf, void* scratch, size_t count, hipStream_t s);
   size_t acc32_slice(size_t count) const;
+  // fp32 all-reduce with a fixed per-element summation order (rank 0 + 1 + ... + P-1, on the
+  // element's owner): the same all-to-all / owner sum / all-gather as the bf16 form, no rounding
+  // step.  Bitwise independent of how a gradient is cut into buckets.  scratch: at least
+  // acc32_scratch_elems(count) floats.
+  void allreduce_f32_ordered(void* buf, void* scratch, size_t count, hipStream_t s);
   size_t acc32_scratch_elems(size_t count) const { return acc32_slice(count) * nranks_; }
   // Returns the RCCL async error code (0 = ok); aborts the communicator on error if asked.
   int poll_error(bool abort_on_error);
@@ -77,6 +82,8 @@ class GradSync {
   void bucket_ready(int b, void* ptr, size_t count, int dtype, hipStream_t compute);
   // bf16 buckets use RcclComm::allreduce_bf16_acc32 with this scratch (nullptr: ncclAllReduce)
   void set_acc32_scratch(void* scratch) { acc32_scratch_ = scratch; }
+  // fp32 buckets use RcclComm::allreduce_f32_ordered with this scratch (nullptr: ncclAllReduce)
+  void set_f32_scratch(void* scratch) { f32_scratch_ = scratch; }
   // diagnostic: after each bucket's collective, hold `blocks` CUs on the comm stream for the
   // time the bucket would take at `gbps` bus bandwidth (kernels.h cu_hold; 0 blocks: off)
   void set_standin(int blocks, double gbps) { standin_blocks_ = blocks; standin_gbps_ = gbps; }
@@ -87,6 +94,7 @@ class GradSync {
  private:
   RcclComm* comm_;
   void* acc32_scratch_ = nullptr;
+  void* f32_scratch_ = nullptr;
   int standin_blocks_ = 0;
   double standin_gbps_ = 0.0;
   hipStream_t comm_stream_ = nullptr;

@@ -101,15 +101,43 @@ __device__ __forceinline__ void slab_reduce_block(const SlabReduce& r, int b, in
       part[(cg * WS + vw) * 64 + lane] = acc;
     }
     __syncthreads();
+    // The transposed weight image (pkd) wants 8 consecutive ROWS per 16 B; a lane holds 4
+    // consecutive columns of one row.  When the block's columns are R whole rows (R = 2 / 4 / 8),
+    // the new values go through LDS (after the partials: [R][N] bf16) and every thread stores
+    // one R x 2-byte run per column, instead of 4 scattered 2-byte stores per lane.
+    const int R = (SS::COLS * 4) / N;
+    const bool pk_lds = r.pkd && r.sg.g_base && WS < SLAB_NW && (R == 2 || R == 4 || R == 8) &&
+                        R * N == SS::COLS * 4 && N <= 2 * SLAB_THREADS;
+    bf16* stash = reinterpret_cast<bf16*>(part + SLAB_NW * 64);
     if (combiner && v < nvec) {
       f32x4 t = part[cg * WS * 64 + lane];
 #pragma unroll
       for (int k = 1; k < WS; ++k) t += part[(cg * WS + k) * 64 + lane];
       if (r.sg.g_base) {
         const f32x4 pn = upd ? sgd_apply4(r.sg, pre, t) : sgd_fused_store4(r.sg, o, t);
-        if (r.pkf || r.pkd) rb_pack_store4(r.pkf, r.pkd, (int)m, (int)n, r.M, r.N, pn);
+        if (r.pkf || (r.pkd && !pk_lds)) rb_pack_store4(r.pkf, pk_lds ? nullptr : r.pkd, (int)m, (int)n, r.M, r.N, pn);
+        if (pk_lds) {
+          bf16x4 h;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) h[e] = (bf16)pn[e];
+          *reinterpret_cast<bf16x4*>(stash + (m % R) * N + n) = h;
+        }
       } else {
         *reinterpret_cast<f32x4*>(o) = t;
+      }
+    }
+    if (pk_lds) {
+      __syncthreads();
+      const long long m0 = (long long)b * SS::COLS * 4 / N;
+      for (int c = threadIdx.x; c < N; c += SLAB_THREADS) {
+        if (m0 >= r.M) break;
+        bf16 col[8];
+#pragma unroll
+        for (int rr = 0; rr < 8; ++rr) col[rr] = rr < R ? stash[rr * N + c] : (bf16)0.f;
+        bf16* d = r.pkd + rb_pk_off(c, (int)m0, r.M);
+        if (R == 8) *reinterpret_cast<bf16x8*>(d) = bf16x8{col[0], col[1], col[2], col[3], col[4], col[5], col[6], col[7]};
+        else if (R == 4) *reinterpret_cast<bf16x4*>(d) = bf16x4{col[0], col[1], col[2], col[3]};
+        else *reinterpret_cast<bf16x2*>(d) = bf16x2{col[0], col[1]};
       }
     }
     return;

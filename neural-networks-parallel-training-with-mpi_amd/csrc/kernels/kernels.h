@@ -319,6 +319,9 @@ hipError_t checksum_f32(const float* x, long long n, double* out, hipStream_t s)
 // for j < n, accumulated in fp32 (the owner step of RcclComm::allreduce_bf16_acc32)
 hipError_t sum_slices_bf16(bf16* out, const bf16* scratch, int P, int me, long long stride,
                            long long n, hipStream_t s);
+// fp32 twin (RcclComm::allreduce_f32_ordered): out[j] = sum_q (q == me ? out : scratch[q])[j]
+hipError_t sum_slices_f32(float* out, const float* scratch, int P, int me, long long stride,
+                          long long n, hipStream_t s);
 // diagnostic: `blocks` 256-thread blocks holding their CUs (and a full wave's VGPRs) for
 // `seconds` of wall time, then exiting (standin.hip; the collective stand-in)
 hipError_t cu_hold(int blocks, double seconds, hipStream_t s);

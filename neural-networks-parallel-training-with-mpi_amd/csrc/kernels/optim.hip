@@ -240,6 +240,40 @@ hipError_t sum_slices_bf16(bf16* out, const bf16* scratch, int P, int me, long l
   return hipGetLastError();
 }
 
+// Owner step of the ordered fp32 all-reduce (rccl_comm.cpp allreduce_f32_ordered): the P fp32
+// copies of a slice summed in rank order, so an element's sum does not depend on where it sits
+// in the buffer (a ring's order does: at P >= 3 two bucketings of one gradient differ in bits).
+__global__ void __launch_bounds__(256) sum_slices_f32_kernel(float* __restrict__ out,
+                                                             const float* __restrict__ sc, int P,
+                                                             int me, long long stride, long long n) {
+  const long long t0 = (long long)blockIdx.x * blockDim.x + threadIdx.x;
+  const long long step = (long long)gridDim.x * blockDim.x;
+  const bool vec = ((((uintptr_t)out) | ((uintptr_t)sc)) & 15) == 0 && (stride % 4) == 0;
+  const long long n4 = vec ? n / 4 : 0;
+  for (long long i = t0; i < n4; i += step) {
+    f32x4 acc = {0.f, 0.f, 0.f, 0.f};
+    for (int q = 0; q < P; ++q) {
+      const float* src = (q == me) ? out : sc + (long long)q * stride;
+      acc += reinterpret_cast<const f32x4*>(src)[i];
+    }
+    reinterpret_cast<f32x4*>(out)[i] = acc;
+  }
+  for (long long j = n4 * 4 + t0; j < n; j += step) {
+    float acc = 0.f;
+    for (int q = 0; q < P; ++q) acc += (q == me) ? out[j] : sc[(long long)q * stride + j];
+    out[j] = acc;
+  }
+}
+
+hipError_t sum_slices_f32(float* out, const float* scratch, int P, int me, long long stride,
+                          long long n, hipStream_t s) {
+  if (P < 1 || me < 0 || me >= P || n < 0 || stride < n) return hipErrorInvalidValue;
+  if (n == 0) return hipSuccess;
+  hipLaunchKernelGGL(sum_slices_f32_kernel, dim3(grid_for((n + 3) / 4)), dim3(256), 0, s, out,
+                     scratch, P, me, stride, n);
+  return hipGetLastError();
+}
+
 // Bitwise replica hash: sum over i of mix64((i << 32) | word_i) mod 2^64 (splitmix64 finaliser).
 // A value sum (checksum_f32) can coincide for different bits (-0.0 vs 0.0, compensating
 // errors); this one changes with any flipped bit of any word, and integer addition makes the

@@ -201,13 +201,20 @@ class NativeRcclSync(GradSync):
     faster than overlap; large volumes use the overlapped comm stream."""
 
     def __init__(self, arena, native_comm, world: int, priority: int = -1, inline: bool = False,
-                 grad_dtype: str = "fp32", mode: str = "allreduce", bf16_reduce: str = ""):
+                 grad_dtype: str = "fp32", mode: str = "allreduce", bf16_reduce: str = "",
+                 f32_reduce: str = ""):
         """``bf16_reduce`` (bf16 payload): ``acc32`` (default) sums the P bf16 copies of every
         element in fp32 on its owner and rounds ONCE (all-to-all + owner sum + all-gather,
         RcclComm::allreduce_bf16_acc32) -- the result is bf16(sum_r bf16(g_r)) whatever P is,
         the same contract as the CPU path's round / fp32-sum / round; ``rccl`` is ncclAllReduce
         in bf16, whose ring rounds the partial sum at every one of its P-1 hops (the error
-        grows with P: tests/test_multirank_gpu.py::test_rccl_bf16_reduction_error_vs_p)."""
+        grows with P: tests/test_multirank_gpu.py::test_rccl_bf16_reduction_error_vs_p).
+        ``f32_reduce`` (fp32 payload): ``ordered`` (default) is the same all-to-all / owner sum
+        / all-gather in fp32 (RcclComm::allreduce_f32_ordered): every element is summed in rank
+        order wherever it sits in a bucket, so two schedules that cut the gradient into
+        different buckets (inline vs overlap_rowband) agree bit for bit at any P -- a ring's
+        order depends on the element's chunk, which differs between bucketings at P >= 3;
+        ``rccl`` is ncclAllReduce."""
         super().__init__(arena)
         self.mode = mode
         # the root pattern is a serial reduce + broadcast: always on the compute stream
@@ -234,6 +241,9 @@ class NativeRcclSync(GradSync):
         self.bf16_reduce = bf16_reduce or knob("NNMPI_BF16_REDUCE", "acc32")
         if self.bf16_reduce not in ("acc32", "rccl"):
             raise ValueError(f"bf16_reduce must be acc32 or rccl, not {self.bf16_reduce!r}")
+        self.f32_reduce = f32_reduce or knob("NNMPI_F32_REDUCE", "ordered")
+        if self.f32_reduce not in ("ordered", "rccl"):
+            raise ValueError(f"f32_reduce must be ordered or rccl, not {self.f32_reduce!r}")
         # collective stand-in (measurement only): "k:gbps" holds k CUs on the comm stream after
         # each bucket's collective for its bytes at gbps (csrc/kernels/standin.hip)
         st = knob("NNMPI_COMM_STANDIN", "")
@@ -247,10 +257,18 @@ class NativeRcclSync(GradSync):
             self.scratch = torch.empty(max(1, native_comm.acc32_scratch_elems(n)),
                                        dtype=torch.bfloat16, device=arena.grad.device)
             self.gs.set_acc32_scratch(self.scratch.data_ptr())
+        self.scratch32 = None
+        if not self.bf16 and self.f32_reduce == "ordered" and mode != "root" and world > 1:
+            n = max(b.numel for b in arena.buckets)
+            self.scratch32 = torch.empty(max(1, native_comm.acc32_scratch_elems(n)),
+                                         dtype=torch.float32, device=arena.grad.device)
+            self.gs.set_f32_scratch(self.scratch32.data_ptr())
 
     def _allreduce(self, ptr: int, n: int, dt: int, h: int):
         if dt == 1 and self.scratch is not None:
             self.comm.allreduce_bf16_acc32(ptr, self.scratch.data_ptr(), n, h)
+        elif dt == 0 and self.scratch32 is not None:
+            self.comm.allreduce_f32_ordered(ptr, self.scratch32.data_ptr(), n, h)
         else:
             self.comm.allreduce(ptr, n, dt, 0, h)
 

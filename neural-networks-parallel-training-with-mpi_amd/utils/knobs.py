@@ -27,6 +27,7 @@ KNOBS = {
     "NNMPI_DEFER_WAIT": "deferred update waits per chunk / per layer",
     "NNMPI_CHUNK_MIN_TILES": "tiles per output-row chunk bucket",
     "NNMPI_BF16_REDUCE": "bf16 all-reduce algorithm (acc32 | rccl)",
+    "NNMPI_F32_REDUCE": "fp32 all-reduce algorithm (ordered | rccl)",
     "NNMPI_SHM": "shared-memory all-reduce of CPU ranks (0: gloo)",
     "NNMPI_CPU_NATIVE": "native host step of tiny CPU models (0: PyTorch)",
     "NNMPI_STAGE_EPI": "LDS-staged 256x256 forward epilogue",

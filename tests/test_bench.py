@@ -139,9 +139,14 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
               "--tune_steps", "4"], timeout=300)
     d = _line(r)
     assert d["n_gpus"] == 2 and d["rccl_ranks"] == 2 and d["shared_gpu_rehearsal"]
-    assert d["config"]["comm"] == "rccl" and d["config"]["comm_mode"] in ("inline", "zero1",
-                                                                         "overlap")
-    assert {"inline", "zero1", "overlap"} <= set(d["config"]["comm_tune_ms_per_step"])
+    mode = d["config"]["comm_mode"]
+    assert d["config"]["comm"] == "rccl" and mode.split("+")[0] in ("inline", "zero1", "overlap",
+                                                                   "overlap_rowband")
+    t = d["config"]["comm_tune_ms_per_step"]
+    assert {"inline", "zero1", "overlap", "overlap_rowband"} <= set(t)
+    # fp32 payload: the ordered all-to-all (default) and RCCL's ring, both timed, one recorded
+    assert d["config"]["grad_dtype"] == "fp32" and len([k for k in t if k.endswith("+rccl")]) == 1
+    assert d["config"]["f32_reduce"] == ("rccl" if mode.endswith("+rccl") else "ordered")
     assert d["parallel_efficiency"] is not None and d["comm_bus_gbps"] is not None
     assert d["strong_scaling"]["global_batch"] == 8192
     assert d["final_loss"] == d["final_loss"]

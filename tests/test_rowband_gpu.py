@@ -149,6 +149,34 @@ def test_rowband_fused_update_is_bitwise_equal_to_separate_pass(monkeypatch):
     assert res[0][3] == res[1][3]
 
 
+@pytest.mark.parametrize("widths", [[512, 512, 512, 512, 1], [256, 256, 256, 1],
+                                    [768, 1024, 1024, 1], [384, 384, 384, 1]])
+def test_rowband_fused_update_writes_the_weight_images(widths, monkeypatch):
+    """The combines that apply the update also rewrite the v2 weight images (the forward image
+    directly, the transposed dgrad image staged through LDS where a block holds whole rows):
+    after a few steps they equal a fresh pack of the new bf16 weights, bit for bit."""
+    from nnmpi_amd.ops.hip_ops import HipOps
+    rows = 8192
+    X, Y = _data(rows, widths)
+    ops = HipOps("cuda")
+    _, ar, eng = _engine(widths, rows, "cuda", ops, lr=1e-3, momentum=0.9, fuse_sgd=True,
+                         rowband=True, monkeypatch=monkeypatch)
+    assert eng.rowband and eng.rb_version == 2
+    eng.load_batch(X, Y)
+    eng.set_scales(1.0 / rows, 1.0 / rows, 1.0)
+    for _ in range(3):
+        eng.step()
+    eng.synchronize()
+    nh = len(widths) - 2
+    buf, fresh = ops.rowband_packed(widths[1], widths[0], nh, "cuda")
+    ops.rowband_pack([ar.compute_weight(i) for i in range(nh)], fresh)
+    torch.cuda.synchronize()
+    for l, ((pf, pd), (qf, qd)) in enumerate(zip(eng.rb_packed, fresh)):
+        assert torch.equal(pf, qf), f"forward image of layer {l}"
+        if pd is not None:
+            assert torch.equal(pd, qd), f"dgrad image of layer {l}"
+
+
 def test_rowband_graph_replay_is_bitwise_equal_to_eager(monkeypatch):
     from nnmpi_amd.engine.arena import Arena
     from nnmpi_amd.engine.engine import MLPEngine
