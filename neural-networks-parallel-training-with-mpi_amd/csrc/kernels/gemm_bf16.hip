@@ -825,16 +825,18 @@ struct WgradMultiParams {
 };
 
 // NS: LDS stages of the DMA ring.  The launch holds about one block per CU (3 jobs x 16 tiles x 5
-// splits = 240 blocks on the proxy step), so no second block hides a k-step's DMA wait: with 2
-// stages a block keeps ONE 32 KiB stage in flight and runs at the L2 round trip, not the per-CU
-// feed (25.5 us for 3 x 512 x 512 x 8192).  4 stages (128 KiB) keep three in flight.
+// splits = 240 blocks on the proxy step), so no second block hides a k-step's DMA wait; a
+// 4-stage ring (128 KiB, three stages in flight) was built to test whether the L2 round trip
+// bounds it: measured equal (proxy step 0.0737 / 0.0739 / 0.0749 ms with 4 stages vs 0.0733 /
+// 0.0731 / 0.0742 with 2, wgrad_multi 26.2 us either way: profiles/r4_wgrad_multi_stages_ab.txt),
+// so the default stays 2 (NNMPI_WG_STAGES=4 selects the deep ring).
 constexpr int WGM_NS = 4;
 constexpr int WGM_SMEM = WGM_NS * (GRP_BM + GRP_BN) * GEMM_BK * 2;
-static int g_wgm_ns = -1;   // NNMPI_WG_STAGES=2: the 2-stage ring (A/B)
+static int g_wgm_ns = -1;
 static int wgm_stages() {
   if (g_wgm_ns < 0) {
     const char* e = knob_env("NNMPI_WG_STAGES");
-    g_wgm_ns = (e && e[0] == '2') ? 2 : WGM_NS;
+    g_wgm_ns = (e && e[0] == '4') ? WGM_NS : 2;
   }
   return g_wgm_ns;
 }

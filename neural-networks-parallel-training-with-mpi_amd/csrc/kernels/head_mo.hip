@@ -4,46 +4,96 @@
 #include "knobs.h"
 
 #include <algorithm>
-#include <type_traits>
 
 namespace nnmpi {
 
 // ------------------------------------------------------------------------------------------
 // Fused multi-output head (MNIST shape: cross-entropy / multi-target MSE, 1 < out <= 16,
-// in = 512 / 1024, bf16 activations): head_mfma_kernel's logits, loss and dZ_prev AND the
-// head's weight gradient in ONE pass (the separate head_wgrad_mfma launch re-read the 16 MB of
-// activations: 16.2 + 7.2 us of the MNIST step, profiles/r3s2_final_kstats_mnist.csv).
+// in = 512 / 1024, bf16 activations): logits, loss, dZ_prev AND the head's weight gradient in
+// ONE pass over the activations, every product on the bf16 matrix cores
+// (v_mfma_f32_16x16x32_bf16, 1/8 the issue cycles of the fp32 v_mfma_f32_16x16x4_f32 per FLOP).
+// The two launches it replaces (head_mfma_kernel + head_wgrad_mfma_kernel, fp32 MFMA) took
+// 16.2 + 7.2 us of the MNIST step (profiles/r3s2_final_kstats_mnist.csv).
 //
-// 512-thread blocks = 2 teams of 4 waves; SIMD s holds wave s of both teams.  Per iteration the
-// two teams take two consecutive 16-row groups.  A team runs its group the head_mfma_kernel way
-// (wave w = feature quarter; two independent 32-step logits chains, the partial tiles summed
-// through LDS in wave order; softmax / MSE in registers; dZ_prev on MFMA) and publishes the
-// group's dlogits (16 x 16 fp32) in LDS.  Then the weight gradient of BOTH groups is split by
-// columns instead of rows: wave (t, w) accumulates gW[:, its quarter's t-th column half] over the
-// 32 rows as v_mfma_f32_16x16x4_f32 products (exact fp32, K = 4 rows per step; A = dl[row][o =
-// l&15] from LDS, B = a[row][c0 + 8(l&15) + tile] re-loaded from global: an L1/L2 hit, the
-// team has just read these rows) -- head_wgrad_mfma's operand map.  Every gW element thus has
-// ONE owner wave summing all of the block's rows in a fixed order: no team combine, and the
-// accumulators are half a quarter wide (32 VGPRs at in = 1024).  The block writes one partial
-// slab gW [out][in], gb [out] and its loss for the deterministic reducer (slab_reduce's deep
-// form: 256 slabs).
+// Precision (the fp32 reference's products, to the bits that matter):
+//   logits  = a . (W_hi + W_lo)^T   W split into two bf16 terms (16 significant bits), a is bf16:
+//             every product exact in fp32, fp32 accumulation -> logits to ~2^-16 relative;
+//   dZ_prev = (bf16(dl) . W_hi) * act'(a), stored as bf16 -- the rounding of every hidden layer's
+//             dgrad GEMM (bf16 operands, fp32 accumulation), inside test_head's bound;
+//   gW      = (dl_hi + dl_lo)^T . a, gb = sum dl (fp32) -- dl split like W: ~2^-16 relative.
+//
+// Block: 512 threads = 2 teams x 4 waves; each iteration the teams take two consecutive 16-row
+// groups.  Wave (t, w) owns feature quarter w of its team's group for the logits (B operand =
+// its 16-byte activation loads, lane (row l&15, 8 features)) and dZ; the partial logit tiles
+// are summed through LDS in wave order.  The weight gradient needs K = rows: the two groups'
+// activations are staged through LDS as a [32 rows][512 columns] image read back transposed
+// (ds_read_b64_tr_b16), one 512-column phase at a time, and every wave owns 4 column tiles of a
+// phase -- each gW element has one owner summing the block's rows in a fixed order.  LDS:
+// W_hi / W_lo [16][in + 8] bf16 (padded rows: conflict-free 16-byte reads), W_hi^T [in][16],
+// the a stage, logit partials, dlogits: 141 KB at in = 1024.  The block writes ONE partial slab
+// gW [out][in], gb [out] and its loss for the deterministic reducer (slab_reduce's deep form).
 // ------------------------------------------------------------------------------------------
 constexpr int MF_TEAMS = 2, MF_WAVES = 4 * MF_TEAMS;
+constexpr int MF_PH = 512;   // columns per weight-gradient phase
+
+template <int IN>
+struct MfLds {
+  static constexpr int WROW = IN + 8;                       // padded W_hi / W_lo row (bf16)
+  static constexpr int WHI = 0;
+  static constexpr int WLO = WHI + 16 * WROW * 2;
+  static constexpr int WT = WLO + 16 * WROW * 2;            // [IN][16] bf16
+  static constexpr int STAGE = WT + IN * 16 * 2;            // [32][MF_PH] bf16, swizzled
+  static constexpr int PART = STAGE + 32 * MF_PH * 2;       // [waves][64] f32x4
+  static constexpr int DLB = PART + MF_WAVES * 64 * 16;     // [team][16 rows][16 outs] fp32
+  static constexpr int SUMS = DLB + MF_TEAMS * 256 * 4;     // loss [team]
+  static constexpr int BYTES = SUMS + 64;
+};
+
+// W_hi^T image: row f (16 outputs, 32 B) stored at row f ^ (bit 3 of f -> bit 2) with its two
+// 16-byte halves swapped when bit 4 of f is set: the 16 lanes of a dZ A-operand read (rows
+// f0 + 8(m >> 2) + 4h + (m & 3), one half) then hit 16 distinct 16-byte slots of a 256-byte bank
+// row (plain 32-byte rows: 4-way conflicts)
+__device__ __forceinline__ int mf_wt_off(int f, int half) {
+  return (f ^ (((f >> 3) & 1) << 2)) * 16 + ((half ^ ((f >> 4) & 1)) << 3);
+}
+
+// a-stage image: row k (0..31) of MF_PH bf16, 16-byte chunk c of row k at c ^ swz(k)
+__device__ __forceinline__ int mf_stage_off(int k, int x) {
+  const int swz = ((k & 3) | ((k >> 1) & 4)) << 1;
+  return k * (MF_PH * 2) + ((((x >> 3) ^ swz)) << 4) + ((x & 7) << 1);
+}
+
+// B operand (k = row 8(l>>4) + j, n = column xb + (l&15)) of the staged activations
+__device__ __forceinline__ bf16x8 mf_stage_frag(const char* stage, int xb, int lane) {
+  const int q = (lane & 15) >> 2, p = lane & 3;
+  const int k = 8 * (lane >> 4) + q;
+  const int x = xb + 4 * p;
+  const s16x4 lo = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(stage + mf_stage_off(k, x)));
+  const s16x4 hi = __builtin_amdgcn_ds_read_tr16_b64_v4i16((lds_s16x4*)(stage + mf_stage_off(k + 4, x)));
+  typedef __attribute__((ext_vector_type(8))) short s16x8;
+  s16x8 v = {lo[0], lo[1], lo[2], lo[3], hi[0], hi[1], hi[2], hi[3]};
+  return __builtin_bit_cast(bf16x8, v);
+}
 
 template <int ACT, int LOSS, int Q>
 __global__ void __launch_bounds__(64 * MF_WAVES) head_mo_fused_kernel(HeadArgs p,
                                                                       float* __restrict__ gws,
                                                                       float* __restrict__ gwsb) {
-  extern __shared__ __attribute__((aligned(16))) float ml[];   // W image | partials | dl | sums
+  extern __shared__ __attribute__((aligned(16))) char smem[];
   constexpr int in = 4 * Q;
-  // a wave's weight-gradient columns: NT tiles of 16 x 16, column of (tile tt, lane row r) =
-  // c0 + 8r + tt0 + tt; B loads of NT bf16 per lane and row
-  constexpr int NT = Q == 256 ? 8 : 4;
+  using L = MfLds<in>;
+  constexpr int NPH = in / MF_PH;           // weight-gradient phases
+  constexpr int QPP = MF_PH / Q;            // feature quarters per phase
+  bf16* whi = reinterpret_cast<bf16*>(smem + L::WHI);
+  bf16* wlo = reinterpret_cast<bf16*>(smem + L::WLO);
+  bf16* wt = reinterpret_cast<bf16*>(smem + L::WT);
+  char* stage = smem + L::STAGE;
+  f32x4* part_all = reinterpret_cast<f32x4*>(smem + L::PART);
+  float* dlb = reinterpret_cast<float*>(smem + L::DLB);
+  float* sums = reinterpret_cast<float*>(smem + L::SUMS);
   const int tid = threadIdx.x, lane = tid & 63;
   const int wv = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int team = wv >> 2, w = wv & 3;
-  const int c0 = Q == 256 ? w * Q + team * 128 : w * Q;
-  const int tt0 = Q == 256 ? 0 : 4 * team;
   const int out = p.out;
   const bf16* A = reinterpret_cast<const bf16*>(p.a);
   bf16* DZ = reinterpret_cast<bf16*>(p.dz_prev);
@@ -54,49 +104,76 @@ __global__ void __launch_bounds__(64 * MF_WAVES) head_mo_fused_kernel(HeadArgs p
   const int per = (ngroups + (int)gridDim.x - 1) / (int)gridDim.x;
   const int g_beg = xcd_remap(blockIdx.x, gridDim.x) * per;
   const int g_end = min(ngroups, g_beg + per);
-  // W image: 16-byte loads, all issued before the first LDS store
+  // the first row group's activations and labels: independent of the W images, so their loads
+  // are issued first and fly during the image build
+  MhLoads<Q> cur, nxt;
+  mh_load<Q, LOSS>(cur, p, A, min((g_beg + team) * 16 + r, p.rows - 1), w, g);
+  // ---- W images: W = W_hi + W_lo (bf16 each) and W_hi^T.  Every load first: 16-byte rows for
+  // W_hi / W_lo, and for W_hi^T one 16-output column per thread and feature (the row-major pass
+  // cannot store the transpose: 2-byte stores 32 B apart put 64 lanes on two banks)
   constexpr int NV = 16 * in / 4 / (64 * MF_WAVES);
+  constexpr int NC = in / (64 * MF_WAVES);   // W^T rows per thread
   f32x4 wimg[NV];
+  float wcol[NC][16];
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int i4 = j * 64 * MF_WAVES + tid, n = i4 / (in / 4), k = (i4 % (in / 4)) * 4;
     wimg[j] = n < out ? *reinterpret_cast<const f32x4*>(p.W + n * in + k) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
 #pragma unroll
+  for (int c = 0; c < NC; ++c)
+#pragma unroll
+    for (int n = 0; n < 16; ++n) wcol[c][n] = n < out ? p.W[n * in + c * 64 * MF_WAVES + tid] : 0.f;
+#pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int i4 = j * 64 * MF_WAVES + tid, n = i4 / (in / 4), k = (i4 % (in / 4)) * 4;
-    *reinterpret_cast<f32x4*>(ml + mh_off(n, k, in)) = wimg[j];
+    bf16x4 h, l;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) {
+      h[e] = (bf16)wimg[j][e];
+      l[e] = (bf16)(wimg[j][e] - (float)h[e]);
+    }
+    *reinterpret_cast<bf16x4*>(whi + n * L::WROW + k) = h;
+    *reinterpret_cast<bf16x4*>(wlo + n * L::WROW + k) = l;
   }
-  f32x4* part = reinterpret_cast<f32x4*>(ml + 16 * in) + team * 4 * 64;   // [team][wave][lane]
-  float* dlb = ml + 16 * in + MF_WAVES * 64 * 4;                          // [team][row][out]
-  float* sums = dlb + MF_TEAMS * 256;                                     // loss [team]
+#pragma unroll
+  for (int c = 0; c < NC; ++c) {
+    const int kk = c * 64 * MF_WAVES + tid;
+    bf16x8 t0, t1;
+#pragma unroll
+    for (int n = 0; n < 8; ++n) {
+      t0[n] = (bf16)wcol[c][n];
+      t1[n] = (bf16)wcol[c][n + 8];
+    }
+    *reinterpret_cast<bf16x8*>(wt + mf_wt_off(kk, 0)) = t0;
+    *reinterpret_cast<bf16x8*>(wt + mf_wt_off(kk, 1)) = t1;
+  }
+  f32x4* part = part_all + team * 4 * 64;
   __syncthreads();
   float bias[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) bias[j] = (4 * g + j) < out ? p.b[4 * g + j] : 0.f;
-  f32x4 gacc[NT];
+  f32x4 gacc[NPH][4];
 #pragma unroll
-  for (int t = 0; t < NT; ++t) gacc[t] = f32x4{0.f, 0.f, 0.f, 0.f};
+  for (int ph = 0; ph < NPH; ++ph)
+#pragma unroll
+    for (int t = 0; t < 4; ++t) gacc[ph][t] = f32x4{0.f, 0.f, 0.f, 0.f};
   float bsum = 0.f, block_loss = 0.f;
+  const bf16x8 zero8 = {};
   for (int base = g_beg; base < g_end; base += MF_TEAMS) {
     const int grp = base + team;
     const int row = grp * 16 + r;
     const bool valid = grp < g_end && row < p.rows;
-    MhLoads<Q> cur;
-    mh_load<Q, LOSS>(cur, p, A, min(row, p.rows - 1), w, g);
     const bf16x8* xs = cur.xs;
-    // ---- logits: this wave's quarter, two independent chains ----
+    // ---- logits: this wave's quarter, W_hi and W_lo terms in two chains ----
     f32x4 acc0 = {0.f, 0.f, 0.f, 0.f}, acc1 = {0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int c = 0; c < Q / 32; ++c) {
       const int k = w * Q + c * 32 + g * 8;
-      const bf16x8 xv = xs[c];
-      const f32x4 w0 = *reinterpret_cast<const f32x4*>(ml + mh_off(r, k, in));
-      const f32x4 w1 = *reinterpret_cast<const f32x4*>(ml + mh_off(r, k + 4, in));
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc0 = __builtin_amdgcn_mfma_f32_16x16x4f32(w0[e], (float)xv[e], acc0, 0, 0, 0);
-#pragma unroll
-      for (int e = 0; e < 4; ++e) acc1 = __builtin_amdgcn_mfma_f32_16x16x4f32(w1[e], (float)xv[e + 4], acc1, 0, 0, 0);
+      const bf16x8 wh = *reinterpret_cast<const bf16x8*>(whi + r * L::WROW + k);
+      const bf16x8 wl = *reinterpret_cast<const bf16x8*>(wlo + r * L::WROW + k);
+      acc0 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wh, xs[c], acc0, 0, 0, 0);
+      acc1 = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wl, xs[c], acc1, 0, 0, 0);
     }
     part[w * 64 + lane] = acc0 + acc1;
     __syncthreads();
@@ -148,77 +225,86 @@ __global__ void __launch_bounds__(64 * MF_WAVES) head_mo_fused_kernel(HeadArgs p
       if (valid && g == 0) block_loss += row_loss;
       *reinterpret_cast<f32x4*>(dlb + team * 256 + r * 16 + 4 * g) = f32x4{dl[0], dl[1], dl[2], dl[3]};
     }
-    // ---- dZ_prev for this wave's quarter (head_mfma_kernel's tile pairs) ----
+    __syncthreads();   // both groups' dlogits published
+    // ---- dZ_prev for this wave's quarter: K = outputs (16, zero-padded to 32) ----
     if (DZ != nullptr) {
-      float bfr[4];
+      bf16x8 bdl = zero8;   // B operand: dl[row r][outputs 8g .. 8g+7] in bf16
+      if (g < 2) {
+        const f32x4 d0 = *reinterpret_cast<const f32x4*>(dlb + team * 256 + r * 16 + 8 * g);
+        const f32x4 d1 = *reinterpret_cast<const f32x4*>(dlb + team * 256 + r * 16 + 8 * g + 4);
 #pragma unroll
-      for (int st = 0; st < 4; ++st) {
-        const int src = st * 16 + r;
-        const float t0 = __shfl(dl[0], src, 64), t1 = __shfl(dl[1], src, 64);
-        const float t2 = __shfl(dl[2], src, 64), t3 = __shfl(dl[3], src, 64);
-        bfr[st] = g == 0 ? t0 : g == 1 ? t1 : g == 2 ? t2 : t3;
+        for (int e = 0; e < 4; ++e) { bdl[e] = (bf16)d0[e]; bdl[e + 4] = (bf16)d1[e]; }
       }
 #pragma unroll
       for (int tp = 0; tp < Q / 32; ++tp) {
         const int f0 = w * Q + tp * 32;
-        const int kf = f0 + 8 * (r >> 2) + (r & 3);
         const bf16x8 av = xs[tp];
-        f32x4 d0 = {0.f, 0.f, 0.f, 0.f}, d1 = {0.f, 0.f, 0.f, 0.f};
+        f32x4 d[2];
 #pragma unroll
-        for (int st = 0; st < 4; ++st) {
-          d0 = __builtin_amdgcn_mfma_f32_16x16x4f32(ml[mh_off(4 * st + g, kf, in)], bfr[st], d0, 0, 0, 0);
-          d1 = __builtin_amdgcn_mfma_f32_16x16x4f32(ml[mh_off(4 * st + g, kf + 4, in)], bfr[st], d1, 0, 0, 0);
+        for (int h = 0; h < 2; ++h) {
+          // A row m = lane & 15 of tile half h is feature f0 + 8(m >> 2) + 4h + (m & 3): the
+          // lane's two accumulators are features f0 + 8g .. +7 of its row (one 16-byte store)
+          const int f = f0 + 8 * (r >> 2) + 4 * h + (r & 3);
+          const bf16x8 wa = g < 2 ? *reinterpret_cast<const bf16x8*>(wt + mf_wt_off(f, g)) : zero8;
+          d[h] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(wa, bdl, f32x4{0.f, 0.f, 0.f, 0.f}, 0, 0, 0);
         }
         if (valid) {
           bf16x8 o;
 #pragma unroll
           for (int j = 0; j < 4; ++j) {
-            o[j] = (bf16)(d0[j] * act_bwd_t<ACT>((float)av[j]));
-            o[j + 4] = (bf16)(d1[j] * act_bwd_t<ACT>((float)av[j + 4]));
+            o[j] = (bf16)(d[0][j] * act_bwd_t<ACT>((float)av[j]));
+            o[j + 4] = (bf16)(d[1][j] * act_bwd_t<ACT>((float)av[j + 4]));
           }
           *reinterpret_cast<bf16x8*>(DZ + (long long)row * in + f0 + 8 * g) = o;
         }
       }
     }
-    // the weight-gradient operand of both groups (rows 4s + g, NT features per lane), issued
-    // after the dZ work (xs dead: no register overlap) so the loads fly across the barrier
-    using BV = typename std::conditional<NT == 8, bf16x8, bf16x4>::type;
-    BV xb[MF_TEAMS][4];
+    // the next iteration's activations (xs stays live for the stage writes below)
+    const bool more = base + MF_TEAMS < g_end;
+    if (more) mh_load<Q, LOSS>(nxt, p, A, min((base + MF_TEAMS + team) * 16 + r, p.rows - 1), w, g);
+    // ---- weight gradient: A = dl[rows 8g .. 8g+7 of the 32][o = r] as hi + lo ----
+    bf16x8 ahi, alo;
 #pragma unroll
-    for (int gg = 0; gg < MF_TEAMS; ++gg)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const int rr = min((base + gg) * 16 + 4 * s + g, p.rows - 1);
-        xb[gg][s] = *reinterpret_cast<const BV*>(A + (long long)rr * in + c0 + 8 * r + tt0);
-      }
-    __syncthreads();   // both groups' dlogits published
-    // ---- gW[:, this wave's columns] += dl^T a over the 32 rows, 4 rows per step ----
-#pragma unroll
-    for (int gg = 0; gg < MF_TEAMS; ++gg)
-#pragma unroll
-      for (int s = 0; s < 4; ++s) {
-        const float dv = dlb[gg * 256 + (4 * s + g) * 16 + r];   // dl[row 4s + g][o = r]
-        if (wv == 0) bsum += dv;
-#pragma unroll
-        for (int t = 0; t < NT; ++t)
-          gacc[t] = __builtin_amdgcn_mfma_f32_16x16x4f32(dv, (float)xb[gg][s][t], gacc[t], 0, 0, 0);
-      }
-    __syncthreads();   // the partial and dl buffers are rewritten by the next iteration
-  }
-  // ---- block partials: every gW element has one owner lane ----
-#pragma unroll
-  for (int i = 0; i < 4; ++i) {
-    const int o = 4 * g + i;
-    if (o < out) {
-      float* dst = gws + ((long long)blockIdx.x * out + o) * in + c0 + 8 * r + tt0;
-      if constexpr (NT == 8) {
-        *reinterpret_cast<f32x4*>(dst) = f32x4{gacc[0][i], gacc[1][i], gacc[2][i], gacc[3][i]};
-        *reinterpret_cast<f32x4*>(dst + 4) = f32x4{gacc[4][i], gacc[5][i], gacc[6][i], gacc[7][i]};
-      } else {
-        *reinterpret_cast<f32x4*>(dst) = f32x4{gacc[0][i], gacc[1][i], gacc[2][i], gacc[3][i]};
-      }
+    for (int e = 0; e < 8; ++e) {
+      const int k = 8 * g + e;   // block row 0..31: group k >> 4, row k & 15
+      const float v = dlb[(k >> 4) * 256 + (k & 15) * 16 + r];
+      if (wv == 0) bsum += v;
+      ahi[e] = (bf16)v;
+      alo[e] = (bf16)(v - (float)ahi[e]);
     }
+#pragma unroll
+    for (int ph = 0; ph < NPH; ++ph) {
+      // stage the two groups' activations of this phase's columns (the waves whose quarter
+      // lies in it): row k = 16 t + r, columns of xs[c]
+      if (w / QPP == ph) {
+#pragma unroll
+        for (int c = 0; c < Q / 32; ++c) {
+          const int x = (w % QPP) * Q + c * 32 + 8 * g;
+          *reinterpret_cast<bf16x8*>(stage + mf_stage_off(team * 16 + r, x)) = xs[c];
+        }
+      }
+      __syncthreads();
+#pragma unroll
+      for (int t = 0; t < 4; ++t) {
+        const bf16x8 bv = mf_stage_frag(stage, (wv * 4 + t) * 16, lane);
+        gacc[ph][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ahi, bv, gacc[ph][t], 0, 0, 0);
+        gacc[ph][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bv, gacc[ph][t], 0, 0, 0);
+      }
+      __syncthreads();   // the stage / partial / dl buffers are rewritten next
+    }
+    if (more) cur = nxt;
   }
+  // ---- block partials: every gW element has one owner lane (o = 4g + i, column l & 15) ----
+#pragma unroll
+  for (int ph = 0; ph < NPH; ++ph)
+#pragma unroll
+    for (int t = 0; t < 4; ++t)
+#pragma unroll
+      for (int i = 0; i < 4; ++i) {
+        const int o = 4 * g + i;
+        if (o < out)
+          gws[((long long)blockIdx.x * out + o) * in + ph * MF_PH + (wv * 4 + t) * 16 + r] = gacc[ph][t][i];
+      }
   bsum += __shfl_xor(bsum, 16, 64);
   bsum += __shfl_xor(bsum, 32, 64);
   if (w == 0) {
@@ -256,7 +342,7 @@ size_t head_mo_workspace_bytes(int rows, int in, int out) {
 template <int Q>
 static hipError_t head_mo_launch_q(const HeadArgs& h, int act, int loss, int blocks, float* gws,
                                    float* gwsb, hipStream_t s) {
-  const size_t smem = (size_t)(16 * h.in + MF_WAVES * 64 * 4 + MF_TEAMS * 256 + 16) * sizeof(float);
+  const size_t smem = (size_t)MfLds<4 * Q>::BYTES;
   using Fn = void (*)(HeadArgs, float*, float*);
   static const Fn fns[2][3] = {
       {head_mo_fused_kernel<ACT_NONE, LOSS_MSE, Q>, head_mo_fused_kernel<ACT_RELU, LOSS_MSE, Q>, head_mo_fused_kernel<ACT_TANH, LOSS_MSE, Q>},

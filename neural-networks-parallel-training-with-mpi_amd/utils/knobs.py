@@ -38,7 +38,7 @@ KNOBS = {
     "NNMPI_GRAPH_UPLOAD": "hipGraphUpload after instantiation (0 off)",
     "NNMPI_PAIR": "wide backward pair launches (experiments build)",
     "NNMPI_COMM_STANDIN": "k:gbps -- k CUs held after every bucket collective (standin.hip)",
-    "NNMPI_WG_STAGES": "grouped weight-gradient launch DMA ring stages (2; default 4)",
+    "NNMPI_WG_STAGES": "grouped weight-gradient launch DMA ring stages (default 2; 4)",
     "NNMPI_HEAD_FUSED": "multi-output head + weight gradient in one kernel (0: two launches)",
 }
 
