@@ -568,6 +568,9 @@ def run(a, job):
     eng.prepare_steps(a.steps, chunk)
     # the step schedule the timed engine runs (rowband.hip / grouped backward / sequential)
     step_schedule = eng.schedule_name()
+    # the all-reduce algorithm the timed engine uses (recorded before the extras free it)
+    sync_algo = {"bf16": getattr(eng.sync, "bf16_reduce", None),
+                 "fp32": getattr(eng.sync, "f32_reduce", None)}
     loss0 = eng.loss()
     milestone("timed")
     barrier()
@@ -723,12 +726,10 @@ def run(a, job):
                        "comm_mode": mode_name if use_comm else None,
                        "comm_tune_ms_per_step": tune,
                        "grad_dtype": grad_dtype if use_comm else None,
-                       "bf16_reduce": ((bf16_reduce or eng.sync.bf16_reduce)
-                                       if use_comm and grad_dtype == "bf16"
-                                       and hasattr(eng.sync, "bf16_reduce") else None),
-                       "f32_reduce": ((bf16_reduce or eng.sync.f32_reduce)
-                                      if use_comm and grad_dtype != "bf16"
-                                      and hasattr(eng.sync, "f32_reduce") else None),
+                       "bf16_reduce": (sync_algo["bf16"] if use_comm and grad_dtype == "bf16"
+                                       else None),
+                       "f32_reduce": (sync_algo["fp32"] if use_comm and grad_dtype != "bf16"
+                                      else None),
                        "grad_wire_bytes_per_rank": wire,
                        "bucket_mb": bucket_mb,
                        "n_buckets": n_buckets},
