@@ -78,8 +78,15 @@ __device__ __forceinline__ bf16x8 mf_stage_frag(const char* stage, int xb, int l
 template <int ACT, int LOSS, int Q>
 __global__ void __launch_bounds__(64 * MF_WAVES) head_mo_fused_kernel(HeadArgs p,
                                                                       float* __restrict__ gws,
-                                                                      float* __restrict__ gwsb) {
+                                                                      float* __restrict__ gwsb,
+                                                                      unsigned long long* st) {
   extern __shared__ __attribute__((aligned(16))) char smem[];
+  // diagnostic phase stamps (st != null: scripts/r4_head_stamps.py): 100 MHz real-time counter
+  // at 8 points of the first iteration, written by thread 0
+  const auto stamp = [&](int i) {
+    if (st && threadIdx.x == 0) st[blockIdx.x * 8 + i] = __builtin_amdgcn_s_memrealtime();
+  };
+  stamp(0);
   constexpr int in = 4 * Q;
   using L = MfLds<in>;
   constexpr int NPH = in / MF_PH;           // weight-gradient phases
@@ -108,22 +115,17 @@ __global__ void __launch_bounds__(64 * MF_WAVES) head_mo_fused_kernel(HeadArgs p
   // are issued first and fly during the image build
   MhLoads<Q> cur, nxt;
   mh_load<Q, LOSS>(cur, p, A, min((g_beg + team) * 16 + r, p.rows - 1), w, g);
-  // ---- W images: W = W_hi + W_lo (bf16 each) and W_hi^T.  Every load first: 16-byte rows for
-  // W_hi / W_lo, and for W_hi^T one 16-output column per thread and feature (the row-major pass
-  // cannot store the transpose: 2-byte stores 32 B apart put 64 lanes on two banks)
+  // ---- W images: W = W_hi + W_lo (bf16 each) from 16-byte row loads; W_hi^T from W_hi in LDS
+  // after a barrier (a second, column-wise read of W from L2 by all 256 blocks cost ~4 us; a
+  // 2-byte transpose store from the row pass puts 64 lanes on two banks)
   constexpr int NV = 16 * in / 4 / (64 * MF_WAVES);
   constexpr int NC = in / (64 * MF_WAVES);   // W^T rows per thread
   f32x4 wimg[NV];
-  float wcol[NC][16];
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int i4 = j * 64 * MF_WAVES + tid, n = i4 / (in / 4), k = (i4 % (in / 4)) * 4;
     wimg[j] = n < out ? *reinterpret_cast<const f32x4*>(p.W + n * in + k) : f32x4{0.f, 0.f, 0.f, 0.f};
   }
-#pragma unroll
-  for (int c = 0; c < NC; ++c)
-#pragma unroll
-    for (int n = 0; n < 16; ++n) wcol[c][n] = n < out ? p.W[n * in + c * 64 * MF_WAVES + tid] : 0.f;
 #pragma unroll
   for (int j = 0; j < NV; ++j) {
     const int i4 = j * 64 * MF_WAVES + tid, n = i4 / (in / 4), k = (i4 % (in / 4)) * 4;
@@ -136,20 +138,22 @@ __global__ void __launch_bounds__(64 * MF_WAVES) head_mo_fused_kernel(HeadArgs p
     *reinterpret_cast<bf16x4*>(whi + n * L::WROW + k) = h;
     *reinterpret_cast<bf16x4*>(wlo + n * L::WROW + k) = l;
   }
+  __syncthreads();
 #pragma unroll
   for (int c = 0; c < NC; ++c) {
     const int kk = c * 64 * MF_WAVES + tid;
     bf16x8 t0, t1;
 #pragma unroll
     for (int n = 0; n < 8; ++n) {
-      t0[n] = (bf16)wcol[c][n];
-      t1[n] = (bf16)wcol[c][n + 8];
+      t0[n] = whi[n * L::WROW + kk];
+      t1[n] = whi[(n + 8) * L::WROW + kk];
     }
     *reinterpret_cast<bf16x8*>(wt + mf_wt_off(kk, 0)) = t0;
     *reinterpret_cast<bf16x8*>(wt + mf_wt_off(kk, 1)) = t1;
   }
   f32x4* part = part_all + team * 4 * 64;
   __syncthreads();
+  stamp(1);
   float bias[4];
 #pragma unroll
   for (int j = 0; j < 4; ++j) bias[j] = (4 * g + j) < out ? p.b[4 * g + j] : 0.f;
@@ -177,6 +181,7 @@ __global__ void __launch_bounds__(64 * MF_WAVES) head_mo_fused_kernel(HeadArgs p
     }
     part[w * 64 + lane] = acc0 + acc1;
     __syncthreads();
+    if (base == g_beg) stamp(2);
     f32x4 z = part[lane];
 #pragma unroll
     for (int ww = 1; ww < 4; ++ww) z += part[ww * 64 + lane];
@@ -226,6 +231,7 @@ __global__ void __launch_bounds__(64 * MF_WAVES) head_mo_fused_kernel(HeadArgs p
       *reinterpret_cast<f32x4*>(dlb + team * 256 + r * 16 + 4 * g) = f32x4{dl[0], dl[1], dl[2], dl[3]};
     }
     __syncthreads();   // both groups' dlogits published
+    if (base == g_beg) stamp(3);
     // ---- dZ_prev for this wave's quarter: K = outputs (16, zero-padded to 32) ----
     if (DZ != nullptr) {
       bf16x8 bdl = zero8;   // B operand: dl[row r][outputs 8g .. 8g+7] in bf16
@@ -259,6 +265,7 @@ __global__ void __launch_bounds__(64 * MF_WAVES) head_mo_fused_kernel(HeadArgs p
         }
       }
     }
+    if (base == g_beg) stamp(4);
     // the next iteration's activations (xs stays live for the stage writes below)
     const bool more = base + MF_TEAMS < g_end;
     if (more) mh_load<Q, LOSS>(nxt, p, A, min((base + MF_TEAMS + team) * 16 + r, p.rows - 1), w, g);
@@ -291,6 +298,7 @@ __global__ void __launch_bounds__(64 * MF_WAVES) head_mo_fused_kernel(HeadArgs p
         gacc[ph][t] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(alo, bv, gacc[ph][t], 0, 0, 0);
       }
       __syncthreads();   // the stage / partial / dl buffers are rewritten next
+      if (base == g_beg) stamp(5 + ph);
     }
     if (more) cur = nxt;
   }
@@ -314,6 +322,7 @@ __global__ void __launch_bounds__(64 * MF_WAVES) head_mo_fused_kernel(HeadArgs p
   if (wv == 0 && g == 0 && r < out) gwsb[(long long)blockIdx.x * out + r] = bsum;
   __syncthreads();
   if (tid == 0) p.loss_part[blockIdx.x] = sums[0] + sums[1];
+  stamp(7);
 }
 
 static int g_head_fused_mo = -1;   // NNMPI_HEAD_FUSED=0: separate head + head_wgrad launches (A/B)
@@ -341,9 +350,9 @@ size_t head_mo_workspace_bytes(int rows, int in, int out) {
 
 template <int Q>
 static hipError_t head_mo_launch_q(const HeadArgs& h, int act, int loss, int blocks, float* gws,
-                                   float* gwsb, hipStream_t s) {
+                                   float* gwsb, unsigned long long* st, hipStream_t s) {
   const size_t smem = (size_t)MfLds<4 * Q>::BYTES;
-  using Fn = void (*)(HeadArgs, float*, float*);
+  using Fn = void (*)(HeadArgs, float*, float*, unsigned long long*);
   static const Fn fns[2][3] = {
       {head_mo_fused_kernel<ACT_NONE, LOSS_MSE, Q>, head_mo_fused_kernel<ACT_RELU, LOSS_MSE, Q>, head_mo_fused_kernel<ACT_TANH, LOSS_MSE, Q>},
       {head_mo_fused_kernel<ACT_NONE, LOSS_XENT, Q>, head_mo_fused_kernel<ACT_RELU, LOSS_XENT, Q>, head_mo_fused_kernel<ACT_TANH, LOSS_XENT, Q>}};
@@ -353,7 +362,7 @@ static hipError_t head_mo_launch_q(const HeadArgs& h, int act, int loss, int blo
     (void)hipFuncSetAttribute((const void*)fns[li][ai], hipFuncAttributeMaxDynamicSharedMemorySize, (int)smem);
     attr[li][ai] = true;
   }
-  hipLaunchKernelGGL(fns[li][ai], dim3(blocks), dim3(64 * MF_WAVES), smem, s, h, gws, gwsb);
+  hipLaunchKernelGGL(fns[li][ai], dim3(blocks), dim3(64 * MF_WAVES), smem, s, h, gws, gwsb, st);
   return hipGetLastError();
 }
 
@@ -365,15 +374,15 @@ hipError_t head_mo_fused(const bf16* a, int rows, int in, const float* W, const 
                          const float* y, const int64_t* labels, int loss, float inv_count,
                          int act_prev, void* dz_prev, float* gW, float* gb, float* ws,
                          float* loss_part, float loss_scale, float* loss_out, hipStream_t s,
-                         const SgdFuse* sgd, SlabReduce* pending) {
+                         const SgdFuse* sgd, SlabReduce* pending, unsigned long long* stamps) {
   if (!head_mo_fused_ok(1, rows, in, out, loss)) return hipErrorInvalidValue;
   if ((loss == LOSS_XENT && !labels) || (loss == LOSS_MSE && !y)) return hipErrorInvalidValue;
   const int G = head_mo_blocks(rows);
   float* gws = ws;
   float* gwsb = ws + (size_t)G * out * in;
   HeadArgs h{a, rows, in, W, b, out, y, labels, inv_count, act_prev, dz_prev, nullptr, loss_part, 1};
-  hipError_t e = in == 512 ? head_mo_launch_q<128>(h, act_prev, loss, G, gws, gwsb, s)
-                           : head_mo_launch_q<256>(h, act_prev, loss, G, gws, gwsb, s);
+  hipError_t e = in == 512 ? head_mo_launch_q<128>(h, act_prev, loss, G, gws, gwsb, stamps, s)
+                           : head_mo_launch_q<256>(h, act_prev, loss, G, gws, gwsb, stamps, s);
   if (e != hipSuccess) return e;
   SlabReduce r{gws, G, (long long)out * in, out, in, gW, in, gwsb, out, gb, loss_part, G, loss_scale,
                loss_out, SgdFuse{}};

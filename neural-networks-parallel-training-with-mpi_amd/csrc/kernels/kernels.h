@@ -235,7 +235,8 @@ hipError_t head_mo_fused(const bf16* a, int rows, int in, const float* W, const 
                          const float* y, const int64_t* labels, int loss, float inv_count,
                          int act_prev, void* dz_prev, float* gW, float* gb, float* ws,
                          float* loss_part, float loss_scale, float* loss_out, hipStream_t s,
-                         const SgdFuse* sgd = nullptr, SlabReduce* pending = nullptr);
+                         const SgdFuse* sgd = nullptr, SlabReduce* pending = nullptr,
+                         unsigned long long* stamps = nullptr);   // stamps: 8 per block (diagnostic)
 // General head on the matrix cores (head.hip): bf16 activations, in % 256 == 0, out <= 128
 bool head_general_mfma_ok(int a_bf16, int in, int out);
 void set_head_general_valu(int on);   // 1: the VALU general head for bf16 heads too (A/B)

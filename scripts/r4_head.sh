@@ -13,6 +13,8 @@ timeout -k 10 600 python -u -m pytest tests/test_kernels_gpu.py -k "head" -x -v 
 rc=$?
 echo "tests rc=$rc"; grep -E "FAILED|ERROR|passed|failed" $O/pytest.log | tail -20 | cut -c1-200
 [ $rc -ne 0 ] && exit $rc
+timeout -k 10 120 python scripts/r4_head_stamps.py > $O/stamps.txt 2>&1 || exit $?
+cat $O/stamps.txt
 for i in 1 2 3; do
   for f in 1 0; do
     NNMPI_EXPERIMENTS=1 NNMPI_HEAD_FUSED=$f timeout -k 10 300 python bench.py --config mnist \

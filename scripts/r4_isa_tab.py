@@ -60,11 +60,12 @@ def parse(path: str, sym: str):
     objdump = any(re.match(r"^[0-9a-f]{16} <", ln) for ln in lines[:2000])
     for ln in lines:
         if objdump:
+            # a listing of exactly the kernel's address range (llvm-objdump --start/--stop-
+            # address): Tensile kernels carry local label_* symbols, which are branch targets
             m = re.match(r"^[0-9a-f]{16} <(.+)>:", ln)
             if m:
-                if inside:
-                    break
-                inside = sym in m.group(1)
+                inside = True
+                labels[m.group(1)] = len(insts)
                 continue
             if not inside:
                 continue
@@ -103,6 +104,11 @@ def loops(insts, labels, objdump):
         idx = {a: i for i, (a, _, _) in enumerate(insts)}
         for i, (a, op, args) in enumerate(insts):
             if op.startswith("s_cbranch") or op == "s_branch":
+                lab = args.split()[0] if args else ""
+                if lab in labels:
+                    if labels[lab] <= i:
+                        out.append((labels[lab], i))
+                    continue
                 try:
                     simm = int(args.split(",")[0].split()[0], 0)
                 except ValueError:
