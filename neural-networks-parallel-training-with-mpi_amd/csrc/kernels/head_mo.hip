@@ -4,6 +4,7 @@
 #include "knobs.h"
 
 #include <algorithm>
+#include <cstdlib>
 
 namespace nnmpi {
 
@@ -335,8 +336,20 @@ static bool head_fused_mo_on() {
   return g_head_fused_mo == 1;
 }
 
+// blocks of the fused head: one 2-group iteration per block up to a cap; the cap trades the
+// partial-slab volume (out x in fp32 per block, written here and read by the combine) and the
+// per-block W image build against parallelism (NNMPI_HEAD_BLOCKS, experiments)
+static int head_mo_cap() {
+  static int cap = -1;
+  if (cap < 0) {
+    const char* e = knob_env("NNMPI_HEAD_BLOCKS");
+    cap = (e && atoi(e) > 0) ? atoi(e) : 256;
+  }
+  return cap;
+}
+
 static int head_mo_blocks(int rows) {
-  return std::max(1, std::min(256, ((rows + 15) / 16 + MF_TEAMS - 1) / MF_TEAMS));
+  return std::max(1, std::min(head_mo_cap(), ((rows + 15) / 16 + MF_TEAMS - 1) / MF_TEAMS));
 }
 
 bool head_mo_fused_ok(int a_bf16, int rows, int in, int out, int loss) {

@@ -214,6 +214,11 @@ class MLPEngine:
         if hasattr(ops, "wgrad_workspace_bytes"):
             for i in range(self.L - 1):
                 need = max(need, ops.wgrad_workspace_bytes(R, w[i + 1], w[i], self.dtype))
+                # an output-row chunk is its own GEMM: fewer tiles than the whole layer, so it
+                # may split K where the layer does not (1024 of 2048 rows at K = 1024: 2 splits)
+                for b in self.arena.chunk_buckets(i):
+                    need = max(need, ops.wgrad_workspace_bytes(R, b.rows[1] - b.rows[0], w[i],
+                                                               self.dtype))
         if hasattr(ops, "head_workspace_bytes"):
             need = max(need, ops.head_workspace_bytes(R, w[-2], w[-1]))
         return need

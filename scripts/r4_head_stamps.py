@@ -30,7 +30,7 @@ ws = torch.zeros(ops.head_workspace_bytes(rows, in_f, out_f) // 4 + 16, device=d
 parts, off = ops._head_split(rows, in_f, out_f)
 st = torch.zeros(256 * 8, dtype=torch.int64, device=dev)
 s = torch.cuda.current_stream().cuda_stream
-names = ["W image", "logits", "loss+dl", "dZ", "wgrad ph0", "wgrad ph1", "tail"]
+names = ["W image", "logits", "loss+dl", "dZ", "wgrad ph0", "wgrad ph1", "rest+tail"]
 per = {n: [] for n in names}
 span = []
 for it in range(12):
@@ -43,15 +43,16 @@ for it in range(12):
     torch.cuda.synchronize()
     if it < 2:
         continue
-    t = st.view(256, 8).cpu().tolist()
+    t = [r for r in st.view(256, 8).cpu().tolist() if r[0] != 0]
     t0 = min(r[0] for r in t)
     span.append((max(r[7] for r in t) - t0) / 100.0)
     for r in t:
         for i, n in enumerate(names):
             per[n].append((r[i + 1] - r[i]) / 100.0)
-print(f"kernel span (first block start -> last block end): median {statistics.median(span):.2f} us")
+print(f"blocks {len(t)} (NNMPI_HEAD_BLOCKS={os.environ.get('NNMPI_HEAD_BLOCKS', '-')}); kernel span "
+      f"(first block start -> last block end): median {statistics.median(span):.2f} us")
 for n in names:
     v = sorted(per[n])
     print(f"  {n:10s} median {statistics.median(v):6.2f} us   p90 {v[int(0.9 * len(v))]:6.2f} us")
-starts = [r[0] for r in st.view(256, 8).cpu().tolist()]
+starts = [r[0] for r in st.view(256, 8).cpu().tolist() if r[0] != 0]
 print(f"block start spread (last run): {(max(starts) - min(starts)) / 100.0:.2f} us")

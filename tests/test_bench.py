@@ -188,7 +188,8 @@ def test_bench_tunes_the_bf16_reduction_algorithm():
     assert len(rccl) == 1 and rccl[0][:-5] in t, t
     assert d["config"]["bf16_reduce"] == ("rccl" if d["config"]["comm_mode"].endswith("+rccl")
                                           else "acc32")
-    assert d["config"]["n_buckets"] > 5          # chunk buckets
+    if d["config"]["comm_mode"].startswith("overlap"):
+        assert d["config"]["n_buckets"] > 5      # chunk buckets (inline replans to one bucket)
     assert d["replicas_bitwise_equal"] is True
 
 
