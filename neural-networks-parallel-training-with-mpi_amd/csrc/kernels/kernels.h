@@ -54,6 +54,9 @@ enum Loss : int { LOSS_MSE = 0, LOSS_XENT = 1 };
 // ---- GEMM (gemm_bf16.hip) ----
 hipError_t linear_fwd_bf16(const bf16* X, int ldx, const bf16* W, int ldw, const float* bias,
                            bf16* Y, int ldy, int M, int N, int K, int act, hipStream_t s);
+// experiment (gemm_w4.hip): the forward on a 4-wave 256 x 256 tile (M, N % 256, K % 64)
+hipError_t gemm_w4_fwd(const bf16* X, int ldx, const bf16* W, int ldw, const float* bias, bf16* Y,
+                       int ldy, int M, int N, int K, int act, hipStream_t s);
 hipError_t linear_dgrad_bf16(const bf16* dZ, int lddz, const bf16* W, int ldw, const bf16* Aprev,
                              int lda_prev, bf16* dX, int lddx, int M, int N, int K, int act,
                              hipStream_t s);
