@@ -833,16 +833,133 @@ struct WgradMultiParams {
 constexpr int WGM_NS = 4;
 constexpr int WGM_SMEM = WGM_NS * (GRP_BM + GRP_BN) * GEMM_BK * 2;
 static int g_wgm_ns = -1;
-static int wgm_stages() {
+static int wgm_stages() {   // 0: register-staged operands (NNMPI_WG_REG=1, A/B)
   if (g_wgm_ns < 0) {
     const char* e = knob_env("NNMPI_WG_STAGES");
-    g_wgm_ns = (e && e[0] == '4') ? WGM_NS : 2;
+    const char* r = knob_env("NNMPI_WG_REG");
+    g_wgm_ns = (r && r[0] == '1') ? 0 : (e && e[0] == '4') ? WGM_NS : 2;
   }
   return g_wgm_ns;
 }
 
+// Register-staged twin of the grouped weight-gradient tile (A/B, NNMPI_WG_REG=1): global ->
+// VGPR -> ds_write with the operands of k-steps t+1 and t+2 in registers while k-step t
+// computes, instead of LDS-DMA.  The row-band step's own weight stream reaches ~67 GB/s per CU
+// through VGPR loads where the DMA ring of this launch moves ~33 (838 KB per block in 25 us).
+// Same MFMA, same operand order, same k order: bitwise the dma_gemm_tile results.
+struct WgRegLoad {   // one XMAJ operand stage: [64 k][128 x] bf16, 2 chunks of 16 B per thread
+  uint4 r[2];
+  __device__ __forceinline__ void load(const bf16* __restrict__ base, int ld, int x0, int X, int k0,
+                                       int kend, int tid) {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int c = tid + it * GRP_THREADS, k = k0 + c / 16, x = x0 + (c % 16) * 8;
+      uint4 v = make_uint4(0u, 0u, 0u, 0u);
+      if (x < X && k < kend) v = *reinterpret_cast<const uint4*>(base + (long long)k * ld + x);
+      r[it] = v;
+    }
+  }
+  __device__ __forceinline__ void store(char* lds, int tid) const {
+#pragma unroll
+    for (int it = 0; it < 2; ++it) {
+      const int c = tid + it * GRP_THREADS, k = c / 16, ch = c % 16;
+      *reinterpret_cast<uint4*>(lds + k * 256 + ((ch ^ swz_x<128>(k)) << 4)) = r[it];
+    }
+  }
+};
+
+__device__ __forceinline__ void wg_reg_tile(const GemmParams& p, char* smem, int tx, int ty, int split) {
+  constexpr int BM = GRP_BM, BN = GRP_BN, BK = GEMM_BK, WGN = GRP_WGN;
+  constexpr int A_BYTES = BM * BK * 2, STAGE = (BM + BN) * BK * 2;
+  constexpr int WM = BM / GRP_WGM, WN = BN / WGN, MI = WM / 16, NJ = WN / 16;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int wm = w / WGN, wn = w % WGN;
+  const int m0 = ty * BM, n0 = tx * BN;
+  const int kbeg = split * p.k_per_split;
+  const int kend = min(p.K, kbeg + p.k_per_split);
+  const int nt = kend > kbeg ? (kend - kbeg + BK - 1) / BK : 0;
+  f32x4 acc[MI][NJ];
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  f32x4 accb[MI];
+#pragma unroll
+  for (int i = 0; i < MI; ++i) accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool do_bg = tx == 0 && wn == 0;
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.0f;
+  WgRegLoad a[2], b[2];   // operands of k-steps t+1 (slot (t+1) & 1) and t+2
+  if (nt > 0) {
+    a[0].load(p.A, p.lda, m0, p.M, kbeg, kend, tid);
+    b[0].load(p.B, p.ldb, n0, p.N, kbeg, kend, tid);
+    a[0].store(smem, tid);
+    b[0].store(smem + A_BYTES, tid);
+    a[1].load(p.A, p.lda, m0, p.M, kbeg + BK, kend, tid);
+    b[1].load(p.B, p.ldb, n0, p.N, kbeg + BK, kend, tid);
+    a[0].load(p.A, p.lda, m0, p.M, kbeg + 2 * BK, kend, tid);
+    b[0].load(p.B, p.ldb, n0, p.N, kbeg + 2 * BK, kend, tid);
+    __syncthreads();
+  }
+  auto step = [&](int t, WgRegLoad& an, WgRegLoad& bn) {
+    const char* cur = smem + (t & 1) * STAGE;
+#pragma unroll
+    for (int kk = 0; kk < BK / 32; ++kk) {
+      bf16x8 af[MI], bfr[NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i) af[i] = read_frag_async<BM, XMAJ>(cur, wm * WM + i * 16, kk, lane);
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) bfr[j] = read_frag_async<BN, XMAJ>(cur + A_BYTES, wn * WN + j * 16, kk, lane);
+      asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+      __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int j = 0; j < NJ; ++j)
+          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
+      if (do_bg) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+          accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[i], accb[i], 0, 0, 0);
+      }
+    }
+    // k-step t+1 into the other stage (last read at step t-1: every wave is past the barrier
+    // that ended it), then its registers take k-step t+3
+    if (t + 1 < nt) {
+      char* nxt = smem + ((t + 1) & 1) * STAGE;
+      an.store(nxt, tid);
+      bn.store(nxt + A_BYTES, tid);
+      an.load(p.A, p.lda, m0, p.M, kbeg + (t + 3) * BK, kend, tid);
+      bn.load(p.B, p.ldb, n0, p.N, kbeg + (t + 3) * BK, kend, tid);
+    }
+    __syncthreads();
+  };
+  for (int t = 0; t < nt; t += 2) {
+    step(t, a[1], b[1]);
+    if (t + 1 < nt) step(t + 1, a[0], b[0]);
+  }
+  if (lepi_ok<EPI_F32>(p)) {
+    lds_epilogue<GRP_WGM, GRP_WGN, EPI_F32, ACT_NONE>(p, acc, smem, m0, n0, wm, wn, w, lane, split);
+    if (do_bg && (lane >> 4) == 0) {
+#pragma unroll
+      for (int i = 0; i < MI; ++i) {
+        const int m = m0 + wm * WM + i * 16 + (lane & 15);
+        if (m >= p.M) continue;
+        float* gb = p.bias_grad + split * p.bg_split_stride + m;
+        if (p.sg.g_base) sgd_fused_store(p.sg, gb, accb[i][0]);
+        else *gb = accb[i][0];
+      }
+    }
+    return;
+  }
+  gemm_epilogue<BM, BN, GRP_WGM, GRP_WGN, EPI_F32, ACT_NONE, true>(p, acc, accb, do_bg, m0, n0, wm, wn,
+                                                                     lane, split, nullptr);
+}
+
 template <int GA, int NS>
-__global__ void __launch_bounds__(GRP_THREADS, 4) wgrad_multi_kernel(WgradMultiParams g) {
+__global__ void __launch_bounds__(GRP_THREADS, NS == 0 ? 2 : 4) wgrad_multi_kernel(WgradMultiParams g) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   int bid = blockIdx.x;
 #pragma unroll
@@ -852,8 +969,11 @@ __global__ void __launch_bounds__(GRP_THREADS, 4) wgrad_multi_kernel(WgradMultiP
       const int l = xcd_remap(bid, g.blocks[j]);
       if (l >= g.n[j]) return;
       const int split = l / g.tiles[j], t = l % g.tiles[j];
-      dma_gemm_tile<GRP_BM, GRP_BN, GRP_WGM, GRP_WGN, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, NS, GA>(
-          g.wg[j], smem, t % g.gx[j], t / g.gx[j], split);
+      if constexpr (NS == 0)   // register-staged operands (A/B)
+        wg_reg_tile(g.wg[j], smem, t % g.gx[j], t / g.gx[j], split);
+      else
+        dma_gemm_tile<GRP_BM, GRP_BN, GRP_WGM, GRP_WGN, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, NS, GA>(
+            g.wg[j], smem, t % g.gx[j], t / g.gx[j], split);
       return;
     }
     bid -= g.blocks[j];
@@ -902,13 +1022,14 @@ hipError_t wgrad_multi(const WgradArgs* jobs, int nj, const int* splits, SlabRed
     nb += g.blocks[j];
   }
   const int ga = g_group_async >= 0 ? std::min(g_group_async, 2) : GROUP_ASYNC_DEFAULT;
-  const int si = wgm_stages() == 2 ? 0 : 1;
+  const int si = wgm_stages() == 2 ? 0 : wgm_stages() == 0 ? 2 : 1;
   using Fn = void (*)(WgradMultiParams);
-  static const Fn fns[2][3] = {
+  static const Fn fns[3][3] = {
       {wgrad_multi_kernel<0, 2>, wgrad_multi_kernel<1, 2>, wgrad_multi_kernel<2, 2>},
-      {wgrad_multi_kernel<0, WGM_NS>, wgrad_multi_kernel<1, WGM_NS>, wgrad_multi_kernel<2, WGM_NS>}};
-  static bool attr[2][3] = {};
-  const int smem = si ? WGM_SMEM : GRP_SMEM;
+      {wgrad_multi_kernel<0, WGM_NS>, wgrad_multi_kernel<1, WGM_NS>, wgrad_multi_kernel<2, WGM_NS>},
+      {wgrad_multi_kernel<2, 0>, wgrad_multi_kernel<2, 0>, wgrad_multi_kernel<2, 0>}};
+  static bool attr[3][3] = {};
+  const int smem = si == 1 ? WGM_SMEM : GRP_SMEM;
   if (!attr[si][ga]) {
     (void)hipFuncSetAttribute((const void*)fns[si][ga], hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr[si][ga] = true;

@@ -39,6 +39,7 @@ KNOBS = {
     "NNMPI_PAIR": "wide backward pair launches (experiments build)",
     "NNMPI_COMM_STANDIN": "k:gbps -- k CUs held after every bucket collective (standin.hip)",
     "NNMPI_WG_STAGES": "grouped weight-gradient launch DMA ring stages (default 2; 4)",
+    "NNMPI_WG_REG": "register-staged operands in the grouped weight-gradient launch (A/B)",
     "NNMPI_HEAD_BLOCKS": "block cap of the fused multi-output head (default 256)",
     "NNMPI_HEAD_FUSED": "multi-output head + weight gradient in one kernel (0: two launches)",
 }
