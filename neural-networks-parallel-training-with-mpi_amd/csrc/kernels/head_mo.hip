@@ -303,17 +303,25 @@ __global__ void __launch_bounds__(64 * MF_WAVES) head_mo_fused_kernel(HeadArgs p
     }
     if (more) cur = nxt;
   }
-  // ---- block partials: every gW element has one owner lane (o = 4g + i, column l & 15) ----
+  // ---- block partials: every gW element has one owner lane (o = 4g + i, column l & 15).  The
+  // accumulators go through LDS (the W images are dead: the loop ended on a barrier) as a
+  // [16][in] fp32 image, then every thread stores whole 16-byte row pieces: 5 coalesced stores
+  // per thread at in = 1024, out = 10 instead of 32 scattered 4-byte ones per lane ----
+  float* gimg = reinterpret_cast<float*>(smem);
 #pragma unroll
   for (int ph = 0; ph < NPH; ++ph)
 #pragma unroll
     for (int t = 0; t < 4; ++t)
 #pragma unroll
-      for (int i = 0; i < 4; ++i) {
-        const int o = 4 * g + i;
-        if (o < out)
-          gws[((long long)blockIdx.x * out + o) * in + ph * MF_PH + (wv * 4 + t) * 16 + r] = gacc[ph][t][i];
-      }
+      for (int i = 0; i < 4; ++i)
+        gimg[(4 * g + i) * in + ph * MF_PH + (wv * 4 + t) * 16 + r] = gacc[ph][t][i];
+  __syncthreads();
+  {
+    const int n4 = out * in / 4;
+    float* dst = gws + (long long)blockIdx.x * out * in;
+    for (int v = tid; v < n4; v += 64 * MF_WAVES)
+      reinterpret_cast<f32x4*>(dst)[v] = reinterpret_cast<const f32x4*>(gimg)[v];
+  }
   bsum += __shfl_xor(bsum, 16, 64);
   bsum += __shfl_xor(bsum, 32, 64);
   if (w == 0) {
