@@ -417,3 +417,30 @@ def test_shm_sync_falls_back_to_gloo_when_one_rank_cannot_load_the_library():
     for r in range(2):
         assert a[r]["losses"] == pytest.approx(b[r]["losses"], rel=1e-5)
         assert torch.allclose(a[r]["final"], b[r]["final"], rtol=1e-5, atol=1e-6)
+
+
+def test_workspace_covers_chunk_bucket_weight_gradients():
+    """A layer cut into output-row chunk buckets runs one weight-gradient GEMM per chunk.  A chunk
+    has fewer output tiles than the whole layer, so it may split K where the layer does not
+    (1024 of 2048 rows at K = 1024: 2 splits, found by the 3-rank wide2048 tuner rehearsal on the
+    GPU) -- the engine's split-K workspace must cover the chunk shapes too."""
+    from types import SimpleNamespace
+    from nnmpi_amd.engine.arena import Arena
+    from nnmpi_amd.engine.engine import MLPEngine
+    widths = [2048, 2048, 2048, 1]
+    arena = Arena([(widths[i + 1], widths[i]) for i in range(3)], "cpu",
+                  bucket_bytes=8 * 2 ** 20, chunk_min_tiles=16)
+    chunked = [i for i in range(3) if arena.chunk_buckets(i)]
+    assert chunked, "the 2048-wide layers must be cut into chunk buckets"
+
+    class Ops:   # a chunk splits, the whole layer does not
+        def wgrad_workspace_bytes(self, rows, out_f, in_f, dtype):
+            return 0 if out_f == 2048 else 1000 + out_f
+
+        def head_workspace_bytes(self, rows, in_f, out_f):
+            return 0
+
+    stub = SimpleNamespace(ops=Ops(), R=1024, spec=SimpleNamespace(widths=widths), L=3,
+                           arena=arena, dtype=torch.bfloat16, use_tiny=False)
+    rows = max(b.rows[1] - b.rows[0] for i in chunked for b in arena.chunk_buckets(i))
+    assert MLPEngine._workspace_bytes(stub) == 1000 + rows
