@@ -359,6 +359,19 @@ void set_pp256_order(int epi, int idx) {
   if (epi >= 0 && epi < 3 && idx >= 0 && idx < 4) g_pp_order[epi] = idx;
 }
 
+// Prefetch of the fused SGD update's operands in the 256x256 weight gradient (pp256_tile PF):
+// 0 off, 1 default cache policy, 2 nt.  NNMPI_PP_PREFETCH (experiments) / set_pp_prefetch A/B.
+static int g_pp_prefetch = -2;
+constexpr int PP_PREFETCH_DEFAULT = 0;
+void set_pp_prefetch(int v) { g_pp_prefetch = (v >= 0 && v <= 2) ? v : -1; }
+static int pp_prefetch() {
+  if (g_pp_prefetch == -2) {
+    const char* e = knob_env("NNMPI_PP_PREFETCH");
+    g_pp_prefetch = (e && e[0] >= '0' && e[0] <= '2') ? e[0] - '0' : -1;
+  }
+  return g_pp_prefetch >= 0 ? g_pp_prefetch : PP_PREFETCH_DEFAULT;
+}
+
 // Kernel-selection knobs of the training step (scripts/step_ab.py A/Bs them; -1 / 0 = default).
 static int g_fwd_variant = -1;    // forward GEMM main-loop variant (launch_t's switch)
 static int g_group_async = -1;    // grouped-backward LDS read mode (dma_gemm_tile ASYNC_TR)
@@ -412,6 +425,23 @@ static hipError_t launch_t(GemmParams p, int splits, hipStream_t s, int variant 
       // the deep-ring twin lives in csrc/experiments (NNMPI_BUILD_EXPERIMENTS=1 builds)
       if (!exp_pp256_ring) return hipErrorNotSupported;
       return exp_pp256_ring(variant, LA, LB, EPI, ACT, BG, p, grid, s);
+    }
+    if constexpr (EPI == EPI_F32) {
+      // weight gradient + fused SGD: the update operands prefetched during the main loop
+      const int pf = pp_prefetch();
+      if (pf > 0 && variant == 0 && dflt == 1 && p.sg.g_base && !p.c16 && p.sgd_serial == 0) {
+        static const K pfns[2] = {gemm_bf16_pp256_kernel<LA, LB, EPI, ACT, BG, true, 1, 0, 1>,
+                                  gemm_bf16_pp256_kernel<LA, LB, EPI, ACT, BG, true, 1, 0, 2>};
+        static bool pattr = false;
+        if (!pattr) {
+          for (K f : pfns)
+            (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize,
+                                      PP_PF_SMEM);
+          pattr = true;
+        }
+        hipLaunchKernelGGL(pfns[pf - 1], grid, dim3(PP_THREADS), PP_PF_SMEM, s, p);
+        return hipGetLastError();
+      }
     }
     const K kfn = kfns[(variant >= 15 && variant <= 18) ? variant - 15 : dflt];
     hipLaunchKernelGGL(kfn, grid, dim3(PP_THREADS), PP_SMEM, s, p);

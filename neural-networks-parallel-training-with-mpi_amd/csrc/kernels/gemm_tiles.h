@@ -965,10 +965,19 @@ __device__ __forceinline__ void bias_act_lds_256(const GemmParams& p, const f32x
 // B0(t+2) | B1(t+2)); 1: one half per phase (B0(t+2) moves to P2: its buffer was last read in
 // P4 of the previous K-tile, the same two-phase WAR margin as A0's), so no memory section
 // carries four DMA instructions beside eight fragment reads.
+// PF (weight gradient with the fused SGD update, ISSUE 0 only): the update's master and
+// momentum rows are pulled toward the chip DURING the main loop -- one LDS-DMA instruction per
+// wave per K-tile, 4 bytes per lane from one 64-byte granule each, landing in a 256-byte dummy
+// slot per wave behind the ring (PP_PF_SMEM) -- so the epilogue, which otherwise has every CU
+// read 512 KiB from HBM at the same moment (measured HBM-bound: scripts/r4_wgrad_sgd_ab.py),
+// finds them in the memory-side cache.  PF 1 default policy, PF 2 `nt`.  The prefetch is one more
+// vector-memory op per K-tile, so the counted waits of P1..P3 allow one (two) more.
+constexpr int PP_PF_SMEM = 128 * 1024 + 8 * 256;
 template <int LA, int LB, int EPI, int ACT, bool BIASGRAD, bool LATE_LGKM = true, int GM = 4,
-          int ISSUE = 0>
+          int ISSUE = 0, int PF = 0>
 __device__ __forceinline__ void pp256_tile(const GemmParams& p, char* smem, int bid, int gx, int gy,
                                            int split) {
+  static_assert(PF == 0 || (ISSUE == 0 && EPI == EPI_F32), "prefetch: wgrad + SGD, issue order 0");
   constexpr int BK = GEMM_BK;
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
@@ -1004,11 +1013,40 @@ __device__ __forceinline__ void pp256_tile(const GemmParams& p, char* smem, int 
   for (int i = 0; i < 8; ++i) rsum[i] = 0.f;
   const bool do_bg = BIASGRAD && tx == 0 && wn == 0;
 
+  // prefetch plan (PF): granule g of 4096 per array (256 rows x 16 x 64 B), K-tile t serves
+  // array t & 1, granules ((t >> 1) * 8 + w) * pf_lpw + lane, spread to finish ~4 K-tiles early
+  __amdgpu_buffer_rsrc_t rsP = rsA, rsM = rsA;
+  bool pf_on = false;
+  int pf_lpw = 0;
+  if constexpr (PF > 0) {
+    pf_on = p.sg.g_base && !p.c16 && p.sgd_serial == 0 && m0 + 256 <= p.M && n0 + 256 <= p.N;
+    if (pf_on) {
+      const long long o = (reinterpret_cast<const float*>(p.C) + split * p.c_split_stride - p.sg.g_base) +
+                          (long long)m0 * p.ldc + n0;
+      const int bytes = (255 * p.ldc + 256) * 4;
+      rsP = __builtin_amdgcn_make_buffer_rsrc((void*)(p.sg.p_base + o), (short)0, bytes, 0x00020000);
+      rsM = __builtin_amdgcn_make_buffer_rsrc((void*)(p.sg.m_base + o), (short)0, bytes, 0x00020000);
+    }
+    const int span = max(nt - 4, 2) / 2;   // K-tiles per array
+    pf_lpw = min(64, (4096 / 8 + span - 1) / span);
+  }
+  auto prefetch = [&](int t) {
+    if constexpr (PF > 0) {
+      const int g = ((t >> 1) * 8 + w) * pf_lpw + lane;
+      const bool ok = pf_on && t >= 0 && lane < pf_lpw && g < 4096;
+      const unsigned v = ok ? (unsigned)((g >> 4) * p.ldc * 4 + (g & 15) * 64) : DMA_OOB;
+      __builtin_amdgcn_raw_ptr_buffer_load_lds((t & 1) ? rsM : rsP,
+          (__attribute__((address_space(3))) void*)(smem + 128 * 1024 + w * 256), 4, v, 0, 0,
+          PF == 2 ? 2 : 0);
+    }
+  };
+
   // prologue: K-tile 0 whole, K-tile 1's A0, B0, B1 (the steady-state issue order); retire
   // K-tile 0's A0 + B0 (five newer halves may stay in flight)
   pa0.issue(rsA, A0(0), w, kof(0), kend);
   pb0.issue(rsB, B0(0), w, kof(0), kend);
   pb1.issue(rsB, B1(0), w, kof(0), kend);
+  prefetch(-1);   // (PF: the slot K-tile -1 would have used; no traffic)
   pa1.issue(rsA, A1(0), w, kof(0), kend);
   if constexpr (ISSUE == 1) {   // the steady-state order of K-tile "-1": B0, A0, B1
     pb0.issue(rsB, B0(1), w, kof(1), kend);
@@ -1018,7 +1056,7 @@ __device__ __forceinline__ void pp256_tile(const GemmParams& p, char* smem, int 
     pb0.issue(rsB, B0(1), w, kof(1), kend);
   }
   pb1.issue(rsB, B1(1), w, kof(1), kend);
-  wait_vm<10>();
+  wait_vm<PF ? 11 : 10>();
   __builtin_amdgcn_s_barrier();
 
   bf16x8 af[4][2], b0f[2][2], b0n[2][2], b1f[2][2];
@@ -1064,20 +1102,23 @@ __device__ __forceinline__ void pp256_tile(const GemmParams& p, char* smem, int 
       // P2 -> A1(t) [8], P3 -> A0 + B0 (t+1) [8] (read in P4 and in the next P1).
       // ISSUE 1: P1 A1(t+1) | P2 B0(t+2) | P3 A0(t+2) | P4 B1(t+2); retire: P1 -> B1(t) [10],
       // P2 -> A1(t) [10], P3 -> B0 + A0 (t+1) [8]
+      // PF: prefetch(t) sits in front of A1(t+1); newer than the retired half: P1 two
+      // prefetches (t-1, t), P2 and P3 one (t)
       if (ph == 0) {
+        prefetch(t);
         pa1.issue(rsA, A1(nb), w, kof(t + 1), kend);
-        wait_vm<10>();
+        wait_vm<PF ? 12 : 10>();
       } else if (ph == 1) {
         if constexpr (ISSUE == 1) {
           pb0.issue(rsB, B0(b), w, kof(t + 2), kend);
           wait_vm<10>();
         } else {
-          wait_vm<8>();
+          wait_vm<PF ? 9 : 8>();
         }
       } else if (ph == 2) {
         pa0.issue(rsA, A0(b), w, kof(t + 2), kend);
         if constexpr (ISSUE == 0) pb0.issue(rsB, B0(b), w, kof(t + 2), kend);
-        wait_vm<8>();
+        wait_vm<PF ? 9 : 8>();
       } else {
         pb1.issue(rsB, B1(b), w, kof(t + 2), kend);
       }
@@ -1158,11 +1199,11 @@ __device__ __forceinline__ void pp256_tile(const GemmParams& p, char* smem, int 
 }
 
 template <int LA, int LB, int EPI, int ACT, bool BIASGRAD, bool LATE_LGKM = true, int GM = 4,
-          int ISSUE = 0>
+          int ISSUE = 0, int PF = 0>
 __global__ void __launch_bounds__(PP_THREADS) gemm_bf16_pp256_kernel(GemmParams p) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int gx = gridDim.x, gy = gridDim.y;
-  pp256_tile<LA, LB, EPI, ACT, BIASGRAD, LATE_LGKM, GM, ISSUE>(
+  pp256_tile<LA, LB, EPI, ACT, BIASGRAD, LATE_LGKM, GM, ISSUE, PF>(
       p, smem, xcd_remap(blockIdx.y * gx + blockIdx.x, gx * gy), gx, gy, blockIdx.z);
 }
 

@@ -67,6 +67,7 @@ void set_gemm_tile(int t);     // 0 = heuristic, 64 / 128 = force (experiments)
 void set_gemm_variant(int v);  // DMA-path main-loop variant (experiments), 0 = default
 // step-level kernel-selection knobs (-1 / 0 = built-in default; scripts/step_ab.py)
 void set_fwd_variant(int v);   // forward GEMM (128x128 tiles) main-loop variant
+void set_pp_prefetch(int v);            // SGD-operand prefetch in the 256x256 wgrad (0 / 1 / 2)
 void set_pp256_order(int epi, int idx);   // 256x256 kernel tile order per epilogue (A/B)
 void set_store_policy(int p);
 void set_slab_store_policy(int p);   // split-K slab stores of the grouped backward (-2: env)  // LDS-epilogue output stores: 0 plain, 1 nt, 2 sc1 (experiments)

@@ -32,6 +32,7 @@ KNOBS = {
     "NNMPI_CPU_NATIVE": "native host step of tiny CPU models (0: PyTorch)",
     "NNMPI_STAGE_EPI": "LDS-staged 256x256 forward epilogue",
     "NNMPI_SGD_SERIAL": "SGD epilogue form",
+    "NNMPI_PP_PREFETCH": "SGD-operand prefetch in the 256x256 weight gradient",
     "NNMPI_GEMM": "GEMM main loop (1 register-staged, 2 LDS-DMA)",
     "NNMPI_SLAB_STORE": "split-K slab store policy",
     "NNMPI_GROUP": "grouped backward launch (0 off)",
