@@ -1,7 +1,7 @@
 #!/bin/bash
-# Round 4: SGD-operand prefetch in the 8192-wide weight gradient (pp256_tile PF) -- kernel A/B
-# with bitwise check (scripts/r4_wgrad_prefetch_ab.py), then the wide step with NNMPI_PP_PREFETCH
-# 0 / 1 / 2 interleaved (experiments).  Usage: scripts/r4_prefetch.sh OUTDIR
+# Round 4: operand prefetch in the 8192-wide weight gradient's SGD epilogue (pp256_tile PF) --
+# kernel A/B with bitwise check (scripts/r4_wgrad_prefetch_ab.py), then the wide step with
+# NNMPI_PP_PREFETCH 0 / 1 / 2 interleaved (experiments).  Usage: scripts/r4_prefetch.sh OUTDIR
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
 O=gpurun_out/${1:-r4pf}; mkdir -p $O

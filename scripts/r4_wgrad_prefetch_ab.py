@@ -1,7 +1,8 @@
-"""The 8192-wide weight gradient + fused SGD with its update operands prefetched during the main
-loop (pp256_tile PF; set_pp_prefetch 0 off / 1 default policy / 2 nt) vs without, one process,
-interleaved rounds, median of 10 launches per cell; plus the update bit-for-bit against PF 0 and
-the whole wide step (bench.py is run separately).  Needs NNMPI_EXPERIMENTS=1."""
+"""The 8192-wide weight gradient + fused SGD with the in-loop operand prefetch (set_pp_prefetch
+0 off / 1 default policy / 2 nt), one process, interleaved rounds, median of 10 launches per
+cell; every variant's update bit for bit against no prefetch.  (A one-round-trip-per-half
+epilogue form was measured with this script as cell "form 3" and removed again:
+profiles/r4_wgrad_sgd_epilogue_bound.txt.)  Needs NNMPI_EXPERIMENTS=1."""
 import os
 import statistics
 import sys
@@ -30,8 +31,9 @@ sgd = (G.data_ptr(), W.data_ptr(), Mo.data_ptr(), S.data_ptr(), hp.data_ptr(), 0
 assert lib.experiments_on(), "run with NNMPI_EXPERIMENTS=1"
 
 
-def run(pf, fused=True):
+def run(pf, fused=True, form=0):
     assert lib.set_pp_prefetch(pf)
+    assert lib.set_sgd_epilogue(form)
     lib.linear_wgrad_bf16(dz.data_ptr(), M, x.data_ptr(), N, G.data_ptr(), G[M * N:].data_ptr(),
                           M, N, rows, ws.data_ptr(), s, sgd if fused else None)
 
@@ -46,26 +48,29 @@ def t_ms(fn, n=10):
     return statistics.median(a.elapsed_time(b) for a, b in ev)
 
 
+cells = {"form 0, PF 0 (default)": (0, 0), "form 0, PF 1 (default policy)": (1, 0),
+         "form 0, PF 2 (nt)": (2, 0)}
 out = {}
-for pf in (0, 1, 2):
+for k, (pf, form) in cells.items():
     W.copy_(W0)
     Mo.copy_(Mo0)
-    run(pf)
+    run(pf, True, form)
     torch.cuda.synchronize()
-    out[pf] = (W.clone(), Mo.clone(), S.clone(), G[M * N:].clone())
-for pf in (1, 2):
-    eq = all(torch.equal(a, b) for a, b in zip(out[0], out[pf]))
-    print(f"PF {pf}: update (master, momentum, bf16 shadow, bias grad) bitwise equal to PF 0: {eq}",
+    out[k] = (W.clone(), Mo.clone(), S.clone(), G[M * N:].clone())
+k0 = next(iter(cells))
+for k in cells:
+    eq = all(torch.equal(a, b) for a, b in zip(out[k0], out[k]))
+    print(f"{k}: update (master, momentum, bf16 shadow, bias grad) bitwise equal to {k0}: {eq}",
           flush=True)
-cells = {"PF 0 (off)": 0, "PF 1 (default policy)": 1, "PF 2 (nt)": 2}
 res = {k: [] for k in cells}
 plain = []
 for rnd in range(4):
-    for k, pf in cells.items():
-        res[k].append(t_ms(lambda: run(pf)))
+    for k, (pf, form) in cells.items():
+        res[k].append(t_ms(lambda: run(pf, True, form)))
     plain.append(t_ms(lambda: run(0, False)))
     print(f"round {rnd} done", flush=True)
 for k in cells:
-    print(f"{k:24s} {statistics.median(res[k]) * 1e3:7.1f} us   rounds {[round(v * 1e3, 1) for v in res[k]]}")
-print(f"{'plain (no update)':24s} {statistics.median(plain) * 1e3:7.1f} us   rounds {[round(v * 1e3, 1) for v in plain]}")
+    print(f"{k:32s} {statistics.median(res[k]) * 1e3:7.1f} us   rounds {[round(v * 1e3, 1) for v in res[k]]}")
+print(f"{'plain (no update)':32s} {statistics.median(plain) * 1e3:7.1f} us   rounds {[round(v * 1e3, 1) for v in plain]}")
 lib.set_pp_prefetch(-1)
+lib.set_sgd_epilogue(-1)
