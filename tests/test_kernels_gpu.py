@@ -55,6 +55,31 @@ def test_gemm_identity_asymmetric():
     torch.testing.assert_close(C, B.float())
 
 
+def test_cu_mask_stream_runs_kernels_bitwise_equal():
+    """cu_mask_stream (the CU-partitioned concurrency experiment, scripts/r4_cu_split_ab.py): a
+    GEMM on a stream restricted to half the CUs gives the same bits as on the whole chip."""
+    lib = _lib()
+    n_cu = torch.cuda.get_device_properties(0).multi_processor_count
+    mask = [0] * ((n_cu + 31) // 32)
+    for c in range(0, n_cu, 2):
+        mask[c // 32] |= 1 << (c % 32)
+    st = lib.cu_mask_stream(mask)
+    try:
+        M, N, K = 1024, 768, 512
+        A = _rand(M, K, seed=11).to(torch.bfloat16)
+        Bs = _rand(N, K, seed=12).to(torch.bfloat16)
+        C0 = torch.zeros(M, N, device=DEV)
+        C1 = torch.zeros(M, N, device=DEV)
+        lib.gemm_bf16(A.data_ptr(), K, 0, Bs.data_ptr(), K, 0, M, N, K, C0.data_ptr(), N, _s())
+        torch.cuda.synchronize()
+        lib.gemm_bf16(A.data_ptr(), K, 0, Bs.data_ptr(), K, 0, M, N, K, C1.data_ptr(), N, st)
+        torch.cuda.ExternalStream(st).synchronize()
+        assert torch.equal(C0, C1)
+        torch.testing.assert_close(C0, A.float() @ Bs.float().t(), rtol=1e-4, atol=1e-3)
+    finally:
+        lib.stream_destroy(st)
+
+
 @pytest.mark.parametrize("act", ["relu", "tanh", "none"])
 @pytest.mark.parametrize("dtype", [torch.bfloat16, torch.float32])
 @pytest.mark.parametrize("M,N,K", [(8192, 512, 512), (1000, 264, 136), (4097, 1024, 784)])
