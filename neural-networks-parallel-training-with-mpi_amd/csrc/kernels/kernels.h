@@ -167,8 +167,11 @@ struct RowbandArgs {
   const float* y;           // targets [rows]
   float inv_count;
   float* wslab; float* bslab; float* loss_part;   // per-band head partials (rowband_blocks)
+  int band_map;             // v2: 1 = block b runs band xcd_remap(b) (an XCD's blocks hold
+                            // contiguous rows), 0 = band b
 };
 int rowband_blocks(int rows);
+void set_rb_band_map(int v);   // A/B: XCD-contiguous band order (-1 re-reads NNMPI_RB_BANDMAP)
 bool rowband_ok(int rows, int H, int in, int nh, int out, int loss, int act);
 bool rowband2_ok(int rows, int H, int in, int nh, int out, int loss, int act);
 // elements of the fragment-major weight images one model needs (rowband_pack)

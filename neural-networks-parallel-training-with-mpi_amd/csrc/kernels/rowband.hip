@@ -278,8 +278,8 @@ __device__ __forceinline__ void rb_dgrad(const bf16* __restrict__ W, const char*
 // order (deterministic), from the per-row dlogits / squared errors in LDS.
 template <int H>
 __device__ __forceinline__ void rb_head_partials(const RowbandArgs& p, const char* act,
-                                                 const float* dls, const float* lss, int tid) {
-  const int blk = blockIdx.x;
+                                                 const float* dls, const float* lss, int tid,
+                                                 int blk) {
   for (int k = tid; k < H; k += RB_THREADS) {
     float s = 0.f;
 #pragma unroll 8
@@ -333,7 +333,7 @@ __device__ __forceinline__ void rb_head(const RowbandArgs& p, const char* in, ch
   {
     // in place: the band's weight-gradient partial reads the activations before dZ replaces them
     __syncthreads();
-    rb_head_partials<H>(p, in, dls, lss, tid);
+    rb_head_partials<H>(p, in, dls, lss, tid, blockIdx.x);
     __syncthreads();
   }
 #pragma unroll
@@ -594,7 +594,8 @@ __device__ __forceinline__ Rb2Par rb2_par(char* base, int H, int nh) {
 // Regression head of the band (out == 1, MSE) in place on `z` = a_{nh-1}: logit, loss, dlogit,
 // the band's head-gradient partials, then dZ_{nh-1} = dl * w * act'(a) over a.
 template <int H, int ACT>
-__device__ __forceinline__ void rb2_head(const RowbandArgs& p, char* z, const Rb2Par& q, int nvalid, int tid) {
+__device__ __forceinline__ void rb2_head(const RowbandArgs& p, char* z, const Rb2Par& q, int nvalid, int tid,
+                                         int band) {
   constexpr int CPT = H / 8 / 16;   // 8-column chunks per thread (16 threads per row)
   const int r = tid >> 4, g = tid & 15;
   // (a and w are re-read from the LDS for the dZ pass instead of held: the weight ring is live
@@ -621,7 +622,7 @@ __device__ __forceinline__ void rb2_head(const RowbandArgs& p, char* z, const Rb
     q.lss[r] = valid ? d * d : 0.f;
   }
   __syncthreads();
-  rb_head_partials<H>(p, z, q.dls, q.lss, tid);
+  rb_head_partials<H>(p, z, q.dls, q.lss, tid, band);
   __syncthreads();   // every partial has read a before dZ replaces it
 #pragma unroll
   for (int c = 0; c < CPT; ++c) {
@@ -647,7 +648,12 @@ __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
   const int blk = blockIdx.x;
-  const int row0 = blk * RB_ROWS;
+  // band_map 1: the 32 blocks an XCD runs hold contiguous rows, so the row-split weight
+  // gradients that read them next (wgrad_multi: split s's blocks sit on the XCDs that wrote its
+  // rows) can find them in that XCD's L2.  Per-band partials stay indexed by band: the combine
+  // order, and so every result bit, does not depend on the map.
+  const int band = p.band_map ? xcd_remap(blk, gridDim.x) : blk;
+  const int row0 = band * RB_ROWS;
   const int nvalid = min(RB_ROWS, p.rows - row0);
   const int nh = p.nh, IN = p.in;
   // column group of this wave, rotated per block so the 32 blocks of an XCD do not all fetch
@@ -719,7 +725,7 @@ __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
   }
   // ---- head (in place on a_{nh-1}) ----
   char* z = slot(nh >= 2 ? 0 : 1);
-  rb2_head<H, ACT>(p, z, q, nvalid, tid);
+  rb2_head<H, ACT>(p, z, q, nvalid, tid, band);
   __syncthreads();
   rb_copy_out<H>(z, p.dz[nh - 1] + (long long)row0 * H, H, nvalid, tid);
   // ---- activation gradients: dZ_{l-1} = (dZ_l W_l) * act'(a_{l-1}), in place over a_{l-1} ----
@@ -858,8 +864,19 @@ size_t rowband_packed_elems(int H, int in, int nh) {
 }
 
 
+// XCD-contiguous band order of the v2 kernel (RowbandArgs::band_map): NNMPI_RB_BANDMAP=0/1
+// (experiments); results are bitwise the same either way.
+static int g_rb_band_map = -1;
+constexpr int RB_BAND_MAP_DEFAULT = 0;
+void set_rb_band_map(int v) { g_rb_band_map = v; }
+static int rb_band_map() {
+  if (g_rb_band_map < 0) g_rb_band_map = rb_env("NNMPI_RB_BANDMAP", RB_BAND_MAP_DEFAULT) ? 1 : 0;
+  return g_rb_band_map;
+}
+
 hipError_t rowband_fwd_bwd(const RowbandArgs& p0, hipStream_t s) {
   RowbandArgs p = p0;
+  p.band_map = rb_band_map();
   if (p.Pf[0]) {   // v2: packed weight images
     if (!rowband2_ok(p.rows, p.H, p.in, p.nh, 1, LOSS_MSE, p.act)) return hipErrorInvalidValue;
     for (int l = 0; l < p.nh; ++l)
