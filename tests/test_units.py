@@ -444,3 +444,24 @@ def test_workspace_covers_chunk_bucket_weight_gradients():
                            arena=arena, dtype=torch.bfloat16, use_tiny=False)
     rows = max(b.rows[1] - b.rows[0] for i in chunked for b in arena.chunk_buckets(i))
     assert MLPEngine._workspace_bytes(stub) == 1000 + rows
+
+
+def _xcd_remap(bid, nwg):
+    """Host replica of csrc/kernels/common.h xcd_remap (block id -> work id)."""
+    if nwg <= 8:
+        return bid
+    q, r, xcd = nwg // 8, nwg % 8, bid % 8
+    return (xcd * (q + 1) if xcd < r else r * (q + 1) + (xcd - r) * q) + bid // 8
+
+
+@pytest.mark.parametrize("nwg", [1, 7, 8, 9, 31, 256, 257, 300, 1023, 1024])
+def test_xcd_remap_is_a_permutation_with_contiguous_xcd_ranges(nwg):
+    """The row-band kernel's XCD-contiguous band order (RowbandArgs::band_map) and the grouped
+    weight gradients use xcd_remap: every band must be run exactly once, and the blocks that
+    share an XCD (same id mod 8) must get one contiguous range of work ids."""
+    ids = [_xcd_remap(b, nwg) for b in range(nwg)]
+    assert sorted(ids) == list(range(nwg))
+    if nwg > 8:
+        for x in range(8):
+            mine = sorted(ids[b] for b in range(x, nwg, 8))
+            assert mine == list(range(mine[0], mine[0] + len(mine)))
