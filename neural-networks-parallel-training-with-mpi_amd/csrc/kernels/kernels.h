@@ -169,11 +169,9 @@ struct RowbandArgs {
   float* wslab; float* bslab; float* loss_part;   // per-band head partials (rowband_blocks)
   int band_map;             // v2: 1 = block b runs band xcd_remap(b) (an XCD's blocks hold
                             // contiguous rows), 0 = band b
-  int epi_swap;             // v2: odd rows store their tile-pair partner first (LDS banks)
 };
 int rowband_blocks(int rows);
 void set_rb_band_map(int v);   // A/B: XCD-contiguous band order (-1 re-reads NNMPI_RB_BANDMAP)
-void set_rb_epi_swap(int v);   // A/B: conflict-free epilogue store order (-1 re-reads NNMPI_RB_EPISWAP)
 bool rowband_ok(int rows, int H, int in, int nh, int out, int loss, int act);
 bool rowband2_ok(int rows, int H, int in, int nh, int out, int loss, int act);
 // elements of the fragment-major weight images one model needs (rowband_pack)

@@ -660,7 +660,6 @@ __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
   // the same weight lines at the same moment
   const int cg = (w + blk) & (RB_WAVES - 1);
   const int n0 = cg * G::WCOLS;
-  const int sw = (G::NJ % 2 == 0 && p.epi_swap) ? (lane & 1) : 0;
   const int SL = RB_ROWS * max(H, IN) * 2;
   const int nslot = max(nh, 2);
   auto slot = [&](int i) { return smem + i * SL; };
@@ -706,20 +705,18 @@ __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
     const char* in = slot(l == 0 ? 0 : l);
     char* out = l < nh - 1 ? slot(l + 1) : slot(nh >= 2 ? 0 : 1);
     rb2_mainloop<H, D>(ring, acc, in, cur, nxt, lane);
-    // lane holds out[16i + (lane & 15)][n0 + 16j + 4(lane >> 4) .. +3].  epi_swap: odd rows
-    // store tile j ^ 1 while even rows store tile j -- rows r and r ^ 1 share their 16-byte
-    // chunk's swizzle, so a 16-lane ds_write_b64 group otherwise hits each bank pair twice.
+    // lane holds out[16i + (lane & 15)][n0 + 16j + 4(lane >> 4) .. +3]
+    const float* bl = q.bias + l * H + n0 + 4 * (lane >> 4);
 #pragma unroll
     for (int j = 0; j < G::NJ; ++j) {
-      const int jj = j ^ sw;
-      const f32x4 bv = *reinterpret_cast<const f32x4*>(q.bias + l * H + n0 + 16 * jj + 4 * (lane >> 4));
+      const f32x4 bv = *reinterpret_cast<const f32x4*>(bl + 16 * j);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const f32x4 v = (sw ? acc[i][j ^ (G::NJ % 2 == 0)] : acc[i][j]) + bv;
+        const f32x4 v = acc[i][j] + bv;
         bf16x4 o;
 #pragma unroll
         for (int r = 0; r < 4; ++r) o[r] = (bf16)act_fwd_t<ACT>(v[r]);
-        *reinterpret_cast<bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * jj + 4 * (lane >> 4))) = o;
+        *reinterpret_cast<bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * j + 4 * (lane >> 4))) = o;
       }
     }
     __syncthreads();
@@ -744,13 +741,11 @@ __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < G::NJ; ++j) {
-        const int jj = j ^ sw;   // (epi_swap, as in the forward epilogue)
-        bf16x4* po = reinterpret_cast<bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * jj + 4 * (lane >> 4)));
+        bf16x4* po = reinterpret_cast<bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * j + 4 * (lane >> 4)));
         const bf16x4 ax = *po;
-        const f32x4 av = sw ? acc[i][j ^ (G::NJ % 2 == 0)] : acc[i][j];
         bf16x4 o;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16)(av[r] * act_bwd_t<ACT>((float)ax[r]));
+        for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc[i][j][r] * act_bwd_t<ACT>((float)ax[r]));
         *po = o;
       }
     __syncthreads();
@@ -879,18 +874,9 @@ static int rb_band_map() {
   return g_rb_band_map;
 }
 
-static int g_rb_epi_swap = -1;
-constexpr int RB_EPI_SWAP_DEFAULT = 0;
-void set_rb_epi_swap(int v) { g_rb_epi_swap = v; }
-static int rb_epi_swap() {
-  if (g_rb_epi_swap < 0) g_rb_epi_swap = rb_env("NNMPI_RB_EPISWAP", RB_EPI_SWAP_DEFAULT) ? 1 : 0;
-  return g_rb_epi_swap;
-}
-
 hipError_t rowband_fwd_bwd(const RowbandArgs& p0, hipStream_t s) {
   RowbandArgs p = p0;
   p.band_map = rb_band_map();
-  p.epi_swap = rb_epi_swap();
   if (p.Pf[0]) {   // v2: packed weight images
     if (!rowband2_ok(p.rows, p.H, p.in, p.nh, 1, LOSS_MSE, p.act)) return hipErrorInvalidValue;
     for (int l = 0; l < p.nh; ++l)

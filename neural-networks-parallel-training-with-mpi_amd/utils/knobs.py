@@ -34,7 +34,6 @@ KNOBS = {
     "NNMPI_SGD_SERIAL": "SGD epilogue form",
     "NNMPI_PP_PREFETCH": "SGD-operand prefetch in the 256x256 weight gradient",
     "NNMPI_RB_BANDMAP": "XCD-contiguous band order of the row-band kernel",
-    "NNMPI_RB_EPISWAP": "row-band epilogue store order (LDS bank conflicts)",
     "NNMPI_GEMM": "GEMM main loop (1 register-staged, 2 LDS-DMA)",
     "NNMPI_SLAB_STORE": "split-K slab store policy",
     "NNMPI_GROUP": "grouped backward launch (0 off)",
