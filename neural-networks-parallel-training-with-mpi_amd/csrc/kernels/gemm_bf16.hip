@@ -852,7 +852,11 @@ struct WgradMultiParams {
   GemmParams wg[RB_MAXL];
   int gx[RB_MAXL], tiles[RB_MAXL], n[RB_MAXL], blocks[RB_MAXL];
   int nj;
+  unsigned long long* stamps;   // diagnostic: per block {start, end, XCC id, HW id} (null: off)
 };
+// diagnostic (scripts/r5_wg_stamps.py): every later wgrad_multi launch records per-block stamps
+static unsigned long long* g_wgm_stamps = nullptr;
+void set_wgrad_multi_stamps(unsigned long long* buf) { g_wgm_stamps = buf; }
 
 // NS: LDS stages of the DMA ring.  The launch holds about one block per CU (3 jobs x 16 tiles x 5
 // splits = 240 blocks on the proxy step), so no second block hides a k-step's DMA wait; a
@@ -989,9 +993,28 @@ __device__ __forceinline__ void wg_reg_tile(const GemmParams& p, char* smem, int
 }
 
 template <int GA, int NS>
+__device__ __forceinline__ void wgrad_multi_body(const WgradMultiParams& g, char* smem, int bid);
+
+template <int GA, int NS>
 __global__ void __launch_bounds__(GRP_THREADS, NS == 0 ? 2 : 4) wgrad_multi_kernel(WgradMultiParams g) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   int bid = blockIdx.x;
+  if (g.stamps) {
+    if (threadIdx.x == 0) {
+      g.stamps[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memrealtime();
+      g.stamps[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_getreg(20 | (31 << 11));   // XCC id
+      g.stamps[blockIdx.x * 4 + 3] = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW id
+    }
+    wgrad_multi_body<GA, NS>(g, smem, bid);
+    __syncthreads();
+    if (threadIdx.x == 0) g.stamps[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime();
+    return;
+  }
+  wgrad_multi_body<GA, NS>(g, smem, bid);
+}
+
+template <int GA, int NS>
+__device__ __forceinline__ void wgrad_multi_body(const WgradMultiParams& g, char* smem, int bid) {
 #pragma unroll
   for (int j = 0; j < RB_MAXL; ++j) {
     if (j >= g.nj) return;
@@ -1051,6 +1074,7 @@ hipError_t wgrad_multi(const WgradArgs* jobs, int nj, const int* splits, SlabRed
     g.blocks[j] = (g.n[j] + 7) & ~7;
     nb += g.blocks[j];
   }
+  g.stamps = g_wgm_stamps;
   const int ga = g_group_async >= 0 ? std::min(g_group_async, 2) : GROUP_ASYNC_DEFAULT;
   const int si = wgm_stages() == 2 ? 0 : wgm_stages() == 0 ? 2 : 1;
   using Fn = void (*)(WgradMultiParams);

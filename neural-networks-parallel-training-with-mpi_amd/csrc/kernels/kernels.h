@@ -169,10 +169,16 @@ struct RowbandArgs {
   float* wslab; float* bslab; float* loss_part;   // per-band head partials (rowband_blocks)
   int band_map;             // v2: 1 = block b runs band xcd_remap(b) (an XCD's blocks hold
                             // contiguous rows), 0 = band b
+  unsigned long long* stamps = nullptr;   // v2 diagnostic phase stamps (set_rowband_stamps)
+  int out_pol = 0;          // copy-out store policy of a / dZ: 0 plain, 1 nt, 2 sc1 (write-through)
 };
+void set_rb_store_policy(int pol);   // A/B of RowbandArgs::out_pol (-1: NNMPI_RB_STORE)
+// diagnostic: every later v2 row-band launch records per-wave phase stamps into buf
+// (rowband_blocks(rows) x rowband_stamp_slots() uint64; null = off)
+void set_rowband_stamps(unsigned long long* buf);
+int rowband_stamp_slots();
 int rowband_blocks(int rows);
 void set_rb_band_map(int v);   // A/B: XCD-contiguous band order (-1 re-reads NNMPI_RB_BANDMAP)
-bool rowband_ok(int rows, int H, int in, int nh, int out, int loss, int act);
 bool rowband2_ok(int rows, int H, int in, int nh, int out, int loss, int act);
 // elements of the fragment-major weight images one model needs (rowband_pack)
 size_t rowband_packed_elems(int H, int in, int nh);

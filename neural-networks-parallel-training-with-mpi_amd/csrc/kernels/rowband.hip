@@ -1,4 +1,4 @@
-// Row-band step for narrow square MLPs (every hidden width and the input width = H = 512, a
+// Row-band step for narrow MLPs (equal hidden widths H = 256..1024, input width % 64, a
 // regression head out == 1 with MSE): the reference's whole forward, loss and activation-gradient
 // chain (ref.py:42-44,170-176: Linear+ReLU x L-1, Linear, MSELoss, and autograd's mm /
 // threshold_backward down to dZ_0) in ONE launch, then every weight gradient in ONE grouped
@@ -14,16 +14,12 @@
 // Infinity Cache per GEMM (docs/PERF.md "Where a launch's time goes"): 8 launches per step
 // become 3.
 //
-// Block = 8 waves (512 threads) x 32 rows; wave w owns output columns [64w, 64w+64) of every
-// layer (2 x 4 v_mfma_f32_16x16x32_bf16 tiles).  LDS (the whole 160 KiB): ONE activation image
-// of the band (the KMAJ image of gemm_tiles.h per 64-deep k-block: conflict-free row-fragment
-// reads), updated in place by every pass -- a barrier separates a pass's main loop from its
-// epilogue -- and two 8 KiB weight stages per wave: KMAJ [64 n][64 k] for the forward's B
-// operand, XMAJ [64 k][64 x] for the dgrad's transposed operand (ds_read_b64_tr_b16, the GEMMs'
-// XMAJ image).  The weights stream global -> registers (whole 128-byte lines per load
-// instruction, a 1-deep ring of k-steps pinned with sched_barrier) -> the stage buffer the
-// fragment reads of the current k-step are not using.  After each pass the image is copied out
-// row-contiguously (activations and dZ are needed by the weight gradients).
+// Block = 8 waves (512 threads) x 32 rows; wave w owns H/8 output columns of every layer
+// (2 x H/128 v_mfma_f32_16x16x32_bf16 tiles).  The weights stream from fragment-major images
+// (one 16-byte load per lane fills one MFMA operand) straight into registers; the LDS holds only
+// the band's activation images (see "v2" below).  After each pass the image is copied out
+// row-contiguously (activations and dZ are needed by the weight gradients).  (The first form of
+// this kernel staged every weight k-step through LDS: 52 vs 40 us per step, round 4.)
 #include "gemm_tiles.h"
 #include "knobs.h"
 
@@ -32,25 +28,6 @@ namespace nnmpi {
 constexpr int RB_ROWS = 32;
 constexpr int RB_WAVES = 8;
 constexpr int RB_THREADS = 64 * RB_WAVES;
-// k-steps of weight loads in flight per lane beyond the staged one: 1 measured fastest with the
-// double-buffered stage (0.0772-0.0775 ms/step vs 0.0783-0.0784 at 2 and 0.0802-0.0805 at 3,
-// profiles/r3s2_rowband_ring_depth_ab.txt) -- deeper rings only add VGPRs and queued requests
-constexpr int RB_RING = 1;
-
-template <int H>
-struct RbGeom {
-  static_assert(H == 512, "row-band step: H = 512");
-  static constexpr int KSTEPS = H / 64;
-  static constexpr int WCOLS = H / RB_WAVES;       // output columns per wave
-  static constexpr int NJ = WCOLS / 16;            // 16-column MFMA tiles per wave
-  static constexpr int KB_BYTES = RB_ROWS * 128;   // one 64-deep k-block of an image
-  static constexpr int BUF = RB_ROWS * H * 2;      // one activation image
-  static constexpr int STAGE = 64 * WCOLS * 2;     // wave-private dgrad weight stage
-  static constexpr int SMEM = BUF + RB_WAVES * 2 * STAGE;   // 160 KiB: the whole LDS
-  static constexpr int FLD = 2 * NJ;               // forward: weight loads per lane per k-step
-  static constexpr int DLD = WCOLS / 8;            // dgrad: 16-B stage chunks per lane per k-step
-};
-
 // byte offset of element (row r, column k) in an activation image
 __device__ __forceinline__ int rb_off(int r, int k) {
   return (k >> 6) * (RB_ROWS * 128) + kmaj_off(r, (k >> 3) & 7) + ((k & 7) << 1);
@@ -59,330 +36,15 @@ __device__ __forceinline__ int rb_off(int r, int k) {
 // Row-contiguous copy between an LDS image and a [rows][ld] bf16 matrix (rows row0 .. row0 +
 // nvalid - 1): each wave moves whole 128-byte row pieces (8 lanes per row).
 template <int H>
-__device__ __forceinline__ void rb_copy_out(const char* img, bf16* dst, int ld, int nvalid, int tid) {
+__device__ __forceinline__ void rb_copy_out(const char* img, bf16* dst, int ld, int nvalid, int tid,
+                                            int pol) {
   constexpr int CH = RB_ROWS * H / 8;
 #pragma unroll
   for (int it = 0; it < CH / RB_THREADS; ++it) {
     const int id = tid + it * RB_THREADS;
     const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
     const bf16x8 v = *reinterpret_cast<const bf16x8*>(img + kb * (RB_ROWS * 128) + kmaj_off(r, k8));
-    if (r < nvalid) *reinterpret_cast<bf16x8*>(dst + (long long)r * ld + kb * 64 + k8 * 8) = v;
-  }
-}
-
-template <int H>
-__device__ __forceinline__ void rb_load_in(char* img, const bf16* src, int ld, int nvalid, int tid) {
-  constexpr int CH = RB_ROWS * H / 8;
-  bf16x8 v[CH / RB_THREADS];
-#pragma unroll
-  for (int it = 0; it < CH / RB_THREADS; ++it) {
-    const int id = tid + it * RB_THREADS;
-    const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
-    const int rr = min(r, nvalid - 1);   // clamped: every load issues; padding rows zeroed below
-    v[it] = *reinterpret_cast<const bf16x8*>(src + (long long)rr * ld + kb * 64 + k8 * 8);
-    if (r >= nvalid) {
-#pragma unroll
-      for (int e = 0; e < 8; ++e) v[it][e] = (bf16)0.f;
-    }
-  }
-#pragma unroll
-  for (int it = 0; it < CH / RB_THREADS; ++it) {
-    const int id = tid + it * RB_THREADS;
-    const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
-    *reinterpret_cast<bf16x8*>(img + kb * (RB_ROWS * 128) + kmaj_off(r, k8)) = v[it];
-  }
-}
-
-// One forward layer of the band: out = act(in . W^T + b) into the other image.  The wave's
-// weight rows stream through its private stage as a KMAJ image ([64 n][64 k] per k-step,
-// 8 lanes per 128-byte row piece: whole cache lines per load instruction).  Loading the B
-// fragments straight from global memory (16 rows x 32-64 B per load instruction, two k
-// permutations tried) ran the three forward passes in 51 us vs 29 us staged
-// (profiles/r3s2_rowband_ab.txt, r3s2_rowband_fwd_direct_and_wgrad_ns_ab.txt).
-template <int H, int ACT, int RING = RB_RING>
-__device__ __forceinline__ void rb_forward(const bf16* __restrict__ W, const float* __restrict__ bias,
-                                           const char* in, char* out, char* stage, int w, int lane) {
-  using G = RbGeom<H>;
-  const int n0 = w * G::WCOLS;
-  f32x4 acc[2][G::NJ];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < G::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // stage chunk q of k-step t: W[n0 + (lane >> 3) + 8q][64t + 8(lane & 7) .. +7]
-  const bf16* wp = W + (long long)(n0 + (lane >> 3)) * H + 8 * (lane & 7);
-  int soff[G::DLD];
-#pragma unroll
-  for (int q = 0; q < G::DLD; ++q) soff[q] = kmaj_off((lane >> 3) + 8 * q, lane & 7);
-  bf16x8 ring[RING][G::DLD];
-  auto issue = [&](int t, bf16x8 (&dst)[G::DLD]) {
-#pragma unroll
-    for (int q = 0; q < G::DLD; ++q)
-      dst[q] = *reinterpret_cast<const bf16x8*>(wp + (long long)8 * q * H + 64 * t);
-  };
-  f32x4 bv[G::NJ];
-#pragma unroll
-  for (int j = 0; j < G::NJ; ++j) bv[j] = *reinterpret_cast<const f32x4*>(bias + n0 + 16 * j + 4 * (lane >> 4));
-#pragma unroll
-  for (int s = 0; s < RING; ++s) issue(s, ring[s]);
-  // (sched_barrier: keep each ring refill where it is issued -- left alone, the scheduler sinks
-  // the loads next to their first use and the ring degenerates to a few loads in flight)
-  __builtin_amdgcn_sched_barrier(0);
-  {
-    // two stage buffers: the stage write of k-step t+1 is issued behind the fragment reads of
-    // k-step t, so the MFMAs of t wait for their reads only, not for the next write
-#pragma unroll
-    for (int q = 0; q < G::DLD; ++q) *reinterpret_cast<bf16x8*>(stage + soff[q]) = ring[0][q];
-    __builtin_amdgcn_sched_barrier(0);
-    if (RING < G::KSTEPS) issue(RING, ring[0]);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-#pragma unroll
-  for (int t = 0; t < G::KSTEPS; ++t) {
-    const char* st = stage + (t & 1) * G::STAGE;
-    const char* kb = in + t * G::KB_BYTES;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[2], bfr[G::NJ];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = read_frag<64, KMAJ>(kb, 16 * i, kk, lane);
-#pragma unroll
-      for (int j = 0; j < G::NJ; ++j) bfr[j] = read_frag<64, KMAJ>(st, 16 * j, kk, lane);
-      {
-        if (kk == 1) {
-          // the next k-step's stage write goes out behind this half's reads: the MFMAs below
-          // wait for the reads only
-          __builtin_amdgcn_sched_barrier(0);
-          if (t + 1 < G::KSTEPS) {
-            char* nx = stage + ((t + 1) & 1) * G::STAGE;
-#pragma unroll
-            for (int q = 0; q < G::DLD; ++q) *reinterpret_cast<bf16x8*>(nx + soff[q]) = ring[(t + 1) % RING][q];
-            __builtin_amdgcn_sched_barrier(0);
-            if (t + 1 + RING < G::KSTEPS) issue(t + 1 + RING, ring[(t + 1) % RING]);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < G::NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    }
-  }
-  __syncthreads();   // in place: every wave has read the whole input image
-  // lane holds out[16i + (lane & 15)][n0 + 16j + 4(lane >> 4) .. +3]
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < G::NJ; ++j) {
-      const f32x4 v = acc[i][j] + bv[j];
-      bf16x4 o;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = (bf16)act_fwd_t<ACT>(v[r]);
-      *reinterpret_cast<bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * j + 4 * (lane >> 4))) = o;
-    }
-}
-
-// One activation-gradient layer: out = (in . W) * act'(aux), in = dZ_l (image), aux = a_{l-1}
-// rows of this band in global memory (written by this block's earlier copy-out).
-template <int H, int ACT, int RING = RB_RING>
-__device__ __forceinline__ void rb_dgrad(const bf16* __restrict__ W, const char* in, char* out,
-                                         char* stage, const bf16* aux, int nvalid, int w, int lane) {
-  using G = RbGeom<H>;
-  const int n0 = w * G::WCOLS;
-  f32x4 acc[2][G::NJ];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < G::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
-  // stage chunk q of k-step t: W[64t + (lane >> 3) + 8q][n0 + 8(lane & 7) .. +7] -> XMAJ image
-  const bf16* wp = W + (long long)(lane >> 3) * H + n0 + 8 * (lane & 7);
-  int soff[G::DLD];
-#pragma unroll
-  for (int q = 0; q < G::DLD; ++q) {
-    const int k = (lane >> 3) + 8 * q, ch = lane & 7;
-    soff[q] = k * (G::WCOLS * 2) + ((ch ^ swz_x<G::WCOLS>(k)) << 4);
-  }
-  bf16x8 ring[RING][G::DLD];
-  auto issue = [&](int t, bf16x8 (&dst)[G::DLD]) {
-#pragma unroll
-    for (int q = 0; q < G::DLD; ++q)
-      dst[q] = *reinterpret_cast<const bf16x8*>(wp + (long long)(64 * t + 8 * q) * H);
-  };
-  // the epilogue's saved activations, loaded up front (their latency hides under the main loop)
-  bf16x4 ax[2][G::NJ];
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < G::NJ; ++j) {
-      const int m = min(16 * i + (lane & 15), nvalid - 1);
-      ax[i][j] = *reinterpret_cast<const bf16x4*>(aux + (long long)m * H + n0 + 16 * j + 4 * (lane >> 4));
-    }
-#pragma unroll
-  for (int s = 0; s < RING; ++s) issue(s, ring[s]);
-  __builtin_amdgcn_sched_barrier(0);
-  {
-#pragma unroll
-    for (int q = 0; q < G::DLD; ++q) *reinterpret_cast<bf16x8*>(stage + soff[q]) = ring[0][q];
-    __builtin_amdgcn_sched_barrier(0);
-    if (RING < G::KSTEPS) issue(RING, ring[0]);
-    __builtin_amdgcn_sched_barrier(0);
-  }
-#pragma unroll
-  for (int t = 0; t < G::KSTEPS; ++t) {
-    const char* st = stage + (t & 1) * G::STAGE;
-    const char* kb = in + t * G::KB_BYTES;
-#pragma unroll
-    for (int kk = 0; kk < 2; ++kk) {
-      bf16x8 af[2], bfr[G::NJ];
-#pragma unroll
-      for (int i = 0; i < 2; ++i) af[i] = read_frag<64, KMAJ>(kb, 16 * i, kk, lane);
-#pragma unroll
-      for (int j = 0; j < G::NJ; ++j) bfr[j] = read_frag<G::WCOLS, XMAJ>(st, 16 * j, kk, lane);
-      {
-        if (kk == 1) {
-          // the next k-step's stage write goes out behind this half's reads: the MFMAs below
-          // wait for the reads only
-          __builtin_amdgcn_sched_barrier(0);
-          if (t + 1 < G::KSTEPS) {
-            char* nx = stage + ((t + 1) & 1) * G::STAGE;
-#pragma unroll
-            for (int q = 0; q < G::DLD; ++q) *reinterpret_cast<bf16x8*>(nx + soff[q]) = ring[(t + 1) % RING][q];
-            __builtin_amdgcn_sched_barrier(0);
-            if (t + 1 + RING < G::KSTEPS) issue(t + 1 + RING, ring[(t + 1) % RING]);
-          }
-          __builtin_amdgcn_sched_barrier(0);
-        }
-      }
-#pragma unroll
-      for (int i = 0; i < 2; ++i)
-#pragma unroll
-        for (int j = 0; j < G::NJ; ++j)
-          acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[j], af[i], acc[i][j], 0, 0, 0);
-    }
-  }
-  __syncthreads();   // in place: every wave has read the whole input image
-#pragma unroll
-  for (int i = 0; i < 2; ++i)
-#pragma unroll
-    for (int j = 0; j < G::NJ; ++j) {
-      bf16x4 o;
-#pragma unroll
-      for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc[i][j][r] * act_bwd_t<ACT>((float)ax[i][j][r]));
-      *reinterpret_cast<bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * j + 4 * (lane >> 4))) = o;
-    }
-}
-
-// The band's head weight/bias-gradient and loss partials: column k of wslab by thread k, rows in
-// order (deterministic), from the per-row dlogits / squared errors in LDS.
-template <int H>
-__device__ __forceinline__ void rb_head_partials(const RowbandArgs& p, const char* act,
-                                                 const float* dls, const float* lss, int tid,
-                                                 int blk) {
-  for (int k = tid; k < H; k += RB_THREADS) {
-    float s = 0.f;
-#pragma unroll 8
-    for (int r = 0; r < RB_ROWS; ++r) s += dls[r] * (float)*reinterpret_cast<const bf16*>(act + rb_off(r, k));
-    p.wslab[(long long)blk * H + k] = s;
-  }
-  if (tid == 0) {
-    float b = 0.f, l = 0.f;
-    for (int r = 0; r < RB_ROWS; ++r) {
-      b += dls[r];
-      l += lss[r];
-    }
-    p.bslab[blk] = b;
-    p.loss_part[blk] = l;
-  }
-}
-
-// Regression head (out == 1, MSE) on the band's last activations `in`: logit, loss, dlogit, the
-// head's weight/bias-gradient partials of this band, and dZ_{L-2} = dl * w * act'(a) into `out`.
-template <int H, int ACT>
-__device__ __forceinline__ void rb_head(const RowbandArgs& p, const char* in, char* out, float* dls,
-                                        float* lss, int row0, int nvalid, int tid) {
-  constexpr int CPT = H / 8 / 16;   // 8-column chunks per thread (16 threads per row)
-  const int r = tid >> 4, g = tid & 15;
-  float a[CPT][8], wv[CPT][8];
-  float dot = 0.f;
-#pragma unroll
-  for (int c = 0; c < CPT; ++c) {
-    const int k = 8 * (g + 16 * c);
-    const bf16x8 v = *reinterpret_cast<const bf16x8*>(in + rb_off(r, k));
-    const float4 w0 = *reinterpret_cast<const float4*>(p.wh + k);
-    const float4 w1 = *reinterpret_cast<const float4*>(p.wh + k + 4);
-    wv[c][0] = w0.x; wv[c][1] = w0.y; wv[c][2] = w0.z; wv[c][3] = w0.w;
-    wv[c][4] = w1.x; wv[c][5] = w1.y; wv[c][6] = w1.z; wv[c][7] = w1.w;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) {
-      a[c][e] = (float)v[e];
-      dot += a[c][e] * wv[c][e];
-    }
-  }
-#pragma unroll
-  for (int sh = 8; sh >= 1; sh >>= 1) dot += __shfl_xor(dot, sh, 64);
-  const bool valid = r < nvalid;
-  const float yv = p.y[row0 + min(r, nvalid - 1)];
-  const float d = dot + p.bh[0] - yv;
-  const float dl = valid ? 2.f * d * p.inv_count : 0.f;
-  if (g == 0) {
-    dls[r] = dl;
-    lss[r] = valid ? d * d : 0.f;
-  }
-  {
-    // in place: the band's weight-gradient partial reads the activations before dZ replaces them
-    __syncthreads();
-    rb_head_partials<H>(p, in, dls, lss, tid, blockIdx.x);
-    __syncthreads();
-  }
-#pragma unroll
-  for (int c = 0; c < CPT; ++c) {
-    const int k = 8 * (g + 16 * c);
-    bf16x8 o;
-#pragma unroll
-    for (int e = 0; e < 8; ++e) o[e] = (bf16)(dl * wv[c][e] * act_bwd_t<ACT>(a[c][e]));
-    *reinterpret_cast<bf16x8*>(out + rb_off(r, k)) = o;
-  }
-}
-
-// The band's whole chain.  ONE activation image, updated in place by every pass (a barrier
-// between a pass's main loop and its epilogue), and two 8 KiB stage buffers per wave: the whole
-// 160 KiB LDS.  (Two ping-pong images + one stage buffer per wave: 0.0815-0.0819 vs 0.0804-0.0808
-// ms/step, profiles/r3s2_rowband_inplace_db_ab.txt.)
-template <int H, int ACT, int RING = RB_RING>
-__global__ void __launch_bounds__(RB_THREADS) rowband_kernel(RowbandArgs p) {
-  using G = RbGeom<H>;
-  extern __shared__ __attribute__((aligned(1024))) char smem[];
-  const int tid = threadIdx.x, lane = tid & 63;
-  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  char* img = smem;
-  char* stage = smem + G::BUF + w * 2 * G::STAGE;
-  // head scratch: wave 0's stage, idle between the last forward pass and the first dgrad
-  float* dls = reinterpret_cast<float*>(smem + G::BUF);
-  float* lss = dls + RB_ROWS;
-  const int blk = blockIdx.x;
-  const int row0 = blk * RB_ROWS;
-  const int nvalid = min(RB_ROWS, p.rows - row0);
-  const int nh = p.nh;
-  const int cg = (w + blk) & (RB_WAVES - 1);
-
-  rb_load_in<H>(img, p.X + (long long)row0 * p.ldx, p.ldx, nvalid, tid);
-  __syncthreads();
-  for (int l = 0; l < nh; ++l) {
-    rb_forward<H, ACT, RING>(p.W[l], p.b[l], img, img, stage, cg, lane);
-    __syncthreads();
-    rb_copy_out<H>(img, p.a[l] + (long long)row0 * H, H, nvalid, tid);
-  }
-  // (the partials' reads and the dZ writes are ordered by the head's own barriers; the stage
-  // scratch is free: every wave has passed the last forward pass's barriers)
-  rb_head<H, ACT>(p, img, img, dls, lss, row0, nvalid, tid);
-  __syncthreads();
-  rb_copy_out<H>(img, p.dz[nh - 1] + (long long)row0 * H, H, nvalid, tid);
-  for (int l = nh - 1; l >= 1; --l) {
-    rb_dgrad<H, ACT, RING>(p.W[l], img, img, stage, p.a[l - 1] + (long long)row0 * H, nvalid, cg, lane);
-    __syncthreads();
-    rb_copy_out<H>(img, p.dz[l - 1] + (long long)row0 * H, H, nvalid, tid);
+    if (r < nvalid) store16(reinterpret_cast<bf16x8*>(dst + (long long)r * ld + kb * 64 + k8 * 8), v, pol);
   }
 }
 
@@ -537,35 +199,6 @@ __device__ __forceinline__ void rb2_mainloop(bf16x8 (&ring)[D][Rb2Geom<H>::NF],
   } while (s0 < cur.ks);
 }
 
-// The band's input rows into the image (runtime width, a multiple of 128 up to 1024): all of a
-// thread's loads are issued before any LDS write, so they are in flight together.  Every load
-// issues unconditionally (past the width: the chunk of iteration 0 again, an L1 hit) -- a load
-// guarded by the runtime width made hipcc wait for each one separately.
-__device__ __forceinline__ void rb2_load_in(char* img, const bf16* src, int ld, int width, int nvalid, int tid) {
-  constexpr int MAXIT = 1024 * RB_ROWS / 8 / RB_THREADS;   // 8
-  const int nit = width * RB_ROWS / 8 / RB_THREADS;
-  bf16x8 v[MAXIT];
-#pragma unroll
-  for (int it = 0; it < MAXIT; ++it) {
-    const int id = tid + min(it, nit - 1) * RB_THREADS;
-    const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
-    v[it] = *reinterpret_cast<const bf16x8*>(src + (long long)min(r, nvalid - 1) * ld + kb * 64 + k8 * 8);
-  }
-#pragma unroll
-  for (int it = 0; it < MAXIT; ++it) {
-    if (it < nit) {
-      const int id = tid + it * RB_THREADS;
-      const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
-      bf16x8 x = v[it];
-      if (r >= nvalid) {
-#pragma unroll
-        for (int e = 0; e < 8; ++e) x[e] = (bf16)0.f;
-      }
-      *reinterpret_cast<bf16x8*>(img + kb * (RB_ROWS * 128) + kmaj_off(r, k8)) = x;
-    }
-  }
-}
-
 // LDS parameter block after the activation slots (floats): every bias, the head weight, the
 // band's targets, the head bias and the head's per-row scratch.  Loaded once at kernel start:
 // a global load issued after the ring's refills would make its wait drain the whole ring.
@@ -591,11 +224,71 @@ __device__ __forceinline__ Rb2Par rb2_par(char* base, int H, int nh) {
   return q;
 }
 
+// The band's head weight/bias-gradient and loss partials (deterministic): column pair
+// (2c, 2c+1) by lanes l and l + 32 of one wave -- rows 0..15 and 16..31, 4-byte LDS reads -- then
+// one shuffle adds the two halves; the bias and loss partials by one 32-lane shuffle tree.  (One
+// thread per column over all 32 rows with 2-byte reads, plus one thread summing the 32 bias and
+// loss terms serially, took ~2.5 us of the head: profiles/r5_rowband_stamps.txt.)
+template <int H>
+__device__ __forceinline__ void rb2_head_partials(const RowbandArgs& p, const char* act,
+                                                  const float* dls, const float* lss, int tid,
+                                                  int band) {
+  const int lane = tid & 63, h = lane >> 5;
+  float dl[16];
+#pragma unroll
+  for (int i = 0; i < 16; i += 4) {
+    const f32x4 d4 = *reinterpret_cast<const f32x4*>(dls + 16 * h + i);
+#pragma unroll
+    for (int e = 0; e < 4; ++e) dl[i + e] = d4[e];
+  }
+#pragma unroll
+  for (int it = 0; it < (H / 2 + RB_THREADS / 2 - 1) / (RB_THREADS / 2); ++it) {
+    const int c = (tid >> 6) * 32 + (lane & 31) + it * (RB_THREADS / 2);   // column pair
+    if (c < H / 2) {
+      const int k = 2 * c;
+      const char* base = act + (k >> 6) * (RB_ROWS * 128) + ((k & 7) << 1);
+      float s0 = 0.f, s1 = 0.f;
+#pragma unroll
+      for (int i = 0; i < 16; ++i) {
+        const int r = 16 * h + i;
+        const bf16x2 v = *reinterpret_cast<const bf16x2*>(base + kmaj_off(r, (k >> 3) & 7));
+        s0 = fmaf(dl[i], (float)v[0], s0);
+        s1 = fmaf(dl[i], (float)v[1], s1);
+      }
+      s0 += __shfl_xor(s0, 32, 64);
+      s1 += __shfl_xor(s1, 32, 64);
+      if (h == 0) {
+        float2 o;
+        o.x = s0;
+        o.y = s1;
+        *reinterpret_cast<float2*>(p.wslab + (long long)band * H + k) = o;
+      }
+    }
+  }
+  if (tid < 64) {
+    float b = tid < RB_ROWS ? dls[tid] : 0.f, l = tid < RB_ROWS ? lss[tid] : 0.f;
+#pragma unroll
+    for (int sh = 16; sh >= 1; sh >>= 1) {
+      b += __shfl_xor(b, sh, 64);
+      l += __shfl_xor(l, sh, 64);
+    }
+    if (tid == 0) {
+      p.bslab[band] = b;
+      p.loss_part[band] = l;
+    }
+  }
+}
+
 // Regression head of the band (out == 1, MSE) in place on `z` = a_{nh-1}: logit, loss, dlogit,
 // the band's head-gradient partials, then dZ_{nh-1} = dl * w * act'(a) over a.
-template <int H, int ACT>
+// LDS bytes of the v2 kernel: the activation slots and the parameter block (8-byte aligned)
+__host__ __device__ __forceinline__ int rb2_smem_core(int H, int in, int nh) {
+  return (((nh > 2 ? nh : 2) * RB_ROWS * (H > in ? H : in) * 2 + rb2_par_bytes(H, nh)) + 7) & ~7;
+}
+
+template <int H, int ACT, typename Stamp, typename Flush>
 __device__ __forceinline__ void rb2_head(const RowbandArgs& p, char* z, const Rb2Par& q, int nvalid, int tid,
-                                         int band) {
+                                         int band, Stamp&& stamp, Flush&& flush) {
   constexpr int CPT = H / 8 / 16;   // 8-column chunks per thread (16 threads per row)
   const int r = tid >> 4, g = tid & 15;
   // (a and w are re-read from the LDS for the dZ pass instead of held: the weight ring is live
@@ -621,9 +314,14 @@ __device__ __forceinline__ void rb2_head(const RowbandArgs& p, char* z, const Rb
     q.dls[r] = dl;
     q.lss[r] = valid ? d * d : 0.f;
   }
+  flush();   // the last forward layer's copy-out, before dZ replaces a (behind the next barrier)
+  stamp();
   __syncthreads();
-  rb_head_partials<H>(p, z, q.dls, q.lss, tid, band);
+  stamp();
+  rb2_head_partials<H>(p, z, q.dls, q.lss, tid, band);
+  stamp();
   __syncthreads();   // every partial has read a before dZ replaces it
+  stamp();
 #pragma unroll
   for (int c = 0; c < CPT; ++c) {
     const int k = 8 * (g + 16 * c);
@@ -641,12 +339,35 @@ __device__ __forceinline__ void rb2_head(const RowbandArgs& p, char* z, const Rb
   }
 }
 
-template <int H, int ACT, int D>
+// Diagnostic phase stamps (ST, rowband_stamps != null; scripts/r5_rb_stamps.py): lane 0 of every
+// wave records the shader-clock counter (s_memtime) at each phase boundary into an LDS table after
+// the parameter block, copied to stamps[band][wave][RB_NST] at exit (slot RB_NST - 2 / - 1: the
+// 100 MHz real-time counter at entry / exit, wave 0).  Never instantiated on the training path.
+constexpr int RB_NST = 48;
+
+template <int H, int ACT, int D, bool ST = false>
 __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
   using G = Rb2Geom<H>;
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  unsigned long long* stl = nullptr;
+  int si = 0;
+  if constexpr (ST) {
+    stl = reinterpret_cast<unsigned long long*>(smem + rb2_smem_core(H, p.in, p.nh)) + w * RB_NST;
+    if (lane == 0 && w == 0) {
+      stl[RB_NST - 2] = __builtin_amdgcn_s_memrealtime();
+      stl[RB_NST - 4] = __builtin_amdgcn_s_getreg(20 | (31 << 11));   // XCC id
+      stl[RB_NST - 3] = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW id
+    }
+  }
+  auto stamp = [&]() {
+    if constexpr (ST) {
+      if (lane == 0 && si < RB_NST - 4) stl[si] = __builtin_amdgcn_s_memtime();
+      ++si;
+    }
+  };
+  stamp();
   const int blk = blockIdx.x;
   // band_map 1: the 32 blocks an XCD runs hold contiguous rows, so the row-split weight
   // gradients that read them next (wgrad_multi: split s's blocks sit on the XCDs that wrote its
@@ -665,24 +386,70 @@ __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
   auto slot = [&](int i) { return smem + i * SL; };
   const Rb2Par q = rb2_par(smem + nslot * SL, H, nh);
 
-  // Startup: the ring's first D k-steps, the band's rows and the small operands are all issued
-  // before the first wait, so the launch pays one memory round trip, not one per operand.
+  // Startup: the small operands (every bias, the head weight, the band's targets, the head
+  // bias) and the band's input rows, THEN the ring's first D k-steps -- all counted asm loads,
+  // so ONE vmcnt(D * NF) retires the operands while the whole ring stays in flight across the
+  // barrier.  (With compiler-issued operand loads behind the ring, hipcc's own vmcnt(0) before
+  // their use drained the ring: half of layer 0's weights fetched before the first MFMA, a
+  // 4.7 us startup -- profiles/r5_rowband_stamps.txt.)
   bf16x8 ring[D][G::NF];
   Rb2Mat cur = rb2_mat<H>(p, 0, cg);
-#pragma unroll
-  for (int d = 0; d < D; ++d) rb2_issue<G::NJ>(ring[d], cur.b, cur.ts, d, lane * 16);
   {
-    // (thread t < H / 4 loads float4 t of every layer's bias and of the head weight; the layer
-    // index is unrolled so each bias pointer is a kernel-argument load, not a memory load of
-    // the pointer array that hipcc would wait for)
+    constexpr int MAXIT = 1024 * RB_ROWS / 8 / RB_THREADS;   // 8: input width <= 1024
+    // (thread t < H / 4 loads float4 t of every layer's bias and of the head weight; the
+    // layer index is unrolled so each bias pointer is a kernel argument)
     f32x4 bq[RB_MAXL], wq;
-    const int tq = min(tid, H / 4 - 1);
+    float yq, bhq;
+    bf16x8 xv[MAXIT];
+    // (only the lanes that own an operand load it: every lane's 16 bytes pass the CU's address
+    // unit, which also feeds the weight stream -- 64 B/clk)
+    if (tid < H / 4) {
 #pragma unroll
-    for (int l = 0; l < RB_MAXL; ++l) bq[l] = reinterpret_cast<const f32x4*>(p.b[l < nh ? l : 0])[tq];
-    wq = reinterpret_cast<const f32x4*>(p.wh)[tq];
-    const float yq = p.y[row0 + min(tid & (RB_ROWS - 1), nvalid - 1)];
-    const float bhq = p.bh[0];
-    rb2_load_in(slot(0), p.X + (long long)row0 * p.ldx, p.ldx, IN, nvalid, tid);
+      for (int l = 0; l < RB_MAXL; ++l)
+        if (l < nh)
+          asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(bq[l]) : "v"(tid * 16), "s"(p.b[l]));
+      asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(wq) : "v"(tid * 16), "s"(p.wh));
+    }
+    if (tid < RB_ROWS)
+      asm volatile("global_load_dword %0, %1, %2" : "=v"(yq) : "v"(min(tid, nvalid - 1) * 4), "s"(p.y + row0));
+    if (tid == 0) asm volatile("global_load_dword %0, %1, %2" : "=v"(bhq) : "v"(0), "s"(p.bh));
+    // the band's rows (past the last valid row that row again -- padding rows are zeroed below)
+    const int nit = IN * RB_ROWS / 8 / RB_THREADS;
+    const bf16* xb = p.X + (long long)row0 * p.ldx;
+#pragma unroll
+    for (int it = 0; it < MAXIT; ++it) {
+      if (it < nit) {
+        const int id = tid + it * RB_THREADS;
+        const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
+        asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(xv[it])
+                     : "v"((min(r, nvalid - 1) * p.ldx + kb * 64 + k8 * 8) * 2), "s"(xb));
+      }
+    }
+    stamp();
+#pragma unroll
+    for (int d = 0; d < D; ++d) rb2_issue<G::NJ>(ring[d], cur.b, cur.ts, d, lane * 16);
+    stamp();
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D * G::NF));
+    stamp();
+#pragma unroll
+    for (int l = 0; l < RB_MAXL; ++l) asm volatile("" : "+v"(bq[l]));
+    asm volatile("" : "+v"(wq), "+v"(yq), "+v"(bhq));
+#pragma unroll
+    for (int it = 0; it < MAXIT; ++it) asm volatile("" : "+v"(xv[it]));
+    char* img = slot(0);
+#pragma unroll
+    for (int it = 0; it < MAXIT; ++it) {
+      if (it < nit) {
+        const int id = tid + it * RB_THREADS;
+        const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
+        bf16x8 x = xv[it];
+        if (r >= nvalid) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] = (bf16)0.f;
+        }
+        *reinterpret_cast<bf16x8*>(img + kb * (RB_ROWS * 128) + kmaj_off(r, k8)) = x;
+      }
+    }
     if (tid < H / 4) {
 #pragma unroll
       for (int l = 0; l < RB_MAXL; ++l)
@@ -691,8 +458,23 @@ __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
     }
     if (tid < RB_ROWS) q.y[tid] = yq;
     if (tid == 0) q.bh[0] = bhq;
+    stamp();
   }
   __syncthreads();
+  stamp();
+
+  // Copy-outs run one phase late: a phase's output image is complete at its closing barrier,
+  // and the NEXT phase's waves copy it out between their epilogue and their own barrier -- the
+  // time a wave that finished its main loop early would otherwise wait there (the waves of a
+  // block end a main loop up to ~1.7 us apart: profiles/r5_rowband_stamps.txt).  No phase
+  // overwrites an image before its copy-out: dZ_{l-1} replaces a_{l-1} one phase after a_{l-1}
+  // was copied, and the head's dZ replaces a_{nh-1} behind the head's own flush.
+  const char* pend_src = nullptr;
+  bf16* pend_dst = nullptr;
+  auto flush = [&]() {
+    if (pend_src) rb_copy_out<H>(pend_src, pend_dst, H, nvalid, tid, p.out_pol);
+    pend_src = nullptr;
+  };
 
   f32x4 acc[2][G::NJ];
   // ---- forward: a_l = act(a_{l-1} W_l^T + b_l) ----
@@ -705,29 +487,41 @@ __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
     const char* in = slot(l == 0 ? 0 : l);
     char* out = l < nh - 1 ? slot(l + 1) : slot(nh >= 2 ? 0 : 1);
     rb2_mainloop<H, D>(ring, acc, in, cur, nxt, lane);
+    stamp();
     // lane holds out[16i + (lane & 15)][n0 + 16j + 4(lane >> 4) .. +3]
     const float* bl = q.bias + l * H + n0 + 4 * (lane >> 4);
+    f32x4 bv[G::NJ];   // (all bias reads issued together: one LDS round trip, not NJ)
+#pragma unroll
+    for (int j = 0; j < G::NJ; ++j) bv[j] = *reinterpret_cast<const f32x4*>(bl + 16 * j);
 #pragma unroll
     for (int j = 0; j < G::NJ; ++j) {
-      const f32x4 bv = *reinterpret_cast<const f32x4*>(bl + 16 * j);
 #pragma unroll
       for (int i = 0; i < 2; ++i) {
-        const f32x4 v = acc[i][j] + bv;
-        bf16x4 o;
+        const f32x4 v = acc[i][j] + bv[j];
+        f32x4 a;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16)act_fwd_t<ACT>(v[r]);
-        *reinterpret_cast<bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * j + 4 * (lane >> 4))) = o;
+        for (int r = 0; r < 4; ++r) a[r] = act_fwd_t<ACT>(v[r]);
+        *reinterpret_cast<bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * j + 4 * (lane >> 4))) =
+            __builtin_convertvector(a, bf16x4);
       }
     }
+    stamp();
+    flush();
+    stamp();
     __syncthreads();
-    rb_copy_out<H>(out, p.a[l] + (long long)row0 * H, H, nvalid, tid);
+    stamp();
+    pend_src = out;
+    pend_dst = p.a[l] + (long long)row0 * H;
     cur = nxt;
   }
   // ---- head (in place on a_{nh-1}) ----
   char* z = slot(nh >= 2 ? 0 : 1);
-  rb2_head<H, ACT>(p, z, q, nvalid, tid, band);
+  rb2_head<H, ACT>(p, z, q, nvalid, tid, band, stamp, flush);
+  stamp();
   __syncthreads();
-  rb_copy_out<H>(z, p.dz[nh - 1] + (long long)row0 * H, H, nvalid, tid);
+  stamp();
+  pend_src = z;
+  pend_dst = p.dz[nh - 1] + (long long)row0 * H;
   // ---- activation gradients: dZ_{l-1} = (dZ_l W_l) * act'(a_{l-1}), in place over a_{l-1} ----
   for (int l = nh - 1; l >= 1; --l) {
     const Rb2Mat nxt = rb2_mat<H>(p, 2 * nh - l, cg);
@@ -737,26 +531,48 @@ __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
       for (int j = 0; j < G::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     char* out = slot(l);   // holds a_{l-1}
     rb2_mainloop<H, D>(ring, acc, z, cur, nxt, lane);
+    stamp();
+    // (every a_{l-1} read issued before the first dZ store: one LDS round trip, not 2 x NJ
+    // read-after-write-ordered ones)
+    bf16x4 ax[2][G::NJ];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < G::NJ; ++j)
+        ax[i][j] = *reinterpret_cast<const bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * j + 4 * (lane >> 4)));
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < G::NJ; ++j) {
-        bf16x4* po = reinterpret_cast<bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * j + 4 * (lane >> 4)));
-        const bf16x4 ax = *po;
-        bf16x4 o;
+        f32x4 o;
 #pragma unroll
-        for (int r = 0; r < 4; ++r) o[r] = (bf16)(acc[i][j][r] * act_bwd_t<ACT>((float)ax[r]));
-        *po = o;
+        for (int r = 0; r < 4; ++r) o[r] = acc[i][j][r] * act_bwd_t<ACT>((float)ax[i][j][r]);
+        *reinterpret_cast<bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * j + 4 * (lane >> 4))) =
+            __builtin_convertvector(o, bf16x4);
       }
+    stamp();
+    flush();
+    stamp();
     __syncthreads();
-    rb_copy_out<H>(out, p.dz[l - 1] + (long long)row0 * H, H, nvalid, tid);
+    stamp();
+    pend_src = out;
+    pend_dst = p.dz[l - 1] + (long long)row0 * H;
     z = out;
     cur = nxt;
   }
+  flush();
+  stamp();
+  if constexpr (ST) {
+    if (lane == 0 && w == 0) stl[RB_NST - 1] = __builtin_amdgcn_s_memrealtime();
+    __syncthreads();
+    const unsigned long long* all = stl - w * RB_NST;
+    for (int i = tid; i < RB_WAVES * RB_NST; i += RB_THREADS)
+      p.stamps[(long long)band * RB_WAVES * RB_NST + i] = all[i];
+  }
 }
 
-static int rb2_smem(int H, int in, int nh) {
-  return std::max(nh, 2) * RB_ROWS * std::max(H, in) * 2 + rb2_par_bytes(H, nh);
+static int rb2_smem(int H, int in, int nh, bool st = false) {
+  return rb2_smem_core(H, in, nh) + (st ? RB_WAVES * RB_NST * 8 : 0);
 }
 
 static bool rowband2_shape_ok(int H, int in, int nh) {
@@ -785,6 +601,22 @@ static hipError_t rowband2_launch(const RowbandArgs& p, hipStream_t s) {
     attr = true;
   }
   const Fn f = fns[p.act == ACT_RELU ? 1 : p.act == ACT_TANH ? 2 : 0];
+  if (p.stamps) {
+    // diagnostic phase stamps: H = 512, relu only
+    if constexpr (H == 512) {
+      if (p.act != ACT_RELU || rb2_smem(H, p.in, p.nh, true) > 160 * 1024) return hipErrorInvalidValue;
+      static bool sattr = false;
+      if (!sattr) {
+        (void)hipFuncSetAttribute((const void*)rowband2_kernel<H, ACT_RELU, D, true>,
+                                  hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+        sattr = true;
+      }
+      hipLaunchKernelGGL((rowband2_kernel<H, ACT_RELU, D, true>), dim3(rowband_blocks(p.rows)),
+                         dim3(RB_THREADS), rb2_smem(H, p.in, p.nh, true), s, p);
+      return hipGetLastError();
+    }
+    return hipErrorInvalidValue;
+  }
   hipLaunchKernelGGL(f, dim3(rowband_blocks(p.rows)), dim3(RB_THREADS), rb2_smem(H, p.in, p.nh), s, p);
   return hipGetLastError();
 }
@@ -848,11 +680,6 @@ hipError_t rowband_pack(const RowbandArgs& p, hipStream_t s) {
 
 int rowband_blocks(int rows) { return (rows + RB_ROWS - 1) / RB_ROWS; }
 
-bool rowband_ok(int rows, int H, int in, int nh, int out, int loss, int act) {
-  return rows > 0 && H == 512 && in == H && nh >= 1 && nh <= RB_MAXL && out == 1 &&
-         loss == LOSS_MSE && (act == ACT_RELU || act == ACT_TANH || act == ACT_NONE);
-}
-
 bool rowband2_ok(int rows, int H, int in, int nh, int out, int loss, int act) {
   return rows > 0 && nh >= 1 && nh <= RB_MAXL && out == 1 && loss == LOSS_MSE &&
          (act == ACT_RELU || act == ACT_TANH || act == ACT_NONE) && rowband2_shape_ok(H, in, nh);
@@ -874,37 +701,36 @@ static int rb_band_map() {
   return g_rb_band_map;
 }
 
+// diagnostic: phase stamps of the v2 kernel into this buffer (rowband_blocks x 8 x RB_NST uint64)
+static unsigned long long* g_rb_stamps = nullptr;
+void set_rowband_stamps(unsigned long long* buf) { g_rb_stamps = buf; }
+int rowband_stamp_slots() { return RB_WAVES * RB_NST; }
+
+// copy-out store policy (RowbandArgs::out_pol): NNMPI_RB_STORE=0/1/2 (experiments)
+static int g_rb_store = -1;
+constexpr int RB_STORE_DEFAULT = 0;
+void set_rb_store_policy(int pol) { g_rb_store = pol; }
+static int rb_store_policy() {
+  if (g_rb_store < 0) g_rb_store = rb_env("NNMPI_RB_STORE", RB_STORE_DEFAULT);
+  return (g_rb_store >= 0 && g_rb_store <= 2) ? g_rb_store : RB_STORE_DEFAULT;
+}
+
 hipError_t rowband_fwd_bwd(const RowbandArgs& p0, hipStream_t s) {
   RowbandArgs p = p0;
   p.band_map = rb_band_map();
-  if (p.Pf[0]) {   // v2: packed weight images
-    if (!rowband2_ok(p.rows, p.H, p.in, p.nh, 1, LOSS_MSE, p.act)) return hipErrorInvalidValue;
-    for (int l = 0; l < p.nh; ++l)
-      if (!p.Pf[l] || (l >= 1 && !p.Pd[l])) return hipErrorInvalidValue;
-    switch (p.H) {
-      case 256: return rowband2_launch<256>(p, s);
-      case 384: return rowband2_launch<384>(p, s);
-      case 512: return rowband2_launch<512>(p, s);
-      case 768: return rowband2_launch<768>(p, s);
-      case 1024: return rowband2_launch<1024>(p, s);
-      default: return hipErrorInvalidValue;
-    }
+  p.out_pol = rb_store_policy();
+  p.stamps = g_rb_stamps;
+  if (!p.Pf[0] || !rowband2_ok(p.rows, p.H, p.in, p.nh, 1, LOSS_MSE, p.act)) return hipErrorInvalidValue;
+  for (int l = 0; l < p.nh; ++l)
+    if (!p.Pf[l] || (l >= 1 && !p.Pd[l])) return hipErrorInvalidValue;
+  switch (p.H) {
+    case 256: return rowband2_launch<256>(p, s);
+    case 384: return rowband2_launch<384>(p, s);
+    case 512: return rowband2_launch<512>(p, s);
+    case 768: return rowband2_launch<768>(p, s);
+    case 1024: return rowband2_launch<1024>(p, s);
+    default: return hipErrorInvalidValue;
   }
-  if (!rowband_ok(p.rows, p.H, p.H, p.nh, 1, LOSS_MSE, p.act)) return hipErrorInvalidValue;
-
-  using G = RbGeom<512>;
-  using Fn = void (*)(RowbandArgs);
-  static const Fn fns[3] = {rowband_kernel<512, ACT_NONE>, rowband_kernel<512, ACT_RELU>,
-                            rowband_kernel<512, ACT_TANH>};
-  static bool attr = false;
-  if (!attr) {
-    for (Fn f : fns)
-      (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, G::SMEM);
-    attr = true;
-  }
-  const Fn f = fns[p.act == ACT_RELU ? 1 : p.act == ACT_TANH ? 2 : 0];
-  hipLaunchKernelGGL(f, dim3(rowband_blocks(p.rows)), dim3(RB_THREADS), G::SMEM, s, p);
-  return hipGetLastError();
 }
 
 // ---- the whole step: row-band launch, grouped weight gradients, grouped combines ----------
@@ -940,9 +766,7 @@ size_t rowband_workspace_bytes(int rows, int H, int in, int nh, int splits) {
 hipError_t rowband_step(const RowbandStep& st0, hipStream_t s) {
   RowbandStep st = st0;
   RowbandArgs& p = st.fb;
-  if (!p.Pf[0]) p.in = p.H;
-  const bool ok = p.Pf[0] ? rowband2_ok(p.rows, p.H, p.in, p.nh, 1, LOSS_MSE, p.act)
-                          : rowband_ok(p.rows, p.H, p.H, p.nh, 1, LOSS_MSE, p.act);
+  const bool ok = p.Pf[0] && rowband2_ok(p.rows, p.H, p.in, p.nh, 1, LOSS_MSE, p.act);
   if (!ok || !st.ws || st.phase < 0 || st.phase > 2) return hipErrorInvalidValue;
   const int H = p.H, nh = p.nh;
   const size_t G = (size_t)rowband_blocks(p.rows);

@@ -321,20 +321,15 @@ class HipOps:
 
     # ---------------- row-band step (rowband.hip) ----------------
     def rowband_version(self, rows: int, widths, act: str, loss: str) -> int:
-        """2: the v2 row-band step (fragment-major weight images) runs this model -- hidden
-        widths all equal (H % 128 == 0, 256..1024), input width % 128 == 0, out == 1, MSE;
-        1: only the v1 kernel (H == in == 512); 0: neither."""
+        """2: the row-band step (fragment-major weight images, rowband.hip) runs this model --
+        hidden widths all equal (H in 256 / 384 / 512 / 768 / 1024), input width % 64 == 0,
+        out == 1, MSE, everything in the LDS; 0: it does not."""
         widths = list(widths)
         if len(widths) < 3 or any(w != widths[1] for w in widths[1:-1]):
             return 0
         H, in_, nh, out = widths[1], widths[0], len(widths) - 2, widths[-1]
         lc, ac = LOSS_CODES.get(loss, -1), ACT_CODES[act]
-        if knob("NNMPI_RB_V2", "1") != "0" and \
-                self.lib.rowband2_ok(int(rows), H, in_, nh, out, lc, ac):
-            return 2
-        if in_ == H and self.lib.rowband_ok(int(rows), H, in_, nh, out, lc, ac):
-            return 1
-        return 0
+        return 2 if self.lib.rowband2_ok(int(rows), H, in_, nh, out, lc, ac) else 0
 
     def rowband_ok(self, rows: int, widths, act: str, loss: str) -> bool:
         """The whole forward + head + activation-gradient chain runs as one launch per step
@@ -389,10 +384,9 @@ class HipOps:
         nh = len(layers)
         H = layers[0][0].shape[0]
         _check(X.dtype == torch.bfloat16 and X.stride(1) == 1, "rowband: bf16 rows")
-        ok = (self.lib.rowband2_ok(rows, H, in_, nh, 1, LOSS_CODES["mse"], ACT_CODES[act])
-              if packed is not None else
-              in_ == H and self.lib.rowband_ok(rows, H, H, nh, 1, LOSS_CODES["mse"], ACT_CODES[act]))
-        _check(ok, "rowband: shape")
+        _check(packed is not None, "rowband: the fragment-major weight images (rowband_packed)")
+        _check(self.lib.rowband2_ok(rows, H, in_, nh, 1, LOSS_CODES["mse"], ACT_CODES[act]),
+               "rowband: shape")
         self._check_ws(ws, self.rowband_workspace_bytes(rows, H, nh, splits, in_), "rowband")
         lay = []
         for l, (W, b, a, dz, gW, gb) in enumerate(layers):

@@ -20,7 +20,6 @@ EXPERIMENTS = "NNMPI_EXPERIMENTS"
 KNOBS = {
     "NNMPI_ROWBAND": "row-band step schedule (0 off)",
     "NNMPI_ROWBAND_MIN_ROWS": "smallest batch that takes the row-band step",
-    "NNMPI_RB_V2": "row-band v2 kernel with fragment-major weight images (0: v1)",
     "NNMPI_RB_SPLITS": "row-band weight-gradient split-K slabs",
     "NNMPI_RB_PLAN": "row-band split-K plan (0 one launch, 1 phased; RowbandStep::plan)",
     "NNMPI_DEFER": "deferred bucket updates in weight-gradient epilogues (0 off)",
@@ -34,6 +33,8 @@ KNOBS = {
     "NNMPI_SGD_SERIAL": "SGD epilogue form",
     "NNMPI_PP_PREFETCH": "SGD-operand prefetch in the 256x256 weight gradient",
     "NNMPI_RB_BANDMAP": "XCD-contiguous band order of the row-band kernel",
+    "NNMPI_RB_STORE": "row-band copy-out store policy (0 plain, 1 nt, 2 sc1)",
+    "NNMPI_RB_STORE": "row-band copy-out store policy (0 plain, 1 nt, 2 sc1)",
     "NNMPI_GEMM": "GEMM main loop (1 register-staged, 2 LDS-DMA)",
     "NNMPI_SLAB_STORE": "split-K slab store policy",
     "NNMPI_GROUP": "grouped backward launch (0 off)",

@@ -31,36 +31,33 @@ def _data(rows, widths, dev="cuda"):
     return X.to(torch.bfloat16), Y
 
 
-_V1_SHAPES = [([512, 512, 512, 512, 1], 1024, "relu"),
-              ([512, 512, 512, 512, 1], 1000, "relu"),
-              ([512, 512, 512, 1], 8191, "relu"),
-              ([512, 512, 1], 37, "relu"),
-              ([512, 512, 512, 512, 1], 777, "tanh"),
-              ([512] * 5 + [1], 2048, "relu")]
-# v2 (fragment-major weight images): other widths, input width != hidden width, 1-4 hidden layers
-_V2_SHAPES = _V1_SHAPES + [([256, 256, 256, 256, 1], 1000, "relu"),
-                           ([768, 768, 768, 1], 555, "tanh"),
-                           ([1024, 1024, 1024, 1], 1024, "relu"),
-                           ([256, 512, 512, 512, 1], 999, "relu"),
-                           ([1024, 512, 512, 1], 640, "tanh"),
-                           ([128, 384, 384, 1], 300, "tanh"),
-                           ([512, 256, 1], 64, "relu")]
+_SHAPES = [([512, 512, 512, 512, 1], 1024, "relu"),
+           ([512, 512, 512, 512, 1], 1000, "relu"),
+           ([512, 512, 512, 1], 8191, "relu"),
+           ([512, 512, 1], 37, "relu"),
+           ([512, 512, 512, 512, 1], 777, "tanh"),
+           ([512] * 5 + [1], 2048, "relu"),
+           # other widths, input width != hidden width, 1-4 hidden layers
+           ([256, 256, 256, 256, 1], 1000, "relu"),
+           ([768, 768, 768, 1], 555, "tanh"),
+           ([1024, 1024, 1024, 1], 1024, "relu"),
+           ([256, 512, 512, 512, 1], 999, "relu"),
+           ([1024, 512, 512, 1], 640, "tanh"),
+           ([128, 384, 384, 1], 300, "tanh"),
+           ([512, 256, 1], 64, "relu")]
 
 
-@pytest.mark.parametrize("version,widths,rows,act", [(1,) + s for s in _V1_SHAPES] +
-                         [(2,) + s for s in _V2_SHAPES])
-def test_rowband_gradients_vs_oracle(version, widths, rows, act, monkeypatch):
+@pytest.mark.parametrize("widths,rows,act", _SHAPES)
+def test_rowband_gradients_vs_oracle(widths, rows, act, monkeypatch):
     """Every layer's weight and bias gradient, the activations, every dZ and the loss of ONE
     row-band step (no optimizer) vs the fp32 oracle: 1e-2 relative norm per tensor (a wrong
     scale on any layer, a missed row of a partial band or a transposed weight operand fails).
-    Version 2 builds the fragment-major weight images first (rowband_pack)."""
+    The fragment-major weight images are built first (rowband_pack)."""
     from nnmpi_amd.ops.hip_ops import HipOps
     from nnmpi_amd.ops.torch_ops import TorchOps
     X, Y = _data(rows, widths)
     out = []
     for dev, ops in (("cuda", HipOps("cuda")), ("cpu", TorchOps("cpu"))):
-        if dev == "cuda":
-            monkeypatch.setenv("NNMPI_RB_V2", "1" if version == 2 else "0")
         spec, ar, eng = _engine(widths, rows, dev, ops, rowband=True, monkeypatch=monkeypatch,
                                 act=act)
         eng.load_batch(X.to(dev), Y.to(dev))
@@ -68,15 +65,14 @@ def test_rowband_gradients_vs_oracle(version, widths, rows, act, monkeypatch):
         L = spec.n_layers
         with torch.no_grad():
             if dev == "cuda":
-                assert ops.rowband_version(rows, widths, act, "mse") == version
-                assert eng.rb_version == version
+                assert ops.rowband_version(rows, widths, act, "mse") == 2
+                assert eng.rb_version == 2
                 layers = [(ar.compute_weight(i), ar.bias(i), eng.acts[i][:rows], eng._dzl(i, rows),
                            ar.grad_weight(i), ar.grad_bias(i)) for i in range(L - 1)]
                 kw = {}
                 with torch.cuda.stream(eng.stream):
-                    if version == 2:
-                        eng._rb_pack()
-                        kw["packed"] = eng.rb_packed
+                    eng._rb_pack()
+                    kw["packed"] = eng.rb_packed
                     ops.rowband_step(eng.X[:rows], layers, ar.weight(L - 1), ar.bias(L - 1),
                                      eng.Y[:rows], eng.inv_count, ar.grad_weight(L - 1),
                                      ar.grad_bias(L - 1), eng.ws_rb, eng.loss_scale, eng.loss_out,

@@ -290,11 +290,7 @@ def test_rowband_host_sizing_invariants():
         prev = need
     # a wider input layer needs a larger first-layer slab
     assert lib.rowband_workspace_bytes(8192, 512, 1024, 3, 0) > cap
-    assert lib.rowband_ok(8192, 512, 512, 3, 1, 0, 1)
-    assert not lib.rowband_ok(8192, 1024, 1024, 3, 1, 0, 1)      # v1: H = 512 only
-    assert not lib.rowband_ok(8192, 512, 784, 3, 1, 0, 1)        # v1: input width = H
-    assert not lib.rowband_ok(8192, 512, 512, 3, 10, 1, 1)       # MSE regression head only
-    assert not lib.rowband_ok(0, 512, 512, 3, 1, 0, 1)
+    assert not lib.rowband2_ok(0, 512, 512, 3, 1, 0, 1)
     # v2 (fragment-major weight images): H in {256, 384, 512, 768, 1024}, input width % 128 == 0,
     # every activation slot + the parameter block in the 160 KiB LDS
     for H, in_, nh in ((512, 512, 3), (512, 512, 4), (256, 256, 4), (384, 128, 2),
