@@ -504,6 +504,7 @@ def run(a, job):
         warm_run["steps"] += ran
 
     tune = None
+    tune_algo = None
     bucket_mb = a.bucket_mb
     chunk_tiles = a.chunk_tiles
     bf16_reduce = None
@@ -539,20 +540,29 @@ def run(a, job):
             e.run_steps(a.warmup, chunk_for(a.warmup))
             tm = min(timed(e, a.tune_steps, chunk_for(a.tune_steps)) for _ in range(2))
             tune[key] = round(tm / a.tune_steps * 1e3, 5)
+            algo = getattr(e.sync, "bf16_reduce" if grad_dtype == "bf16" else "f32_reduce", None)
+            if m != "zero1" and algo:
+                tune_algo[key] = algo
             # every rank sees the same max-over-ranks times, so every rank keeps the same mode
             if eng is None or tm < best_t:
                 eng, best_t, mode, bucket_mb, chunk_tiles = e, tm, key, (bmb or a.bucket_mb), ct
                 bf16_reduce, best = red, (key, m, bmb, ct)
             del e
 
+        tune_algo = {}
         for key, m, bmb, ct in cands:
             try_cand(key, m, bmb, ct)
-        if native_comm is not None and best[1] != "zero1":
-            # the all-reduce algorithm is tuned too, under the chosen schedule: the all-to-all
-            # with the owner's rank-order sum (bf16: acc32, one rounding; fp32: ordered -- the
-            # defaults) vs RCCL's own ring / tree algorithms
-            key, m, bmb, ct = best
-            try_cand(f"{key}+rccl", m, bmb, ct, red="rccl")
+        if native_comm is not None:
+            # the all-reduce algorithm is tuned too, under the TWO fastest all-reduce schedules
+            # (a slow default algorithm must not decide which schedule wins): each one's default
+            # (bf16: acc32, one rounding; fp32: rccl for one bucket, the rank-ordered all-to-all
+            # for several) against the other algorithm
+            ranked = sorted((k for k in tune_algo), key=lambda k: tune[k])[:2]
+            for key in ranked:
+                c = next(c for c in cands if c[0] == key)
+                alt = ("rccl" if tune_algo[key] != "rccl" else
+                       ("acc32" if grad_dtype == "bf16" else "ordered"))
+                try_cand(f"{key}+{alt}", c[1], c[2], c[3], red=alt)
         if gpu:
             torch.cuda.empty_cache()
         # the chosen engine idled while the other candidates ran: warm it again (untimed, like
@@ -725,6 +735,7 @@ def run(a, job):
                        "schedule": step_schedule,
                        "comm_mode": mode_name if use_comm else None,
                        "comm_tune_ms_per_step": tune,
+                       "comm_tune_algorithm": (tune_algo if tune is not None else None),
                        "grad_dtype": grad_dtype if use_comm else None,
                        "bf16_reduce": (sync_algo["bf16"] if use_comm and grad_dtype == "bf16"
                                        else None),

@@ -992,44 +992,39 @@ __device__ __forceinline__ void wg_reg_tile(const GemmParams& p, char* smem, int
                                                                      lane, split, nullptr);
 }
 
-template <int GA, int NS>
-__device__ __forceinline__ void wgrad_multi_body(const WgradMultiParams& g, char* smem, int bid);
-
-template <int GA, int NS>
+// ST: diagnostic per-block stamps (set_wgrad_multi_stamps); the job loop breaks instead of
+// returning so both forms share one body (ST = false is the production kernel, unchanged code)
+template <int GA, int NS, bool ST = false>
 __global__ void __launch_bounds__(GRP_THREADS, NS == 0 ? 2 : 4) wgrad_multi_kernel(WgradMultiParams g) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
-  int bid = blockIdx.x;
-  if (g.stamps) {
+  if constexpr (ST) {
     if (threadIdx.x == 0) {
       g.stamps[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memrealtime();
       g.stamps[blockIdx.x * 4 + 2] = __builtin_amdgcn_s_getreg(20 | (31 << 11));   // XCC id
       g.stamps[blockIdx.x * 4 + 3] = __builtin_amdgcn_s_getreg(4 | (31 << 11));    // HW id
     }
-    wgrad_multi_body<GA, NS>(g, smem, bid);
-    __syncthreads();
-    if (threadIdx.x == 0) g.stamps[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime();
-    return;
   }
-  wgrad_multi_body<GA, NS>(g, smem, bid);
-}
-
-template <int GA, int NS>
-__device__ __forceinline__ void wgrad_multi_body(const WgradMultiParams& g, char* smem, int bid) {
+  int bid = blockIdx.x;
 #pragma unroll
   for (int j = 0; j < RB_MAXL; ++j) {
-    if (j >= g.nj) return;
+    if (j >= g.nj) break;
     if (bid < g.blocks[j]) {
       const int l = xcd_remap(bid, g.blocks[j]);
-      if (l >= g.n[j]) return;
+      if (l >= g.n[j]) break;
       const int split = l / g.tiles[j], t = l % g.tiles[j];
       if constexpr (NS == 0)   // register-staged operands (A/B)
         wg_reg_tile(g.wg[j], smem, t % g.gx[j], t / g.gx[j], split);
       else
-        dma_gemm_tile<GRP_BM, GRP_BN, GRP_WGM, GRP_WGN, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, NS, GA>(
-            g.wg[j], smem, t % g.gx[j], t / g.gx[j], split);
-      return;
+        dma_gemm_tile<GRP_BM, GRP_BN, GRP_WGM, GRP_WGN, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, NS, GA, ST>(
+            g.wg[j], smem, t % g.gx[j], t / g.gx[j], split,
+            ST ? g.stamps + 1024 * 4 + (long long)blockIdx.x * 128 : nullptr);
+      break;
     }
     bid -= g.blocks[j];
+  }
+  if constexpr (ST) {
+    __syncthreads();
+    if (threadIdx.x == 0) g.stamps[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -1087,6 +1082,16 @@ hipError_t wgrad_multi(const WgradArgs* jobs, int nj, const int* splits, SlabRed
   if (!attr[si][ga]) {
     (void)hipFuncSetAttribute((const void*)fns[si][ga], hipFuncAttributeMaxDynamicSharedMemorySize, smem);
     attr[si][ga] = true;
+  }
+  if (g.stamps && si == 0 && ga == 2) {   // diagnostic stamps: the default form only
+    static bool sattr = false;
+    if (!sattr) {
+      (void)hipFuncSetAttribute((const void*)wgrad_multi_kernel<2, 2, true>,
+                                hipFuncAttributeMaxDynamicSharedMemorySize, GRP_SMEM);
+      sattr = true;
+    }
+    hipLaunchKernelGGL((wgrad_multi_kernel<2, 2, true>), dim3(nb), dim3(GRP_THREADS), GRP_SMEM, s, g);
+    return hipGetLastError();
   }
   hipLaunchKernelGGL(fns[si][ga], dim3(nb), dim3(GRP_THREADS), smem, s, g);
   return hipGetLastError();

@@ -617,10 +617,12 @@ struct DmaPlan {
 //      VGPRs: every fragment of the stage is live at once);
 //   2  asm reads + explicit lgkmcnt per 32-deep k-half (half the fragment registers of 1, so
 //      the 512-thread grouped launch keeps 2 blocks per CU).
+// KST (diagnostic, scripts/r5_wg_stamps.py): per k-step shader-clock stamps of wave 0 into kst
+// [3 * t + 0] ring wait done, [3 * t + 1] barrier passed, [3 * t + 2] MFMAs issued (t < 32)
 template <int BM, int BN, int WGM, int WGN, int LA, int LB, int EPI, int ACT, bool BIASGRAD, int NS,
-          int ASYNC_TR = 1>
+          int ASYNC_TR = 1, bool KST = false>
 __device__ __forceinline__ void dma_gemm_tile(const GemmParams& p, char* smem, int tx, int ty,
-                                              int split) {
+                                              int split, unsigned long long* kst = nullptr) {
   constexpr int NW = WGM * WGN;
   constexpr int BK = GEMM_BK;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -688,7 +690,13 @@ __device__ __forceinline__ void dma_gemm_tile(const GemmParams& p, char* smem, i
     } else {
       wait_vm<0>();
     }
+    if constexpr (KST) {
+      if (tid == 0 && t < 32) kst[3 * t] = __builtin_amdgcn_s_memtime();
+    }
     __builtin_amdgcn_s_barrier();
+    if constexpr (KST) {
+      if (tid == 0 && t < 32) kst[3 * t + 1] = __builtin_amdgcn_s_memtime();
+    }
     // refill the stage consumed in iteration t-1 (all waves are past its reads)
     if (t + NS - 1 < nt) {
       char* st = smem + ((t + NS - 1) % NS) * STAGE;
@@ -770,6 +778,9 @@ __device__ __forceinline__ void dma_gemm_tile(const GemmParams& p, char* smem, i
           }
         }
       }
+    }
+    if constexpr (KST) {
+      if (tid == 0 && t < 32) kst[3 * t + 2] = __builtin_amdgcn_s_memtime();
     }
     // all of this wave's LDS reads of stage t are consumed before the next barrier
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");

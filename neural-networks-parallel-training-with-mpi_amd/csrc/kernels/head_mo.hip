@@ -351,7 +351,9 @@ static int head_mo_cap() {
   static int cap = -1;
   if (cap < 0) {
     const char* e = knob_env("NNMPI_HEAD_BLOCKS");
-    cap = (e && atoi(e) > 0) ? atoi(e) : 256;
+    // (clamped to the loss-partial count head_fwd_parts sizes the workspace for, MH_MAX_BLOCKS:
+    // a larger cap would write loss partials past it, into the weight-gradient slabs)
+    cap = (e && atoi(e) > 0) ? std::min(atoi(e), 256) : 256;
   }
   return cap;
 }

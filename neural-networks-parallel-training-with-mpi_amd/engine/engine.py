@@ -120,7 +120,7 @@ class MLPEngine:
         # every combine (+ the fused update on one rank) in a third -- see rowband.hip.  Taken
         # whenever the gradient is reduced after the backward (one rank, the inline all-reduce,
         # ZeRO-1): it produces every layer's gradient at once, so there is nothing for a
-        # per-bucket overlapped schedule to hide.  NNMPI_ROWBAND=0 keeps the grouped schedule
+        # per-bucket overlapped schedule to hide.  NNMPI_EXPERIMENTS=1 NNMPI_ROWBAND=0 keeps the grouped schedule
         # (proxy step 0.082 vs 0.094 ms, profiles/r3s2_rowband_*).
         # rowband_overlap: also with per-bucket collectives on the comm stream -- the band launch
         # and the last hidden layer's + the head's weight gradients first, their bucket's
@@ -169,8 +169,10 @@ class MLPEngine:
         # separate memory-bound pass next to compute-bound GEMMs.  _defer_plan: chunk bucket
         # index -> the partner bucket it updates.
         self._defer_plan: Dict[int, object] = {}
+        # (not for the row-band schedules: they never launch the chunk weight gradients whose
+        # epilogues would apply these updates, so every target bucket would fall to _join_comm)
         if (self._w16 and hasattr(ops, "linear_wgrad_defer") and not self.sharded
-                and knob("NNMPI_DEFER", "1") != "0"):
+                and not self.rb_overlap and knob("NNMPI_DEFER", "1") != "0"):
             for i in range(L - 2):
                 if spec.layer_shape(i) != spec.layer_shape(i + 1):
                     continue

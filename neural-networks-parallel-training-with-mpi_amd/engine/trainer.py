@@ -18,6 +18,7 @@ import dataclasses
 import json
 import math
 import os
+import sys
 import time
 from dataclasses import dataclass, field
 from typing import List, Optional
@@ -355,8 +356,20 @@ def run_worker(cfg: TrainConfig) -> TrainResult:
         j.close()
 
 
+def _warn_ignored_knobs(rank: int):
+    """An NNMPI_* experiment knob in the environment without NNMPI_EXPERIMENTS=1 selects
+    nothing (utils/knobs.py): say so once (rank 0, stderr) instead of ignoring it silently."""
+    from ..utils import knobs
+    ignored = sorted(k for k, v in knobs.seen().items() if not v["honoured"])
+    if ignored and rank == 0:
+        print(f"[nnmpi_amd] warning: {', '.join(ignored)} set but not honoured (experiment knobs "
+              f"need {knobs.EXPERIMENTS}=1)", file=sys.stderr, flush=True)
+    return ignored
+
+
 def _run(j: Job) -> TrainResult:
     cfg, rank, world = j.cfg, j.rank, j.world
+    _warn_ignored_knobs(rank)
     spec = MLPSpec(tuple(cfg.widths), cfg.activation, cfg.loss)
     X, Y, labels, part = build_shard(j)
     # held-out validation rows: the tail of every shard (same rule on every rank, so the

@@ -7,7 +7,7 @@ ATen calls per step for a few hundred flops.  Here the whole step (forward, loss
 one rank the SGD-momentum update) is ONE native call.  With several ranks the update after the
 all-reduce stays TorchOps' (ATen) pass, so the all-reduce and ZeRO-1 paths keep one update
 formula and stay bitwise equal.  Every wider model keeps the TorchOps path, which stays the
-numerics oracle (``NNMPI_CPU_NATIVE=0`` selects it for tiny models too).
+numerics oracle (``NNMPI_EXPERIMENTS=1 NNMPI_CPU_NATIVE=0`` selects it for tiny models too).
 """
 from __future__ import annotations
 

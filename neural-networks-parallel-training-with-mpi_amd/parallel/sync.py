@@ -209,12 +209,16 @@ class NativeRcclSync(GradSync):
         the same contract as the CPU path's round / fp32-sum / round; ``rccl`` is ncclAllReduce
         in bf16, whose ring rounds the partial sum at every one of its P-1 hops (the error
         grows with P: tests/test_multirank_gpu.py::test_rccl_bf16_reduction_error_vs_p).
-        ``f32_reduce`` (fp32 payload): ``ordered`` (default) is the same all-to-all / owner sum
-        / all-gather in fp32 (RcclComm::allreduce_f32_ordered): every element is summed in rank
+        ``f32_reduce`` (fp32 payload): ``ordered`` is the same all-to-all / owner sum /
+        all-gather in fp32 (RcclComm::allreduce_f32_ordered): every element is summed in rank
         order wherever it sits in a bucket, so two schedules that cut the gradient into
-        different buckets (inline vs overlap_rowband) agree bit for bit at any P -- a ring's
-        order depends on the element's chunk, which differs between bucketings at P >= 3;
-        ``rccl`` is ncclAllReduce."""
+        different buckets (inline vs overlap_rowband) agree bit for bit at any P when their
+        per-rank gradients agree (for the row-band schedules: under the same RowbandStep
+        split-K plan, NNMPI_RB_PLAN) -- a ring's order depends on the element's chunk, which
+        differs between bucketings at P >= 3; ``rccl`` is one ncclAllReduce per bucket.  Default
+        (""): ``rccl`` when the gradient is ONE bucket (the inline schedule: nothing to be
+        independent of, and one collective costs less than two grouped all-to-all rounds plus
+        a sum kernel), ``ordered`` when it is cut into several."""
         super().__init__(arena)
         self.mode = mode
         # the root pattern is a serial reduce + broadcast: always on the compute stream
@@ -241,7 +245,8 @@ class NativeRcclSync(GradSync):
         self.bf16_reduce = bf16_reduce or knob("NNMPI_BF16_REDUCE", "acc32")
         if self.bf16_reduce not in ("acc32", "rccl"):
             raise ValueError(f"bf16_reduce must be acc32 or rccl, not {self.bf16_reduce!r}")
-        self.f32_reduce = f32_reduce or knob("NNMPI_F32_REDUCE", "ordered")
+        self.f32_reduce = f32_reduce or knob(
+            "NNMPI_F32_REDUCE", "rccl" if len(arena.buckets) == 1 else "ordered")
         if self.f32_reduce not in ("ordered", "rccl"):
             raise ValueError(f"f32_reduce must be ordered or rccl, not {self.f32_reduce!r}")
         # collective stand-in (measurement only): "k:gbps" holds k CUs on the comm stream after

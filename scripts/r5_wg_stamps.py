@@ -25,31 +25,36 @@ widths = [512, 512, 512, 512, 1]
 spec = MLPSpec(tuple(widths), "relu", "mse")
 arena = Arena([spec.layer_shape(i) for i in range(spec.n_layers)], dev, shadow_dtype=torch.bfloat16)
 arena.bind_model(reference_init(widths))
+graph = os.environ.get("R5_GRAPH", "1") == "1"
 eng = MLPEngine(spec, arena, HipOps(dev), NoSync(arena), device=dev, dtype=torch.bfloat16,
-                rows_capacity=rows, lr=1e-5, momentum=0.9, use_graph=False)
+                rows_capacity=rows, lr=1e-5, momentum=0.9, use_graph=graph)
 X, Y = synth.chunked_regression(0, rows, widths[0], device=dev)
 eng.load_batch(X.to(torch.bfloat16), Y)
 eng.set_scales(1.0 / rows, 1.0 / rows, 1.0)
 lib = native.lib()
-for _ in range(200):
-    eng.step()
-torch.cuda.synchronize()
 NB = 512
-wst = torch.zeros(NB * 4, dtype=torch.int64, device=dev)
+wst = torch.zeros(1024 * 4 + NB * 128, dtype=torch.int64, device=dev)
 nbands = lib.rowband_blocks(rows)
 slots = lib.rowband_stamp_slots()
 NST = slots // 8
 rst = torch.zeros(nbands * slots, dtype=torch.int64, device=dev)
 lib.set_wgrad_multi_stamps(wst.data_ptr())
-lib.set_rowband_stamps(rst.data_ptr())
+if os.environ.get("R5_RBSTAMPS", "0") == "1":
+    lib.set_rowband_stamps(rst.data_ptr())
+# (graph mode: the stamp buffers are baked into the captured launches)
+eng.run_steps(1, 1)
+eng.prepare_steps(16, 16)
+for _ in range(20):
+    eng.run_steps(16, 16)
+torch.cuda.synchronize()
 durs, skews, spans, percu, aligned = [], [], [], [], []
 for it in range(iters):
     wst.zero_()
-    eng.step()
+    eng.run_steps(16, 16)
     torch.cuda.synchronize()
     if it < 3:
         continue
-    w = wst.view(NB, 4).cpu().tolist()
+    w = wst[:NB * 4].view(NB, 4).cpu().tolist()
     w = [r for r in w if r[0] != 0]
     t0 = min(r[0] for r in w)
     spans.append((max(r[1] for r in w) - t0) / 100.0)
@@ -66,7 +71,20 @@ for it in range(iters):
         print(f"block duration: min {d[0]:.2f} p10 {d[len(d)//10]:.2f} median {statistics.median(d):.2f} "
               f"p90 {d[9*len(d)//10]:.2f} max {d[-1]:.2f} us")
         print("max blocks on one CU:", collections.Counter(percu))
-        xcc_of_block = [r[2] & 15 for r in wst.view(NB, 4).cpu().tolist()[:len(w)]]
+        xcc_of_block = [r[2] & 15 for r in wst[:NB * 4].view(NB, 4).cpu().tolist()[:len(w)]]
+        # per k-step phases (wave 0 of each block): ring wait, barrier, LDS reads + MFMA issue
+        k = wst[1024 * 4:].view(NB, 128)[:len(w), :96].view(len(w), 32, 3).double()
+        nt = int((k[0, :, 0] > 0).sum())
+        kk = k[:, :nt]
+        comp = (kk[:, :, 2] - kk[:, :, 1])
+        bar = (kk[:, :, 1] - kk[:, :, 0])
+        wait = kk[:, 1:, 0] - kk[:, :-1, 2]
+        print(f"k-steps {nt}: per k-step median cycles: wait {wait.median():.0f}  barrier "
+              f"{bar.median():.0f}  compute-issue {comp.median():.0f};  wave-0 main loop "
+              f"{(kk[:, -1, 2] - kk[:, 0, 0]).median():.0f} cycles")
+        for t in (0, 1, 2, nt // 2, nt - 1):
+            print(f"   t={t:2d}: wait {(kk[:, t, 0] - (kk[:, t - 1, 2] if t else kk[:, t, 0])).median():6.0f} "
+                  f"bar {bar[:, t].median():6.0f} comp {comp[:, t].median():6.0f}")
         print("wgrad block -> XCC (first 32):", xcc_of_block[:32])
         print("row band -> XCC (first 40):", [int(x) & 15 for x in rb[:40]])
 lib.set_wgrad_multi_stamps(0)

@@ -144,13 +144,17 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
                                                                    "overlap_rowband")
     t = d["config"]["comm_tune_ms_per_step"]
     assert {"inline", "zero1", "overlap", "overlap_rowband"} <= set(t)
-    # fp32 payload: under an all-reduce schedule the ordered all-to-all (default) and RCCL's
-    # ring are both timed and one is recorded (ZeRO-1 reduce-scatters: no algorithm candidate)
+    # fp32 payload: under the two fastest all-reduce schedules both algorithms (the default and
+    # the other one) are timed; the chosen one is recorded (ZeRO-1 reduce-scatters: none)
     assert d["config"]["grad_dtype"] == "fp32"
     zero1 = mode == "zero1"
-    assert len([k for k in t if k.endswith("+rccl")]) == (0 if zero1 else 1), t
-    assert d["config"]["f32_reduce"] == (None if zero1 else
-                                         "rccl" if mode.endswith("+rccl") else "ordered")
+    alg = d["config"]["comm_tune_algorithm"]
+    alts = [k for k in t if "+" in k]
+    assert len(alts) == 2, t
+    for k in alts:
+        base, alt = k.split("+")
+        assert alt in ("rccl", "ordered") and alg[k] == alt != alg[base], (k, alg)
+    assert d["config"]["f32_reduce"] == (None if zero1 else alg[mode]), (mode, alg)
     assert d["parallel_efficiency"] is not None and d["comm_bus_gbps"] is not None
     assert d["strong_scaling"]["global_batch"] == 8192
     assert d["final_loss"] == d["final_loss"]

@@ -461,3 +461,24 @@ def test_xcd_remap_is_a_permutation_with_contiguous_xcd_ranges(nwg):
         for x in range(8):
             mine = sorted(ids[b] for b in range(x, nwg, 8))
             assert mine == list(range(mine[0], mine[0] + len(mine)))
+
+
+def test_knob_without_experiments_switch_is_ignored_and_reported():
+    """Production gating (conftest turns NNMPI_EXPERIMENTS on for the suite, so this runs in a
+    clean subprocess): without NNMPI_EXPERIMENTS=1 a knob keeps its default, and the trainer's
+    check names it on stderr."""
+    import os
+    import subprocess
+    import sys
+    ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    env = {k: v for k, v in os.environ.items() if not k.startswith("NNMPI_")}
+    env["NNMPI_ROWBAND"] = "0"
+    code = ("import sys; sys.path.insert(0, %r)\n"
+            "from nnmpi_amd.utils import knobs\n"
+            "from nnmpi_amd.engine.trainer import _warn_ignored_knobs\n"
+            "assert knobs.knob('NNMPI_ROWBAND', '1') == '1'\n"
+            "assert _warn_ignored_knobs(0) == ['NNMPI_ROWBAND']\n") % ROOT
+    r = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
+                       timeout=300)
+    assert r.returncode == 0, r.stderr[-2000:]
+    assert "NNMPI_ROWBAND set but not honoured" in r.stderr
