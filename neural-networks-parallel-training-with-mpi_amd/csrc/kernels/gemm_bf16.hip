@@ -378,6 +378,7 @@ static int g_group_async = -1;    // grouped-backward LDS read mode (dma_gemm_ti
 static int g_wgrad_splits = 0;    // > 0: upper bound on the weight-gradient split-K factor
 constexpr int FWD_VARIANT_DEFAULT = 0;
 constexpr int GROUP_ASYNC_DEFAULT = 2;   // measured: 102.3 -> 97.9 us/step (proxy512, step_ab)
+constexpr int WGM_ASYNC_DEFAULT = 2;     // wgrad_multi (row-band step); 3 = pipelined k-halves
 void set_fwd_variant(int v) { g_fwd_variant = v; }
 void set_group_async(int m) { g_group_async = m; }
 void set_wgrad_splits(int s) { g_wgrad_splits = s; }
@@ -848,11 +849,27 @@ hipError_t bwd_group(const DgradArgs* dg, const WgradArgs* wg, const SlabReduce*
 // (same tile body, same slab layout as the standalone launch); jobs follow each other in block
 // order, each padded to a multiple of 8 blocks so its XCD remap sees the round-robin XCD
 // assignment.
+// In-launch split-K fixup of one job (FIX): the split that arrives LAST at a tile sums the S
+// partial slabs in split order and applies the update (or stores the gradient).
+struct WgmFix {
+  float* out;    // dW [M][N] (ld N): the gradient's arena position (SGD: the update's operand)
+  float* bout;   // db [M]
+  SgdFuse sg;    // g_base set: apply SGD-momentum at those positions, else store the gradient
+  bf16* pkf;     // with sg: the row-band v2 images of the updated W and W^T (null: none)
+  bf16* pkd;
+  int* cnt;      // one arrival counter per tile: zero between launches (the last arrival resets it)
+  int S;         // splits
+};
+
 struct WgradMultiParams {
   GemmParams wg[RB_MAXL];
   int gx[RB_MAXL], tiles[RB_MAXL], n[RB_MAXL], blocks[RB_MAXL];
   int nj;
   unsigned long long* stamps;   // diagnostic: per block {start, end, XCC id, HW id} (null: off)
+  WgmFix fix[RB_MAXL];          // FIX kernels only
+  int gemm_blocks;              // FIX: blocks past this one run the extra combine `tail`
+  SlabReduce tail;              // (the row-band head's per-band partials)
+  int tail_ws, tail_nb_main, tail_nb_bias;
 };
 // diagnostic (scripts/r5_wg_stamps.py): every later wgrad_multi launch records per-block stamps
 static unsigned long long* g_wgm_stamps = nullptr;
@@ -871,7 +888,7 @@ static int wgm_stages() {   // 0: register-staged operands (NNMPI_WG_REG=1, A/B)
   if (g_wgm_ns < 0) {
     const char* e = knob_env("NNMPI_WG_STAGES");
     const char* r = knob_env("NNMPI_WG_REG");
-    g_wgm_ns = (r && r[0] == '1') ? 0 : (e && e[0] == '4') ? WGM_NS : 2;
+    g_wgm_ns = (r && r[0] == '1') ? 0 : (e && e[0] == '4') ? WGM_NS : (e && e[0] == '3') ? 3 : 2;
   }
   return g_wgm_ns;
 }
@@ -992,11 +1009,248 @@ __device__ __forceinline__ void wg_reg_tile(const GemmParams& p, char* smem, int
                                                                      lane, split, nullptr);
 }
 
+// 16-byte write-through store / L1-bypassing load (the split-K hand-off inside wgrad_multi:
+// MI355X_MICROARCH.md "Valid forms", row 1 -- every store and every load of the handed-off slab
+// bytes is sc1, each storing wave drains vmcnt before the workgroup barrier, one lane's
+// agent-scope atomic add signals, the workgroup whose add returned S - 1 reads)
+__device__ __forceinline__ void st_sc1(float* p, f32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_sc1_f(float* p, float v) {
+  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ f32x4 ld_sc1(const float* p) {
+  f32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ float ld_sc1_f(const float* p) {
+  float v;
+  asm volatile("global_load_dword %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
+// In-launch split-K fixup of a wgrad_multi tile (the grouped tile: 8 waves as 2 x 4, 64 x 32
+// accumulators each, BM = BN = 128), cooperative and deadlock-free:
+//  1. every split publishes its partial slab (LDS-staged rows, write-through stores) and counts
+//     in at the tile's arrival counter (MI355X_MICROARCH.md "Valid forms" row 1: every store and
+//     load of the slab bytes sc1, each storing wave drains vmcnt before the workgroup barrier, one
+//     lane's agent-scope atomic signals);
+//  2. the tile's rows are cut into S portions of whole 8-row groups; portion p belongs to split
+//     p, taken by CAS on its claim word.  The LAST arrival (its add returned S - 1) never waits:
+//     it takes its own portion and then every portion still unclaimed.  An earlier split polls the
+//     counter (bounded, with s_sleep) and, once all S have arrived, claims its own portion; on
+//     timeout it leaves the portion to the last arrival.  So no block ever depends on another
+//     being resident, and each portion is combined exactly once;
+//  3. a portion sums its rows of the S slabs in slab_multi's order (WS interleaved partials from
+//     zero: bitwise the combine launch's result), then applies SGD-momentum (master, momentum,
+//     bf16 shadow, the forward image; the transposed image from the portion restaged through LDS,
+//     one 16-byte piece per lane) or stores the gradient; tiles of the first column also combine
+//     the bias rows of the portion.
+// The counters and claim words (WGM_CW per tile) are zeroed by the row-band launch before every
+// weight-gradient launch (RowbandArgs::zero_words).
+// slab_multi's virtual-wave count for S partial slabs (slab_ws, S <= 64)
+__host__ __device__ __forceinline__ int slab_ws_n(int S) {
+  int ws = 1;
+  while (ws < 16 && ws * 8 < S) ws *= 2;
+  return ws;
+}
+constexpr int WGM_MAXS = 16;       // most splits the fixup takes (more: the combine launch)
+constexpr int WGM_CW = 32;         // counter words per tile: [0] arrivals, [1 + p] portion claims
+constexpr int WGM_SPIN = 400;      // polls of an early split (x ~0.2 us) before it gives up
+__device__ __forceinline__ int ld_sc1_i(const int* p) {
+  int v;
+  asm volatile("global_load_dword %0, %1, off sc1\n s_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
+__device__ __forceinline__ void wgm_portion(const GemmParams& p, const WgmFix& f, char* smem, int tx,
+                                            int ty, int portion) {
+  const int tid = threadIdx.x;
+  const int m0 = ty * GRP_BM, n0 = tx * GRP_BN, M = p.M, N = p.N, S = f.S, WS = slab_ws_n(S);
+  const int g0 = (GRP_BM / 8) * portion / S, g1 = (GRP_BM / 8) * (portion + 1) / S;   // 8-row groups
+  const int r0 = 8 * g0, nr = 8 * (g1 - g0);
+  const long long ss = (long long)M * N;
+  const float* slab = reinterpret_cast<const float*>(p.C);
+  bf16* tb = reinterpret_cast<bf16*>(smem);   // the portion's updated rows, bf16 [nr][128]
+  constexpr int IT = 32 * (GRP_BN / 4) / GRP_THREADS;   // float4 items per thread per 32 rows
+  const bool upd = f.sg.g_base != nullptr;
+  for (int c0 = 0; c0 < nr; c0 += 32) {   // (32-row chunks: one for S >= 4)
+  // every split's values of this thread's items in flight at once, then the sums
+  f32x4 u[IT][WGM_MAXS];
+  int gm[IT], gn[IT];
+  bool ok[IT];
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+    const int e = c0 * (GRP_BN / 4) + tid + k * GRP_THREADS, row = r0 + e / (GRP_BN / 4);
+    gm[k] = m0 + row;
+    gn[k] = n0 + 4 * (e % (GRP_BN / 4));
+    ok[k] = e < nr * (GRP_BN / 4) && gm[k] < M && gn[k] < N;
+#pragma unroll
+    for (int z = 0; z < WGM_MAXS; ++z)
+      if (ok[k] && z < S) u[k][z] = ld_sc1(slab + z * ss + (long long)gm[k] * N + gn[k]);
+  }
+  SgdPre4 pre[IT];
+  if (upd) {
+#pragma unroll
+    for (int k = 0; k < IT; ++k)
+      if (ok[k]) pre[k] = sgd_pre4(f.sg, f.out + (long long)gm[k] * N + gn[k]);
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+  for (int k = 0; k < IT; ++k) {
+#pragma unroll
+    for (int z = 0; z < WGM_MAXS; ++z) asm volatile("" : "+v"(u[k][z]));
+    if (!ok[k]) continue;
+    f32x4 t = {0.f, 0.f, 0.f, 0.f};
+    for (int vw = 0; vw < WS; ++vw) {
+      f32x4 pv = {0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+      for (int z = 0; z < WGM_MAXS; ++z)
+        if (z < S && z % WS == vw) pv += u[k][z];
+      t = vw == 0 ? pv : t + pv;
+    }
+    float* o = f.out + (long long)gm[k] * N + gn[k];
+    if (upd) {
+      const f32x4 pn = sgd_apply4(f.sg, pre[k], t);
+      bf16x4 hv;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) hv[e] = (bf16)pn[e];
+      if (f.pkf) *reinterpret_cast<bf16x4*>(f.pkf + rb_pk_off(gm[k], gn[k], N)) = hv;
+      if (f.pkd) *reinterpret_cast<bf16x4*>(tb + (gm[k] - m0 - r0) * GRP_BN + (gn[k] - n0)) = hv;
+    } else {
+      *reinterpret_cast<f32x4*>(o) = t;
+    }
+  }
+  }
+  // bias rows of the portion (the tiles of the first column hold them)
+  if (p.bias_grad && tx == 0 && tid < nr && m0 + r0 + tid < M) {
+    const int m = m0 + r0 + tid;
+    float bz[WGM_MAXS];
+#pragma unroll
+    for (int z = 0; z < WGM_MAXS; ++z)
+      if (z < S) bz[z] = ld_sc1_f(p.bias_grad + z * p.bg_split_stride + m);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int z = 0; z < WGM_MAXS; ++z) asm volatile("" : "+v"(bz[z]));
+    float b = 0.f;
+    for (int vw = 0; vw < WS; ++vw) {
+      float pb = 0.f;
+#pragma unroll
+      for (int z = 0; z < WGM_MAXS; ++z)
+        if (z < S && z % WS == vw) pb += bz[z];
+      b = vw == 0 ? pb : b + pb;
+    }
+    if (upd) sgd_fused_store(f.sg, f.bout + m, b);
+    else f.bout[m] = b;
+  }
+  if (upd && f.pkd) {
+    // W^T image pieces: column n, rows m .. m+7 of one 8-row group -> 16 contiguous bytes
+    __syncthreads();
+    for (int e = tid; e < (nr / 8) * GRP_BN; e += GRP_THREADS) {
+      const int gi = e / GRP_BN, c = e % GRP_BN, n = n0 + c, m = m0 + r0 + 8 * gi;
+      if (n >= N || m >= M) continue;
+      bf16x8 col;
+#pragma unroll
+      for (int r = 0; r < 8; ++r) col[r] = tb[(8 * gi + r) * GRP_BN + c];
+      *reinterpret_cast<bf16x8*>(f.pkd + rb_pk_off(n, m, M)) = col;
+    }
+  }
+  __syncthreads();   // (the LDS rows may be reused by the next portion)
+}
+
+__device__ __forceinline__ void wgm_fixup(const GemmParams& p, const WgmFix& f, char* smem, int tx,
+                                          int ty, int split, int tile, const f32x4* acc,
+                                          const f32x4* accb) {
+  constexpr int NW = GRP_WGM * GRP_WGN, WM = GRP_BM / GRP_WGM, WN = GRP_BN / GRP_WGN;
+  constexpr int MI = WM / 16, NJ = WN / 16, ITER = GRP_BM / (NW * LEPI_ROWS);
+  const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w / GRP_WGN, wn = w % GRP_WGN;
+  const int m0 = ty * GRP_BM, n0 = tx * GRP_BN, M = p.M, N = p.N, S = f.S;
+  float* img = reinterpret_cast<float*>(smem);
+  // ---- 1. publish this split's slab ----
+  __builtin_amdgcn_s_barrier();   // every wave is past its last read of the DMA ring
+#pragma unroll
+  for (int i = 0; i < MI; ++i)
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) {
+      const int r = wm * WM + i * 16 + (lane & 15);
+      const int c4 = (wn * WN + j * 16) / 4 + (lane >> 4);
+      *reinterpret_cast<f32x4*>(img + lepi_off(r, c4)) = acc[i * NJ + j];
+    }
+  asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  __builtin_amdgcn_s_barrier();
+  const int q = lane & 15, gn = n0 + q * 8;
+  float* slab = reinterpret_cast<float*>(p.C) + split * (long long)M * N;
+#pragma unroll
+  for (int it = 0; it < ITER; ++it) {
+    const int r = (it * NW + w) * LEPI_ROWS + (lane >> 4), gm = m0 + r;
+    const f32x4 v0 = *reinterpret_cast<const f32x4*>(img + lepi_off(r, 2 * q));
+    const f32x4 v1 = *reinterpret_cast<const f32x4*>(img + lepi_off(r, 2 * q + 1));
+    if (gm < M && gn < N) {
+      float* o = slab + (long long)gm * N + gn;
+      st_sc1(o, v0);
+      st_sc1(o + 4, v1);
+    }
+  }
+  if (p.bias_grad && tx == 0 && wn == 0 && (lane >> 4) == 0) {   // the row-sum lanes
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+      const int m = m0 + wm * WM + i * 16 + (lane & 15);
+      if (m < M) st_sc1_f(p.bias_grad + split * p.bg_split_stride + m, accb[i][0]);
+    }
+  }
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();   // every wave's slab stores are complete; the LDS image is free
+  // ---- 2. arrive; the last arrival never waits ----
+  int* cw = f.cnt + tile * WGM_CW;   // [0] arrivals, [1 + p] claim of portion p
+  int* flag = reinterpret_cast<int*>(smem + 60 * 1024);
+  if (tid == 0) {
+    const int old = __hip_atomic_fetch_add(cw, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    int mode = 0;   // 0: leave, 1: own portion, 2: last arrival
+    if (old == S - 1) {
+      mode = 2;
+    } else {
+      int polls = 0;
+      while (ld_sc1_i(cw) < S && ++polls < WGM_SPIN) __builtin_amdgcn_s_sleep(8);
+      if (polls < WGM_SPIN &&
+          __hip_atomic_fetch_add(cw + 1 + split, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0)
+        mode = 1;
+    }
+    if (mode == 2)
+      mode = __hip_atomic_fetch_add(cw + 1 + split, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0 ? 2 : 3;
+    flag[0] = mode;
+  }
+  __syncthreads();
+  const int mode = flag[0];
+  __syncthreads();
+  if (mode == 0) return;
+  // ---- 3. combine ----
+  if (mode == 1 || mode == 2) wgm_portion(p, f, smem, tx, ty, split);
+  if (mode >= 2) {
+    for (int o = 1; o < S; ++o) {
+      const int pp = (split + o) % S;
+      if (tid == 0)
+        flag[0] = __hip_atomic_fetch_add(cw + 1 + pp, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == 0;
+      __syncthreads();
+      const int mine = flag[0];
+      __syncthreads();
+      if (mine) wgm_portion(p, f, smem, tx, ty, pp);
+    }
+  }
+}
+
 // ST: diagnostic per-block stamps (set_wgrad_multi_stamps); the job loop breaks instead of
 // returning so both forms share one body (ST = false is the production kernel, unchanged code)
-template <int GA, int NS, bool ST = false>
-__global__ void __launch_bounds__(GRP_THREADS, NS == 0 ? 2 : 4) wgrad_multi_kernel(WgradMultiParams g) {
+template <int GA, int NS, bool ST = false, bool FIX = false>
+__global__ void __launch_bounds__(GRP_THREADS, (NS == 0 || GA >= 3 || FIX || ST) ? 2 : 4) wgrad_multi_kernel(WgradMultiParams g) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
+  if constexpr (FIX) {
+    if ((int)blockIdx.x >= g.gemm_blocks) {   // the extra combine (row-band head partials)
+      slab_reduce_any(g.tail_ws, g.tail, blockIdx.x - g.gemm_blocks, g.tail_nb_main, g.tail_nb_bias,
+                      reinterpret_cast<f32x4*>(smem));
+      return;
+    }
+  }
   if constexpr (ST) {
     if (threadIdx.x == 0) {
       g.stamps[blockIdx.x * 4 + 0] = __builtin_amdgcn_s_memrealtime();
@@ -1012,12 +1266,19 @@ __global__ void __launch_bounds__(GRP_THREADS, NS == 0 ? 2 : 4) wgrad_multi_kern
       const int l = xcd_remap(bid, g.blocks[j]);
       if (l >= g.n[j]) break;
       const int split = l / g.tiles[j], t = l % g.tiles[j];
-      if constexpr (NS == 0)   // register-staged operands (A/B)
+      unsigned long long* kst = ST ? g.stamps + 1024 * 4 + (long long)blockIdx.x * 128 : nullptr;
+      if constexpr (FIX) {
+        constexpr int MI = GRP_BM / GRP_WGM / 16, NJ = GRP_BN / GRP_WGN / 16;
+        f32x4 acc[MI * NJ], accb[MI];
+        dma_gemm_tile<GRP_BM, GRP_BN, GRP_WGM, GRP_WGN, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, NS, GA, ST,
+                      true>(g.wg[j], smem, t % g.gx[j], t / g.gx[j], split, kst, acc, accb);
+        wgm_fixup(g.wg[j], g.fix[j], smem, t % g.gx[j], t / g.gx[j], split, t, acc, accb);
+      } else if constexpr (NS == 0) {   // register-staged operands (A/B)
         wg_reg_tile(g.wg[j], smem, t % g.gx[j], t / g.gx[j], split);
-      else
+      } else {
         dma_gemm_tile<GRP_BM, GRP_BN, GRP_WGM, GRP_WGN, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, NS, GA, ST>(
-            g.wg[j], smem, t % g.gx[j], t / g.gx[j], split,
-            ST ? g.stamps + 1024 * 4 + (long long)blockIdx.x * 128 : nullptr);
+            g.wg[j], smem, t % g.gx[j], t / g.gx[j], split, kst);
+      }
       break;
     }
     bid -= g.blocks[j];
@@ -1026,6 +1287,43 @@ __global__ void __launch_bounds__(GRP_THREADS, NS == 0 ? 2 : 4) wgrad_multi_kern
     __syncthreads();
     if (threadIdx.x == 0) g.stamps[blockIdx.x * 4 + 1] = __builtin_amdgcn_s_memrealtime();
   }
+}
+
+// Kernel variant of a wgrad_multi launch: DMA ring stages (NNMPI_WG_STAGES 2 / 3 / 4, or 0 =
+// register-staged, NNMPI_WG_REG=1), LDS read mode (dma_gemm_tile ASYNC_TR; NNMPI_WGM_ASYNC or
+// set_group_async), in-launch fixup, diagnostic stamps.
+template <int GA, int NS>
+static void* wgm_fn(bool fix, bool st) {
+  if (fix) return st ? (void*)wgrad_multi_kernel<GA, NS, true, true> : (void*)wgrad_multi_kernel<GA, NS, false, true>;
+  return st ? (void*)wgrad_multi_kernel<GA, NS, true, false> : (void*)wgrad_multi_kernel<GA, NS, false, false>;
+}
+
+static hipError_t wgm_launch(const WgradMultiParams& g, int nb, bool fix, hipStream_t s) {
+  static const int env_ga = [] {
+    const char* e = knob_env("NNMPI_WGM_ASYNC");
+    return (e && e[0] >= '0' && e[0] <= '4') ? e[0] - '0' : -1;
+  }();
+  int ga = g_group_async >= 0 ? std::min(g_group_async, 4) : env_ga >= 0 ? env_ga : WGM_ASYNC_DEFAULT;
+  int ns = wgm_stages();
+  if (fix && ns == 0) ns = 2;          // (the fixup takes the DMA tile only)
+  if (ga < 2) ga = 2;                  // (the compiler-scheduled / whole-stage read modes retired)
+  const bool st = g.stamps != nullptr;
+  void* f = nullptr;
+  if (ns == 0) f = st ? (void*)wgrad_multi_kernel<2, 0, true> : (void*)wgrad_multi_kernel<2, 0>;
+  else if (ns == 3) f = ga == 2 ? wgm_fn<2, 3>(fix, st) : ga == 3 ? wgm_fn<3, 3>(fix, st) : wgm_fn<4, 3>(fix, st);
+  else if (ns == WGM_NS) f = ga == 2 ? wgm_fn<2, WGM_NS>(fix, st) : ga == 3 ? wgm_fn<3, WGM_NS>(fix, st)
+                                                                   : wgm_fn<4, WGM_NS>(fix, st);
+  else f = ga == 2 ? wgm_fn<2, 2>(fix, st) : ga == 3 ? wgm_fn<3, 2>(fix, st) : wgm_fn<4, 2>(fix, st);
+  const int smem = (ns == 0 ? 2 : ns) * (GRP_BM + GRP_BN) * GEMM_BK * 2;
+  static void* attr_done[64] = {};
+  bool seen = false;
+  for (void*& a : attr_done) {
+    if (a == f) { seen = true; break; }
+    if (!a) { a = f; break; }
+  }
+  if (!seen) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, smem);
+  hipLaunchKernelGGL(reinterpret_cast<void (*)(WgradMultiParams)>(f), dim3(nb), dim3(GRP_THREADS), smem, s, g);
+  return hipGetLastError();
 }
 
 int wgrad_multi_splits(int nj, int M, int N, int K) {
@@ -1070,31 +1368,57 @@ hipError_t wgrad_multi(const WgradArgs* jobs, int nj, const int* splits, SlabRed
     nb += g.blocks[j];
   }
   g.stamps = g_wgm_stamps;
-  const int ga = g_group_async >= 0 ? std::min(g_group_async, 2) : GROUP_ASYNC_DEFAULT;
-  const int si = wgm_stages() == 2 ? 0 : wgm_stages() == 0 ? 2 : 1;
-  using Fn = void (*)(WgradMultiParams);
-  static const Fn fns[3][3] = {
-      {wgrad_multi_kernel<0, 2>, wgrad_multi_kernel<1, 2>, wgrad_multi_kernel<2, 2>},
-      {wgrad_multi_kernel<0, WGM_NS>, wgrad_multi_kernel<1, WGM_NS>, wgrad_multi_kernel<2, WGM_NS>},
-      {wgrad_multi_kernel<2, 0>, wgrad_multi_kernel<2, 0>, wgrad_multi_kernel<2, 0>}};
-  static bool attr[3][3] = {};
-  const int smem = si == 1 ? WGM_SMEM : GRP_SMEM;
-  if (!attr[si][ga]) {
-    (void)hipFuncSetAttribute((const void*)fns[si][ga], hipFuncAttributeMaxDynamicSharedMemorySize, smem);
-    attr[si][ga] = true;
+  return wgm_launch(g, nb, false, s);
+}
+
+int wgrad_fix_counters(int M, int N) {
+  return ((M + GRP_BM - 1) / GRP_BM) * ((N + GRP_BN - 1) / GRP_BN) * WGM_CW;
+}
+
+// The row-band step's weight gradients with the in-launch fixup (one launch, no combine launch):
+// jobs as wgrad_multi; fix[j] says where job j's result goes (its out / bout / sg / images; cnt =
+// its tile counters, zero); `tail` (may have S == 0 / null loss): an extra combine run by blocks
+// appended to the grid (the head's per-band partials).
+hipError_t wgrad_multi_fix(const WgradArgs* jobs, int nj, const int* splits, const WgmFixArgs* fix,
+                           const SlabReduce* tail, hipStream_t s) {
+  if (nj < 1 || nj > RB_MAXL) return hipErrorInvalidValue;
+  WgradMultiParams g{};
+  g.nj = nj;
+  int nb = 0;
+  for (int j = 0; j < nj; ++j) {
+    const WgradArgs& a = jobs[j];
+    if (wgrad_tile(a.M, a.N) != 128 || a.db == nullptr || a.ws == nullptr || a.dW16 != nullptr ||
+        !fix[j].cnt)
+      return hipErrorInvalidValue;
+    const int want = (splits && splits[j] > 0) ? splits[j] : wgrad_multi_splits(nj, a.M, a.N, a.K);
+    GemmParams p;
+    SlabReduce pend;
+    const int sp = make_wgrad_s(a, p, pend, want);
+    if (sp > WGM_MAXS) return hipErrorNotSupported;
+    // every split writes its slab (even S == 1: the fixup reads the partial from registers)
+    p.C = a.ws; p.c_split_stride = (long long)a.M * a.N; p.sg = SgdFuse{};
+    p.bias_grad = a.ws + (size_t)sp * a.M * a.N; p.bg_split_stride = a.M;
+    p.c16 = nullptr; p.bg16 = nullptr;
+    set_extents<XMAJ, XMAJ>(p);
+    g.wg[j] = p;
+    g.gx[j] = (p.N + GRP_BN - 1) / GRP_BN;
+    g.tiles[j] = g.gx[j] * ((p.M + GRP_BM - 1) / GRP_BM);
+    g.n[j] = g.tiles[j] * sp;
+    g.blocks[j] = (g.n[j] + 7) & ~7;
+    g.fix[j] = WgmFix{a.dW, a.db, a.sg, fix[j].pkf, fix[j].pkd, fix[j].cnt, sp};
+    nb += g.blocks[j];
   }
-  if (g.stamps && si == 0 && ga == 2) {   // diagnostic stamps: the default form only
-    static bool sattr = false;
-    if (!sattr) {
-      (void)hipFuncSetAttribute((const void*)wgrad_multi_kernel<2, 2, true>,
-                                hipFuncAttributeMaxDynamicSharedMemorySize, GRP_SMEM);
-      sattr = true;
-    }
-    hipLaunchKernelGGL((wgrad_multi_kernel<2, 2, true>), dim3(nb), dim3(GRP_THREADS), GRP_SMEM, s, g);
-    return hipGetLastError();
+  g.gemm_blocks = nb;
+  if (tail && tail->ws && tail->S > 0) {
+    g.tail = *tail;
+    g.tail.sgd_serial = sgd_serial();
+    g.tail_ws = slab_ws(*tail);
+    int nbt = 0;
+    slab_blocks(*tail, g.tail_nb_main, g.tail_nb_bias, nbt);
+    nb += nbt;
   }
-  hipLaunchKernelGGL(fns[si][ga], dim3(nb), dim3(GRP_THREADS), smem, s, g);
-  return hipGetLastError();
+  g.stamps = g_wgm_stamps;
+  return wgm_launch(g, nb, true, s);
 }
 
 struct SlabMultiParams {

@@ -618,11 +618,15 @@ struct DmaPlan {
 //   2  asm reads + explicit lgkmcnt per 32-deep k-half (half the fragment registers of 1, so
 //      the 512-thread grouped launch keeps 2 blocks per CU).
 // KST (diagnostic, scripts/r5_wg_stamps.py): per k-step shader-clock stamps of wave 0 into kst
-// [3 * t + 0] ring wait done, [3 * t + 1] barrier passed, [3 * t + 2] MFMAs issued (t < 32)
+// [4 t] ring wait done, [4 t + 1] barrier passed, [4 t + 2] DMA refill issued, [4 t + 3] MFMAs
+// issued (t < 32)
+// RET: no epilogue -- the accumulators go to acc_out[MI * NJ] / accb_out[MI] (row-major over
+// (i, j)) for a caller-side epilogue (wgrad_multi's in-launch split-K fixup)
 template <int BM, int BN, int WGM, int WGN, int LA, int LB, int EPI, int ACT, bool BIASGRAD, int NS,
-          int ASYNC_TR = 1, bool KST = false>
+          int ASYNC_TR = 1, bool KST = false, bool RET = false>
 __device__ __forceinline__ void dma_gemm_tile(const GemmParams& p, char* smem, int tx, int ty,
-                                              int split, unsigned long long* kst = nullptr) {
+                                              int split, unsigned long long* kst = nullptr,
+                                              f32x4* acc_out = nullptr, f32x4* accb_out = nullptr) {
   constexpr int NW = WGM * WGN;
   constexpr int BK = GEMM_BK;
   constexpr int A_BYTES = BM * BK * 2, B_BYTES = BN * BK * 2, STAGE = A_BYTES + B_BYTES;
@@ -691,21 +695,109 @@ __device__ __forceinline__ void dma_gemm_tile(const GemmParams& p, char* smem, i
       wait_vm<0>();
     }
     if constexpr (KST) {
-      if (tid == 0 && t < 32) kst[3 * t] = __builtin_amdgcn_s_memtime();
+      if (tid == 0 && t < 32) kst[4 * t] = __builtin_amdgcn_s_memtime();
     }
     __builtin_amdgcn_s_barrier();
     if constexpr (KST) {
-      if (tid == 0 && t < 32) kst[3 * t + 1] = __builtin_amdgcn_s_memtime();
+      if (tid == 0 && t < 32) kst[4 * t + 1] = __builtin_amdgcn_s_memtime();
     }
-    // refill the stage consumed in iteration t-1 (all waves are past its reads)
-    if (t + NS - 1 < nt) {
+    // refill the stage consumed in iteration t-1 (all waves are past its reads); ASYNC_TR 4
+    // issues it between the k-halves' MFMAs below instead
+    if (ASYNC_TR != 4 && t + NS - 1 < nt) {
       char* st = smem + ((t + NS - 1) % NS) * STAGE;
       da.issue(rsA, st, w, kbeg + (t + NS - 1) * BK, kend);
       db.issue(rsB, st + A_BYTES, w, kbeg + (t + NS - 1) * BK, kend);
     }
+    if constexpr (KST) {
+      if (tid == 0 && t < 32) kst[4 * t + 2] = __builtin_amdgcn_s_memtime();
+    }
     const char* cur = smem + (t % NS) * STAGE;
     constexpr bool TR = (LA == XMAJ || LB == XMAJ);
-    if constexpr (ASYNC_TR == 2 && TR) {
+    if constexpr (ASYNC_TR == 4 && TR && BK == 64) {
+      // as 3, and the refill's DMA pieces go out between the k-halves' MFMAs: every wave's
+      // pieces pass the CU's address unit (64 B/clk: 512 cycles per 32 KiB stage), so issued
+      // together after the barrier they stalled each wave ~400 cycles before its first MFMA
+      // (profiles/r5_wgrad_kstep_stamps.txt); here the matrix pipe runs meanwhile
+      constexpr int NR = 2 * (MI + NJ);
+      static_assert(NR <= 15, "lgkmcnt counts at most 15 outstanding LDS reads");
+      const bool refill = t + NS - 1 < nt;
+      char* rst = smem + ((t + NS - 1) % NS) * STAGE;
+      bf16x8 af[2][MI], bfr[2][NJ];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) af[kk][i] = read_frag_async<BM, LA>(cur, wm * WM + i * 16, kk, lane);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bfr[kk][j] = read_frag_async<BN, LB>(cur + A_BYTES, wn * WN + j * 16, kk, lane);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        if (refill) {
+          if (kk == 0) da.issue(rsA, rst, w, kbeg + (t + NS - 1) * BK, kend);
+          else db.issue(rsB, rst + A_BYTES, w, kbeg + (t + NS - 1) * BK, kend);
+        }
+        if (kk == 0) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NR) : "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < MI; ++i) asm volatile("" : "+v"(af[kk][i]));
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) asm volatile("" : "+v"(bfr[kk][j]));
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[kk][j], af[kk][i], acc[i][j], 0, 0, 0);
+        if constexpr (BIASGRAD) {
+          if (do_bg) {
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+              accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[kk][i], accb[i], 0, 0, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if constexpr (ASYNC_TR == 3 && TR && BK == 64) {
+      // both k-halves' fragments issued up front; the first half's MFMAs run while the second
+      // half's reads are still in flight (counted lgkmcnt), so a wave's LDS latency overlaps its
+      // own matrix work instead of the SIMD partner's alone.  (Per k-step stamps of the grouped
+      // weight gradient under ASYNC_TR 2: reads + wait + MFMAs 1,444 cycles for 16 + 8 MFMAs,
+      // profiles/r5_wgrad_kstep_stamps.txt.)  Needs the fragment registers of both halves:
+      // 2 x (MI + NJ) x 4 VGPRs.
+      constexpr int NR = 2 * (MI + NJ);   // asm LDS reads per k-half (tr reads: 2 per fragment)
+      static_assert(NR <= 15, "lgkmcnt counts at most 15 outstanding LDS reads");
+      bf16x8 af[2][MI], bfr[2][NJ];
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+#pragma unroll
+        for (int i = 0; i < MI; ++i) af[kk][i] = read_frag_async<BM, LA>(cur, wm * WM + i * 16, kk, lane);
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) bfr[kk][j] = read_frag_async<BN, LB>(cur + A_BYTES, wn * WN + j * 16, kk, lane);
+      }
+#pragma unroll
+      for (int kk = 0; kk < 2; ++kk) {
+        if (kk == 0) asm volatile("s_waitcnt lgkmcnt(%0)" ::"n"(NR) : "memory");
+        else asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+#pragma unroll
+        for (int i = 0; i < MI; ++i) asm volatile("" : "+v"(af[kk][i]));
+#pragma unroll
+        for (int j = 0; j < NJ; ++j) asm volatile("" : "+v"(bfr[kk][j]));
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int i = 0; i < MI; ++i)
+#pragma unroll
+          for (int j = 0; j < NJ; ++j)
+            acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(bfr[kk][j], af[kk][i], acc[i][j], 0, 0, 0);
+        if constexpr (BIASGRAD) {
+          if (do_bg) {
+#pragma unroll
+            for (int i = 0; i < MI; ++i)
+              accb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, af[kk][i], accb[i], 0, 0, 0);
+          }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+      }
+    } else if constexpr (ASYNC_TR == 2 && TR) {
 #pragma unroll
       for (int kk = 0; kk < BK / 32; ++kk) {
         bf16x8 af[MI], bfr[NJ];
@@ -780,10 +872,19 @@ __device__ __forceinline__ void dma_gemm_tile(const GemmParams& p, char* smem, i
       }
     }
     if constexpr (KST) {
-      if (tid == 0 && t < 32) kst[3 * t + 2] = __builtin_amdgcn_s_memtime();
+      if (tid == 0 && t < 32) kst[4 * t + 3] = __builtin_amdgcn_s_memtime();
     }
     // all of this wave's LDS reads of stage t are consumed before the next barrier
     asm volatile("s_waitcnt lgkmcnt(0)" ::: "memory");
+  }
+  if constexpr (RET) {
+#pragma unroll
+    for (int i = 0; i < MI; ++i) {
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc_out[i * NJ + j] = acc[i][j];
+      accb_out[i] = accb[i];
+    }
+    return;
   }
   if constexpr (BM == 128 && BN == 128 && NS * STAGE >= 128 * 128 * 4) {
     if (lepi_ok<EPI>(p)) {

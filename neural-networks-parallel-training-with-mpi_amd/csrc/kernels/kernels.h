@@ -171,8 +171,11 @@ struct RowbandArgs {
                             // contiguous rows), 0 = band b
   unsigned long long* stamps = nullptr;   // v2 diagnostic phase stamps (set_rowband_stamps)
   int out_pol = 0;          // copy-out store policy of a / dZ: 0 plain, 1 nt, 2 sc1 (write-through)
+  int* zero_words = nullptr;   // block 0 zeroes these (the weight-gradient fixup's tile counters)
+  int n_zero = 0;
 };
 void set_rb_store_policy(int pol);   // A/B of RowbandArgs::out_pol (-1: NNMPI_RB_STORE)
+void set_rb_fixup(int on);   // 1: split-K combine inside the weight-gradient launch (default), 0: own launch
 // diagnostic: every later v2 row-band launch records per-wave phase stamps into buf
 // (rowband_blocks(rows) x rowband_stamp_slots() uint64; null = off)
 void set_rowband_stamps(unsigned long long* buf);
@@ -213,6 +216,17 @@ hipError_t wgrad_multi(const WgradArgs* jobs, int nj, const int* splits, SlabRed
                        hipStream_t s);
 // Several independent combines in ONE launch (same per-block body as slab_reduce).
 hipError_t slab_reduce_multi(const SlabReduce* r, int nr, hipStream_t s);
+// The same weight gradients with the split-K combine INSIDE the launch: the split that arrives
+// last at a tile sums the tile's slabs (slab_multi's order: bitwise the same result) and applies
+// the update (job.sg) or stores the gradient (job.dW / job.db), plus the row-band images; `tail`
+// (may be null) is one more combine run by extra blocks of the same launch.
+struct WgmFixArgs {
+  bf16* pkf; bf16* pkd;   // with job.sg: the updated W's fragment-major images (null: none)
+  int* cnt;               // per-tile counter words (wgrad_fix_counters of them), zero
+};
+int wgrad_fix_counters(int M, int N);
+hipError_t wgrad_multi_fix(const WgradArgs* jobs, int nj, const int* splits, const WgmFixArgs* fix,
+                           const SlabReduce* tail, hipStream_t s);
 
 // ---- fp32 GEMM (gemm_f32.hip) ----
 hipError_t linear_fwd_f32(const float* X, int ldx, const float* W, int ldw, const float* bias,

@@ -385,6 +385,9 @@ __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
   const int nslot = max(nh, 2);
   auto slot = [&](int i) { return smem + i * SL; };
   const Rb2Par q = rb2_par(smem + nslot * SL, H, nh);
+  // the next weight-gradient launch's fixup counters (wgrad_multi_fix) start from zero
+  if (blk == 0 && p.zero_words)
+    for (int i = tid; i < p.n_zero; i += RB_THREADS) p.zero_words[i] = 0;
 
   // Startup: the small operands (every bias, the head weight, the band's targets, the head
   // bias) and the band's input rows, THEN the ring's first D k-steps -- all counted asm loads,
@@ -756,11 +759,30 @@ static int rb_max_splits(int splits, int nh, int H, int rows) {
   return std::max(rb_splits(splits, nh, H, rows), rb_splits(0, 1, H, rows));
 }
 
+// per-tile arrival counters of the in-launch fixup (wgrad_multi_fix), one set per layer, after
+// the slabs: zero in a fresh workspace, reset by each tile's last arrival
+static size_t rb_counters(int H, int in) { return rb_pad4((size_t)wgrad_fix_counters(H, std::max(H, in))); }
+
 size_t rowband_workspace_bytes(int rows, int H, int in, int nh, int splits) {
   const size_t G = (size_t)rowband_blocks(rows);
   const int S = rb_max_splits(splits, nh, H, rows);
   const size_t head = G * H + rb_pad4(G) + rb_pad4(G);
-  return (head + (size_t)nh * S * ((size_t)H * std::max(H, in) + H)) * sizeof(float);
+  return (head + (size_t)nh * S * ((size_t)H * std::max(H, in) + H) + (size_t)nh * rb_counters(H, in)) *
+         sizeof(float);
+}
+
+// The split-K combine of the row-band weight gradients: as its own launch (slab_multi, default)
+// or inside the weight-gradient launch (wgrad_multi_fix, NNMPI_RB_FIXUP=1: the tile's splits
+// combine cooperatively once all have arrived).  Bitwise the same results.  Measured on the proxy
+// step: 37.4 us for the fused launch vs 25.4 + 9.1 us for the two (profiles/r5_wgrad_fixup_ab.txt)
+// -- the combine moves the same slab and optimizer bytes at the same per-CU rate either way, and
+// the fused form adds the wait for a tile's last split -- so it stays off.
+static int g_rb_fixup = -1;
+constexpr int RB_FIXUP_DEFAULT = 0;
+void set_rb_fixup(int on) { g_rb_fixup = on; }
+static bool rb_fixup() {
+  if (g_rb_fixup < 0) g_rb_fixup = rb_env("NNMPI_RB_FIXUP", RB_FIXUP_DEFAULT) ? 1 : 0;
+  return g_rb_fixup == 1;
 }
 
 hipError_t rowband_step(const RowbandStep& st0, hipStream_t s) {
@@ -775,12 +797,17 @@ hipError_t rowband_step(const RowbandStep& st0, hipStream_t s) {
   p.bslab = ws + G * H;
   p.loss_part = p.bslab + rb_pad4(G);
   float* slabs = p.loss_part + rb_pad4(G);
+  const size_t per = (size_t)rb_max_splits(st.splits, nh, H, p.rows) * ((size_t)H * std::max(H, p.in) + H);
+  int* cnt = reinterpret_cast<int*>(slabs + (size_t)nh * per);
+  if (rb_fixup()) {
+    p.zero_words = cnt;
+    p.n_zero = nh * (int)rb_counters(H, p.in);
+  }
   hipError_t e = hipSuccess;
   if (st.phase <= 1) {
     e = rowband_fwd_bwd(p, s);
     if (e != hipSuccess) return e;
   }
-  const size_t per = (size_t)rb_max_splits(st.splits, nh, H, p.rows) * ((size_t)H * std::max(H, p.in) + H);
   if (st.plan < 0 || st.plan > 1) return hipErrorInvalidValue;
   // the layers of this phase: [l0, l1); phase 1 also combines the head
   const int l0 = st.phase == 1 ? nh - 1 : 0;
@@ -795,6 +822,21 @@ hipError_t rowband_step(const RowbandStep& st0, hipStream_t s) {
                              st.gb[l], H, l == 0 ? p.in : H, p.rows, slabs + (size_t)l * per, st.sg};
     sp[l - l0] = rb_layer_splits(st.plan, st.splits, nh, H, p.rows, l);
   }
+  const SlabReduce head_red{p.wslab, (int)G, H, 1, H, st.gWh, H, p.bslab, 1, st.gbh, p.loss_part,
+                            (int)G, st.loss_scale, st.loss_out, st.sg};
+  if (nj > 0 && rb_fixup()) {
+    // one launch: every layer's weight gradient, its split-K combine + update in the tile's last
+    // split, and the head's combine in extra blocks
+    WgmFixArgs fx[RB_MAXL];
+    for (int l = l0; l < l1; ++l) {
+      const bool img = st.sg.g_base && p.Pf[0];
+      fx[l - l0] = WgmFixArgs{img ? const_cast<bf16*>(p.Pf[l]) : nullptr,
+                              img && l >= 1 ? const_cast<bf16*>(p.Pd[l]) : nullptr,
+                              cnt + (size_t)l * rb_counters(H, p.in)};
+    }
+    const hipError_t ef = wgrad_multi_fix(jobs, nj, sp, fx, head ? &head_red : nullptr, s);
+    if (ef != hipErrorNotSupported) return ef;   // (more splits than the fixup takes: below)
+  }
   if (nj > 0) {
     e = wgrad_multi(jobs, nj, sp, red, s);
     if (e != hipSuccess) return e;
@@ -808,10 +850,7 @@ hipError_t rowband_step(const RowbandStep& st0, hipStream_t s) {
     }
   }
   int nr = nj;
-  if (head) {
-    red[nr++] = SlabReduce{p.wslab, (int)G, H, 1, H, st.gWh, H, p.bslab, 1, st.gbh, p.loss_part,
-                           (int)G, st.loss_scale, st.loss_out, st.sg};
-  }
+  if (head) red[nr++] = head_red;
   if (nr == 0) return hipSuccess;
   return slab_reduce_multi(red, nr, s);
 }

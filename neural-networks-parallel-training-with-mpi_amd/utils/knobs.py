@@ -34,7 +34,7 @@ KNOBS = {
     "NNMPI_PP_PREFETCH": "SGD-operand prefetch in the 256x256 weight gradient",
     "NNMPI_RB_BANDMAP": "XCD-contiguous band order of the row-band kernel",
     "NNMPI_RB_STORE": "row-band copy-out store policy (0 plain, 1 nt, 2 sc1)",
-    "NNMPI_RB_STORE": "row-band copy-out store policy (0 plain, 1 nt, 2 sc1)",
+    "NNMPI_RB_FIXUP": "row-band split-K combine inside the weight-gradient launch (0: own launch)",
     "NNMPI_GEMM": "GEMM main loop (1 register-staged, 2 LDS-DMA)",
     "NNMPI_SLAB_STORE": "split-K slab store policy",
     "NNMPI_GROUP": "grouped backward launch (0 off)",
@@ -43,6 +43,7 @@ KNOBS = {
     "NNMPI_COMM_STANDIN": "k:gbps -- k CUs held after every bucket collective (standin.hip)",
     "NNMPI_WG_STAGES": "grouped weight-gradient launch DMA ring stages (default 2; 4)",
     "NNMPI_WG_REG": "register-staged operands in the grouped weight-gradient launch (A/B)",
+    "NNMPI_WGM_ASYNC": "LDS read mode of the row-band weight-gradient launch (2; 3 pipelined)",
     "NNMPI_HEAD_BLOCKS": "block cap of the fused multi-output head (default 256)",
     "NNMPI_HEAD_FUSED": "multi-output head + weight gradient in one kernel (0: two launches)",
 }

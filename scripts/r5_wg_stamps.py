@@ -72,19 +72,17 @@ for it in range(iters):
               f"p90 {d[9*len(d)//10]:.2f} max {d[-1]:.2f} us")
         print("max blocks on one CU:", collections.Counter(percu))
         xcc_of_block = [r[2] & 15 for r in wst[:NB * 4].view(NB, 4).cpu().tolist()[:len(w)]]
-        # per k-step phases (wave 0 of each block): ring wait, barrier, LDS reads + MFMA issue
-        k = wst[1024 * 4:].view(NB, 128)[:len(w), :96].view(len(w), 32, 3).double()
+        # per k-step phases (wave 0 of each block): ring wait, barrier, DMA issue, reads + MFMAs
+        k = wst[1024 * 4:].view(NB, 128)[:len(w), :128].view(len(w), 32, 4).double()
         nt = int((k[0, :, 0] > 0).sum())
         kk = k[:, :nt]
-        comp = (kk[:, :, 2] - kk[:, :, 1])
-        bar = (kk[:, :, 1] - kk[:, :, 0])
-        wait = kk[:, 1:, 0] - kk[:, :-1, 2]
+        bar = kk[:, :, 1] - kk[:, :, 0]
+        dma = kk[:, :, 2] - kk[:, :, 1]
+        comp = kk[:, :, 3] - kk[:, :, 2]
+        wait = kk[:, 1:, 0] - kk[:, :-1, 3]
         print(f"k-steps {nt}: per k-step median cycles: wait {wait.median():.0f}  barrier "
-              f"{bar.median():.0f}  compute-issue {comp.median():.0f};  wave-0 main loop "
-              f"{(kk[:, -1, 2] - kk[:, 0, 0]).median():.0f} cycles")
-        for t in (0, 1, 2, nt // 2, nt - 1):
-            print(f"   t={t:2d}: wait {(kk[:, t, 0] - (kk[:, t - 1, 2] if t else kk[:, t, 0])).median():6.0f} "
-                  f"bar {bar[:, t].median():6.0f} comp {comp[:, t].median():6.0f}")
+              f"{bar.median():.0f}  DMA issue {dma.median():.0f}  reads+MFMA {comp.median():.0f};  "
+              f"wave-0 main loop {(kk[:, -1, 3] - kk[:, 0, 0]).median():.0f} cycles")
         print("wgrad block -> XCC (first 32):", xcc_of_block[:32])
         print("row band -> XCC (first 40):", [int(x) & 15 for x in rb[:40]])
 lib.set_wgrad_multi_stamps(0)

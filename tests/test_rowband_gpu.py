@@ -145,6 +145,43 @@ def test_rowband_fused_update_is_bitwise_equal_to_separate_pass(monkeypatch):
     assert res[0][3] == res[1][3]
 
 
+@pytest.mark.parametrize("widths,rows,fuse", [([512, 512, 512, 512, 1], 8192, True),
+                                              ([512, 512, 512, 512, 1], 8192, False),
+                                              ([256, 512, 512, 512, 1], 3000, True),
+                                              ([128, 384, 384, 1], 777, True),
+                                              ([1024, 512, 512, 1], 4096, False),
+                                              ([512, 256, 1], 64, True)])
+def test_rowband_in_launch_fixup_is_bitwise_equal_to_combine_launch(widths, rows, fuse, monkeypatch):
+    """The split-K combine inside the weight-gradient launch (the last split of each tile sums
+    the slabs and applies the update, wgrad_multi_fix) against the separate combine launch
+    (slab_multi): three steps, bitwise-equal master, momentum, shadow, weight images and loss --
+    with the fused update (one rank) and with gradients + the optimizer pass."""
+    from nnmpi_amd import native
+    from nnmpi_amd.ops.hip_ops import HipOps
+    X, Y = _data(rows, widths)
+    res = []
+    lib = native.lib()
+    monkeypatch.setenv("NNMPI_ROWBAND_MIN_ROWS", "1")
+    try:
+        for fix in (1, 0):
+            assert lib.set_rb_fixup(fix)
+            _, ar, eng = _engine(widths, rows, "cuda", HipOps("cuda"), lr=1e-3, momentum=0.9,
+                                 fuse_sgd=fuse, rowband=True, monkeypatch=monkeypatch)
+            assert eng.rowband and eng.uses_rowband(rows)
+            eng.load_batch(X, Y)
+            eng.set_scales(1.0 / rows, 1.0 / rows, 1.0)
+            for _ in range(3):
+                eng.step()
+            eng.synchronize()
+            res.append((ar.master.clone(), ar.momentum.clone(), ar.shadow.clone(),
+                        eng._rb_buf.clone(), eng.loss()))
+    finally:
+        lib.set_rb_fixup(-1)
+    for a, b in zip(res[0][:4], res[1][:4]):
+        assert torch.equal(a, b)
+    assert res[0][4] == res[1][4]
+
+
 @pytest.mark.parametrize("widths", [[512, 512, 512, 512, 1], [256, 256, 256, 1],
                                     [768, 1024, 1024, 1], [384, 384, 384, 1]])
 def test_rowband_fused_update_writes_the_weight_images(widths, monkeypatch):
