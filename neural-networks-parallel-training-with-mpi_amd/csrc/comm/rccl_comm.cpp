@@ -246,6 +246,7 @@ void GradSync::bucket_ready(int b, void* ptr, size_t count, int dtype, hipStream
   if (standin_blocks_ > 0 && standin_gbps_ > 0.0) {
     // a ring all-reduce moves 2 (P-1)/P of the bytes per rank; at P = 8: 1.75
     const double bytes = 1.75 * (double)count * (dtype == 1 ? 2.0 : 4.0);
+    if (!cu_hold) throw std::runtime_error("collective stand-in: experiments build only");
     HIP_THROW(cu_hold(standin_blocks_, bytes / (standin_gbps_ * 1e9), comm_stream_));
   }
 }

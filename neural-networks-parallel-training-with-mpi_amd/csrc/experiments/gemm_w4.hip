@@ -16,7 +16,7 @@
 // tiles needed 128 and hipcc shuffled accumulators through VGPRs: 240 v_accvgpr moves per K
 // tile).  sched_group_barrier pins 1 ds_read per 2 MFMAs.  Not bitwise equal to pp256_tile (a
 // different MFMA shape sums k in 16-deep pieces).
-#include "gemm_tiles.h"
+#include "kernels/gemm_tiles.h"
 
 namespace nnmpi {
 

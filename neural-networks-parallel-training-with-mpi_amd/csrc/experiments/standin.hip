@@ -5,7 +5,7 @@
 // comm kernels on the overlapped wide schedule is measured on a one-GPU box (GradSync::
 // set_standin, knob NNMPI_COMM_STANDIN).  The spin is bounded by construction: every wave
 // leaves once the 100 MHz real-time counter passes start + ticks (ticks clamped to 1 s).
-#include "common.h"
+#include "kernels/common.h"
 
 namespace nnmpi {
 

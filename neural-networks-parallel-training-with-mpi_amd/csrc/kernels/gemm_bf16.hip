@@ -1289,6 +1289,45 @@ __global__ void __launch_bounds__(GRP_THREADS, (NS == 0 || GA >= 3 || FIX || ST)
   }
 }
 
+// Half-width tile of the grouped weight gradient (NNMPI_WGM_TILE=1): 128 (M) x 64 (N), 4 waves
+// of 64 x 32 -- the same per-wave work as the 128 x 128 tile, twice the blocks, so two blocks
+// share each CU and one's DMA / LDS phase runs beside the other's MFMAs (per-k-step stamps of the
+// 128 x 128 tile at one block per CU: wait 320 + barrier 88 + DMA issue 412 + reads and MFMAs
+// 892 cycles, in lockstep -- profiles/r5_wgrad_kstep_stamps.txt).  Same K split, same slab
+// layout, same per-element accumulation order: bitwise the 128 x 128 tile's slabs.
+constexpr int WGH_BM = 128, WGH_BN = 64, WGH_WGM = 2, WGH_WGN = 2;
+constexpr int WGH_THREADS = 64 * WGH_WGM * WGH_WGN;
+constexpr int WGH_SMEM = 2 * (WGH_BM + WGH_BN) * GEMM_BK * 2;
+
+template <int GA>
+__global__ void __launch_bounds__(WGH_THREADS, 2) wgrad_multi_h_kernel(WgradMultiParams g) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  int bid = blockIdx.x;
+#pragma unroll
+  for (int j = 0; j < RB_MAXL; ++j) {
+    if (j >= g.nj) break;
+    if (bid < g.blocks[j]) {
+      const int l = xcd_remap(bid, g.blocks[j]);
+      if (l >= g.n[j]) break;
+      const int split = l / g.tiles[j], t = l % g.tiles[j];
+      dma_gemm_tile<WGH_BM, WGH_BN, WGH_WGM, WGH_WGN, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, 2, GA>(
+          g.wg[j], smem, t % g.gx[j], t / g.gx[j], split);
+      break;
+    }
+    bid -= g.blocks[j];
+  }
+}
+
+static int g_wgm_tile = -1;
+void set_wgm_tile(int t) { g_wgm_tile = t; }   // -1: re-read NNMPI_WGM_TILE
+static int wgm_tile() {
+  if (g_wgm_tile < 0) {
+    const char* e = knob_env("NNMPI_WGM_TILE");
+    g_wgm_tile = (e && e[0] == '1') ? 1 : 0;
+  }
+  return g_wgm_tile;
+}
+
 // Kernel variant of a wgrad_multi launch: DMA ring stages (NNMPI_WG_STAGES 2 / 3 / 4, or 0 =
 // register-staged, NNMPI_WG_REG=1), LDS read mode (dma_gemm_tile ASYNC_TR; NNMPI_WGM_ASYNC or
 // set_group_async), in-launch fixup, diagnostic stamps.
@@ -1361,11 +1400,31 @@ hipError_t wgrad_multi(const WgradArgs* jobs, int nj, const int* splits, SlabRed
     set_extents<XMAJ, XMAJ>(p);
     p.store_pol = slab_store_pol();
     g.wg[j] = p;
-    g.gx[j] = (p.N + GRP_BN - 1) / GRP_BN;
+    const int bn = wgm_tile() == 1 ? WGH_BN : GRP_BN;
+    g.gx[j] = (p.N + bn - 1) / bn;
     g.tiles[j] = g.gx[j] * ((p.M + GRP_BM - 1) / GRP_BM);
     g.n[j] = g.tiles[j] * sp;
     g.blocks[j] = (g.n[j] + 7) & ~7;
     nb += g.blocks[j];
+  }
+  if (wgm_tile() == 1) {
+    static const int env_ga = [] {
+      const char* e = knob_env("NNMPI_WGM_ASYNC");
+      return (e && e[0] >= '2' && e[0] <= '4') ? e[0] - '0' : -1;
+    }();
+    const int ga = env_ga == 3 ? 3 : env_ga == 4 ? 4 : 2;
+    void* f = ga == 3 ? (void*)wgrad_multi_h_kernel<3> : ga == 4 ? (void*)wgrad_multi_h_kernel<4>
+                                                               : (void*)wgrad_multi_h_kernel<2>;
+    static void* attr_done[4] = {};
+    bool seen = false;
+    for (void*& a : attr_done) {
+      if (a == f) { seen = true; break; }
+      if (!a) { a = f; break; }
+    }
+    if (!seen) (void)hipFuncSetAttribute(f, hipFuncAttributeMaxDynamicSharedMemorySize, WGH_SMEM);
+    hipLaunchKernelGGL(reinterpret_cast<void (*)(WgradMultiParams)>(f), dim3(nb), dim3(WGH_THREADS),
+                       WGH_SMEM, s, g);
+    return hipGetLastError();
   }
   g.stamps = g_wgm_stamps;
   return wgm_launch(g, nb, false, s);

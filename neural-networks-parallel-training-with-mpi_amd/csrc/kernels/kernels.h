@@ -54,8 +54,9 @@ enum Loss : int { LOSS_MSE = 0, LOSS_XENT = 1 };
 // ---- GEMM (gemm_bf16.hip) ----
 hipError_t linear_fwd_bf16(const bf16* X, int ldx, const bf16* W, int ldw, const float* bias,
                            bf16* Y, int ldy, int M, int N, int K, int act, hipStream_t s);
-// experiment (gemm_w4.hip): the forward on a 4-wave 256 x 256 tile (M, N % 256, K % 64)
-hipError_t gemm_w4_fwd(const bf16* X, int ldx, const bf16* W, int ldw, const float* bias, bf16* Y,
+// experiment (csrc/experiments/gemm_w4.hip, NNMPI_BUILD_EXPERIMENTS=1 builds only; a weak
+// reference, null otherwise): the forward on a 4-wave 256 x 256 tile (M, N % 256, K % 64)
+__attribute__((weak)) hipError_t gemm_w4_fwd(const bf16* X, int ldx, const bf16* W, int ldw, const float* bias, bf16* Y,
                        int ldy, int M, int N, int K, int act, hipStream_t s);
 hipError_t linear_dgrad_bf16(const bf16* dZ, int lddz, const bf16* W, int ldw, const bf16* Aprev,
                              int lda_prev, bf16* dX, int lddx, int M, int N, int K, int act,
@@ -352,7 +353,10 @@ hipError_t sum_slices_f32(float* out, const float* scratch, int P, int me, long 
                           long long n, hipStream_t s);
 // diagnostic: `blocks` 256-thread blocks holding their CUs (and a full wave's VGPRs) for
 // `seconds` of wall time, then exiting (standin.hip; the collective stand-in)
-hipError_t cu_hold(int blocks, double seconds, hipStream_t s);
+// (csrc/experiments/standin.hip: experiments builds only; weak, null otherwise)
+__attribute__((weak)) hipError_t cu_hold(int blocks, double seconds, hipStream_t s);
+// a stream restricted to a CU mask (csrc/experiments/exp_host.cpp; weak, null otherwise)
+__attribute__((weak)) hipError_t exp_cu_mask_stream(const uint32_t* mask, int words, hipStream_t* out);
 // bitwise replica hash of n 32-bit words; out: 1025 uint64, result at out[1024]
 hipError_t hash_u32(const unsigned* x, long long n, unsigned long long* out, hipStream_t s);
 

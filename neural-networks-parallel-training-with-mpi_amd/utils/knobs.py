@@ -44,6 +44,7 @@ KNOBS = {
     "NNMPI_WG_STAGES": "grouped weight-gradient launch DMA ring stages (default 2; 4)",
     "NNMPI_WG_REG": "register-staged operands in the grouped weight-gradient launch (A/B)",
     "NNMPI_WGM_ASYNC": "LDS read mode of the row-band weight-gradient launch (2; 3 pipelined)",
+    "NNMPI_WGM_TILE": "row-band weight-gradient tile (0: 128x128, 8 waves; 1: 128x64, 4 waves)",
     "NNMPI_HEAD_BLOCKS": "block cap of the fused multi-output head (default 256)",
     "NNMPI_HEAD_FUSED": "multi-output head + weight gradient in one kernel (0: two launches)",
 }

@@ -56,9 +56,14 @@ def test_gemm_identity_asymmetric():
 
 
 def test_cu_mask_stream_runs_kernels_bitwise_equal():
-    """cu_mask_stream (the CU-partitioned concurrency experiment, scripts/r4_cu_split_ab.py): a
-    GEMM on a stream restricted to half the CUs gives the same bits as on the whole chip."""
+    """cu_mask_stream (the CU-partitioned concurrency experiment, scripts/r4_cu_split_ab.py; an
+    experiments-build entry point): a GEMM on a stream restricted to half the CUs gives the same
+    bits as on the whole chip."""
     lib = _lib()
+    if not lib.experiments_built():
+        with pytest.raises(RuntimeError, match="experiments build only"):
+            lib.cu_mask_stream([1])
+        pytest.skip("the production library carries no experiment entry point")
     n_cu = torch.cuda.get_device_properties(0).multi_processor_count
     mask = [0] * ((n_cu + 31) // 32)
     for c in range(0, n_cu, 2):

@@ -182,6 +182,36 @@ def test_rowband_in_launch_fixup_is_bitwise_equal_to_combine_launch(widths, rows
     assert res[0][4] == res[1][4]
 
 
+@pytest.mark.parametrize("widths,rows", [([512, 512, 512, 512, 1], 8192), ([256, 512, 512, 512, 1], 3000),
+                                         ([128, 384, 384, 1], 6500)])
+def test_rowband_half_width_wgrad_tile_is_bitwise_equal(widths, rows, monkeypatch):
+    """The 128 x 64 weight-gradient tile (NNMPI_WGM_TILE=1, two blocks per CU) against the
+    128 x 128 tile: same K split, same accumulation order -- bitwise-equal parameters, momentum
+    and images after three fused-update steps."""
+    from nnmpi_amd import native
+    from nnmpi_amd.ops.hip_ops import HipOps
+    X, Y = _data(rows, widths)
+    res = []
+    lib = native.lib()
+    monkeypatch.setenv("NNMPI_ROWBAND_MIN_ROWS", "1")
+    try:
+        for tile in (1, 0):
+            assert lib.set_wgm_tile(tile)
+            _, ar, eng = _engine(widths, rows, "cuda", HipOps("cuda"), lr=1e-3, momentum=0.9,
+                                 fuse_sgd=True, rowband=True, monkeypatch=monkeypatch)
+            eng.load_batch(X, Y)
+            eng.set_scales(1.0 / rows, 1.0 / rows, 1.0)
+            for _ in range(3):
+                eng.step()
+            eng.synchronize()
+            res.append((ar.master.clone(), ar.momentum.clone(), eng._rb_buf.clone(), eng.loss()))
+    finally:
+        lib.set_wgm_tile(-1)
+    for a, b in zip(res[0][:3], res[1][:3]):
+        assert torch.equal(a, b)
+    assert res[0][3] == res[1][3]
+
+
 @pytest.mark.parametrize("widths", [[512, 512, 512, 512, 1], [256, 256, 256, 1],
                                     [768, 1024, 1024, 1], [384, 384, 384, 1]])
 def test_rowband_fused_update_writes_the_weight_images(widths, monkeypatch):
