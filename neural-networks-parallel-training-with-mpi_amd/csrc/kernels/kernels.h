@@ -174,7 +174,14 @@ struct RowbandArgs {
   int out_pol = 0;          // copy-out store policy of a / dZ: 0 plain, 1 nt, 2 sc1 (write-through)
   int* zero_words = nullptr;   // block 0 zeroes these (the weight-gradient fixup's tile counters)
   int n_zero = 0;
+  // column-split form (small batches, rowband_split_ok): per-band exchange counters + done
+  // counter + error word (zero, self-resetting) and the head's partial-dot exchange buffer
+  int* xsync = nullptr;
+  float* hx = nullptr;
 };
+// the column-split row-band kernel takes this batch (H = 512, in <= 512, rows below the
+// full-band threshold): 8 blocks per 32-row band, each one 64-column slice of every layer
+bool rowband_split_ok(int rows, int H, int in, int nh);
 void set_rb_store_policy(int pol);   // A/B of RowbandArgs::out_pol (-1: NNMPI_RB_STORE)
 void set_rb_fixup(int on);   // 1: split-K combine inside the weight-gradient launch (default), 0: own launch
 // diagnostic: every later v2 row-band launch records per-wave phase stamps into buf

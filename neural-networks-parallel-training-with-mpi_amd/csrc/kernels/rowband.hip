@@ -513,8 +513,10 @@ __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
     stamp();
     __syncthreads();
     stamp();
-    pend_src = out;
-    pend_dst = p.a[l] + (long long)row0 * H;
+    // (a null p.a[l] -- the last hidden layer's activations, which no weight gradient reads --
+    // skips the copy-out)
+    pend_src = p.a[l] ? out : nullptr;
+    pend_dst = p.a[l] ? p.a[l] + (long long)row0 * H : nullptr;
     cur = nxt;
   }
   // ---- head (in place on a_{nh-1}) ----

@@ -153,6 +153,9 @@ class MLPEngine:
         # 1,024 rows as at 8,192, profiles/r3s2_rowband_pmc.txt), so small batches (strong-scaling
         # shards, mini-batches) keep the grouped schedule: 0.053 vs ~0.064 ms at 1,024 rows.
         self.rowband_min_rows = int(knob("NNMPI_ROWBAND_MIN_ROWS", "6144"))
+        # True: the row-band step also copies out the last hidden layer's activations (debug /
+        # inspection; nothing downstream reads them)
+        self.rb_keep_last = False
         if self.is_cuda:
             self.ev_wfree = [torch.cuda.Event(enable_timing=False) for _ in range(L)]
         # bf16-payload overlapped schedule: per-bucket updates read the bf16 payload
@@ -605,7 +608,12 @@ class MLPEngine:
 
     def _rb_layers(self):
         rows, ar = self.rows, self.arena
-        return [(ar.compute_weight(i), ar.bias(i), self.acts[i][:rows], self._dzl(i, rows),
+        # (the last hidden layer's activations are consumed inside the band -- head and its
+        # weight-gradient partials -- so the hot path does not copy them out; evaluation and the
+        # other schedules recompute or write their own)
+        last = self.L - 2
+        return [(ar.compute_weight(i), ar.bias(i),
+                 self.acts[i][:rows] if (i < last or self.rb_keep_last) else None, self._dzl(i, rows),
                  ar.grad_weight(i), ar.grad_bias(i)) for i in range(self.L - 1)]
 
     def _rb_launch(self, sgd=None, phase: int = 0):

@@ -393,8 +393,11 @@ class HipOps:
             k = in_ if l == 0 else H
             _check(tuple(W.shape) == (H, k) and W.is_contiguous() and W.dtype == torch.bfloat16,
                    "rowband: bf16 [H, in] weights")
-            _check(a.shape[0] >= rows and dz.shape[0] >= rows and a.stride(0) == H and
-                   dz.stride(0) == H and a.dtype == dz.dtype == torch.bfloat16,
+            # (a may be None for the last hidden layer: its activations stay inside the band)
+            _check((a is None and l == nh - 1) or (a.shape[0] >= rows and a.stride(0) == H and
+                                                   a.dtype == torch.bfloat16),
+                   "rowband: dense bf16 activation buffers")
+            _check(dz.shape[0] >= rows and dz.stride(0) == H and dz.dtype == torch.bfloat16,
                    "rowband: dense bf16 activation buffers")
             _check(gW.is_contiguous() and gW.numel() == H * k and gb.numel() == H and
                    b.numel() == H, "rowband: gradient / bias shapes")

@@ -10,6 +10,6 @@ SAN="-Xarch_host -fsanitize=address -Xarch_host -fsanitize=undefined -Xarch_host
 "$ROCM/bin/hipcc" --offload-arch=gfx950 -O1 -g -std=c++17 $SAN \
   -I csrc -I "$ROCM/include" -Wno-unused-command-line-argument \
   -x hip native_tests/runtime_check.cpp -x hip csrc/comm/rccl_comm.cpp \
-  csrc/kernels/optim.hip csrc/kernels/data.hip csrc/kernels/standin.hip \
+  csrc/kernels/optim.hip csrc/kernels/data.hip \
   -L "$ROCM/lib" -lrccl -Wl,-rpath,"$ROCM/lib" -o native_tests/runtime_check_asan
 echo "built native_tests/runtime_check_asan"

@@ -368,10 +368,13 @@ def test_rowband_overlap_matches_inline_bitwise(world):
     parameters and losses, replicas bitwise equal."""
     kw = dict(widths=[512, 512, 512, 512, 1], n_features=512, n_samples=2048 * world - 1,
               lr=1e-4, nepochs=4)
+    # one fp32 reduction for both: the inline schedule's single bucket defaults to ncclAllReduce
     a = run_ranks_proc(_cfg(comm="native", comm_mode="overlap_rowband", **kw), world,
-                       env_per_rank=rccl_env, timeout=300.0)
+                       env_per_rank=lambda r: dict(rccl_env(r), NNMPI_F32_REDUCE="ordered"),
+                       timeout=300.0)
     b = run_ranks_proc(_cfg(comm="native", comm_mode="inline", **kw), world,
-                       env_per_rank=lambda r: dict(rccl_env(r), NNMPI_RB_PLAN="1"), timeout=300.0)
+                       env_per_rank=lambda r: dict(rccl_env(r), NNMPI_RB_PLAN="1",
+                                                   NNMPI_F32_REDUCE="ordered"), timeout=300.0)
     for o in a + b:
         assert o["schedule"]["rowband"], o["schedule"]
     _replicas_equal(a)
