@@ -677,7 +677,9 @@ def run(a, job):
             # (weak scaling gives every rank rows_pg rows, the last one rows_pg - 1)
             st = {"global_batch": rows_pg, "ms_per_step": round(s_ms, 5),
                   "samples_per_s": round(rows_pg / (s_ms * 1e-3), 1),
-                  "parallel_efficiency": round(comp_ms / (world * s_ms), 4)}
+                  "parallel_efficiency": round(comp_ms / (world * s_ms), 4),
+                  "schedule": e.schedule_name(),
+                  "rowband_split": bool(getattr(e, "uses_rowband_split", lambda: False)())}
             base = BASELINE_SAMPLES_PER_S.get(world) if a.config == "proxy512" else None
             st["vs_baseline"] = round(st["samples_per_s"] / base, 2) if base else None
             strong = st

@@ -1009,27 +1009,6 @@ __device__ __forceinline__ void wg_reg_tile(const GemmParams& p, char* smem, int
                                                                      lane, split, nullptr);
 }
 
-// 16-byte write-through store / L1-bypassing load (the split-K hand-off inside wgrad_multi:
-// MI355X_MICROARCH.md "Valid forms", row 1 -- every store and every load of the handed-off slab
-// bytes is sc1, each storing wave drains vmcnt before the workgroup barrier, one lane's
-// agent-scope atomic add signals, the workgroup whose add returned S - 1 reads)
-__device__ __forceinline__ void st_sc1(float* p, f32x4 v) {
-  asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ void st_sc1_f(float* p, float v) {
-  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
-}
-__device__ __forceinline__ f32x4 ld_sc1(const float* p) {
-  f32x4 v;
-  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
-__device__ __forceinline__ float ld_sc1_f(const float* p) {
-  float v;
-  asm volatile("global_load_dword %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
-
 // In-launch split-K fixup of a wgrad_multi tile (the grouped tile: 8 waves as 2 x 4, 64 x 32
 // accumulators each, BM = BN = 128), cooperative and deadlock-free:
 //  1. every split publishes its partial slab (LDS-staged rows, write-through stores) and counts
@@ -1058,11 +1037,6 @@ __host__ __device__ __forceinline__ int slab_ws_n(int S) {
 constexpr int WGM_MAXS = 16;       // most splits the fixup takes (more: the combine launch)
 constexpr int WGM_CW = 32;         // counter words per tile: [0] arrivals, [1 + p] portion claims
 constexpr int WGM_SPIN = 400;      // polls of an early split (x ~0.2 us) before it gives up
-__device__ __forceinline__ int ld_sc1_i(const int* p) {
-  int v;
-  asm volatile("global_load_dword %0, %1, off sc1\n s_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
-  return v;
-}
 
 __device__ __forceinline__ void wgm_portion(const GemmParams& p, const WgmFix& f, char* smem, int tx,
                                             int ty, int portion) {

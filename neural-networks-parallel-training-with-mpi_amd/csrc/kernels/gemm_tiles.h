@@ -59,10 +59,50 @@ __device__ __forceinline__ void store16(V* ptr, const V& v, int pol) {
   } else if (pol == 2) {
     typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
     const u32x4 d = __builtin_bit_cast(u32x4, v);
-    asm volatile("global_store_dwordx4 %0, %1, off sc1" ::"v"(ptr), "v"(d) : "memory");
+    asm volatile("global_store_dwordx4 %0, %1, off sc1\n s_nop 1" ::"v"(ptr), "v"(d) : "memory");
   } else {
     *ptr = v;
   }
+}
+
+// 16-byte write-through store / L1-bypassing load (in-launch hand-offs -- wgrad_multi's split-K fixup, the column-split row-band kernel:
+// MI355X_MICROARCH.md "Valid forms", row 1 -- every store and every load of the handed-off slab
+// bytes is sc1, each storing wave drains vmcnt before the workgroup barrier, one lane's
+// agent-scope atomic add signals, the workgroup whose add returned S - 1 reads)
+// (an asm store of more than 8 bytes ends with s_nop 1: the data registers may otherwise be
+// overwritten by the next VALU before the store has read them -- cdna_hip_programming.md, the
+// inline-asm store rule; without it the column-split row-band kernel stored garbage into the first
+// element of some 16-byte pieces)
+__device__ __forceinline__ void st_sc1(float* p, f32x4 v) {
+  asm volatile("global_store_dwordx4 %0, %1, off sc1\n s_nop 1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ void st_sc1_f(float* p, float v) {
+  asm volatile("global_store_dword %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ f32x4 ld_sc1(const float* p) {
+  f32x4 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+__device__ __forceinline__ float ld_sc1_f(const float* p) {
+  float v;
+  asm volatile("global_load_dword %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+
+__device__ __forceinline__ void st_sc1_b8(void* p, uint2 v) {   // 8 bytes (4 bf16)
+  asm volatile("global_store_dwordx2 %0, %1, off sc1" ::"v"(p), "v"(v) : "memory");
+}
+__device__ __forceinline__ bf16x8 ld_sc1_b16(const void* p) {
+  bf16x8 v;
+  asm volatile("global_load_dwordx4 %0, %1, off sc1" : "=v"(v) : "v"(p) : "memory");
+  return v;
+}
+// (a poll: the value is waited for)
+__device__ __forceinline__ int ld_sc1_i(const int* p) {
+  int v;
+  asm volatile("global_load_dword %0, %1, off sc1\n s_waitcnt vmcnt(0)" : "=v"(v) : "v"(p) : "memory");
+  return v;
 }
 
 // s_waitcnt with only the vector-memory counter constrained (lgkm/exp counters left free).

@@ -181,7 +181,9 @@ struct RowbandArgs {
 };
 // the column-split row-band kernel takes this batch (H = 512, in <= 512, rows below the
 // full-band threshold): 8 blocks per 32-row band, each one 64-column slice of every layer
-bool rowband_split_ok(int rows, int H, int in, int nh);
+bool rowband_split_ok(int rows, int H, int in, int nh, int act);
+void set_rb_split(int v);    // NNMPI_RB_SPLIT: 0 off, 2 / 4 / 8 blocks per band, else automatic
+int rowband_error_word();    // int index of the split kernel's sticky wait-timeout word in the workspace
 void set_rb_store_policy(int pol);   // A/B of RowbandArgs::out_pol (-1: NNMPI_RB_STORE)
 void set_rb_fixup(int on);   // 1: split-K combine inside the weight-gradient launch (default), 0: own launch
 // diagnostic: every later v2 row-band launch records per-wave phase stamps into buf
@@ -213,6 +215,9 @@ struct RowbandStep {
   // launch); 1 the phased plan -- the last layer filling the chip alone, the others together.
   // Phases 1 + 2 of a plan == phase 0 of the same plan, bitwise.
   int plan = 0;
+  // small batches: the column-split kernel (rowband_split_ok) -- 0 never, 1 when it takes the
+  // batch, -1 the same (the engine passes 0 / 1 by its own row threshold)
+  int split = -1;
 };
 size_t rowband_workspace_bytes(int rows, int H, int in, int nh, int splits);
 hipError_t rowband_step(const RowbandStep& st, hipStream_t s);

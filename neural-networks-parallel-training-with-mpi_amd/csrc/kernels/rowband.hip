@@ -129,8 +129,7 @@ struct Rb2Mat {
   int ks;          // 64-deep k-steps
 };
 template <int H>
-__device__ __forceinline__ Rb2Mat rb2_mat(const RowbandArgs& p, int q, int cg) {
-  using G = Rb2Geom<H>;
+__device__ __forceinline__ Rb2Mat rb2_mat(const RowbandArgs& p, int q, int t0) {   // t0: first 16-col tile
   const int nh = p.nh;
   const bool past = q >= 2 * nh - 1;
   if (past) q = 2 * nh - 2;
@@ -145,7 +144,7 @@ __device__ __forceinline__ Rb2Mat rb2_mat(const RowbandArgs& p, int q, int cg) {
   }
   const int ts = (K >> 5) * 1024;
   Rb2Mat m;
-  m.b = base + (long long)cg * G::NJ * ts;
+  m.b = base + (long long)t0 * ts;
   m.ts = past ? 0 : ts;
   m.ks = K >> 6;
   return m;
@@ -157,42 +156,42 @@ __device__ __forceinline__ Rb2Mat rb2_mat(const RowbandArgs& p, int q, int cg) {
 // do-while: every matrix has >= D k-steps, and a loop the compiler must assume can be skipped
 // makes it wait for the refills at the loop exit -- rule: no global load between the ring
 // refills and their use, or vmcnt drains the ring.)
-template <int H, int D>
-__device__ __forceinline__ void rb2_mainloop(bf16x8 (&ring)[D][Rb2Geom<H>::NF],
-                                             f32x4 (&acc)[2][Rb2Geom<H>::NJ], const char* img,
-                                             const Rb2Mat& cur, const Rb2Mat& nxt, int lane) {
-  using G = Rb2Geom<H>;
+template <int NJ, int D>
+__device__ __forceinline__ void rb2_mainloop(bf16x8 (&ring)[D][2 * NJ], f32x4 (&acc)[2][NJ],
+                                             const char* img, const Rb2Mat& cur, const Rb2Mat& nxt,
+                                             int lane) {
+  constexpr int NF = 2 * NJ, KB_BYTES = RB_ROWS * 128;
   const int voff = lane * 16;
   int s0 = 0;
   do {
 #pragma unroll
     for (int d = 0; d < D; ++d) {
       const int s = s0 + d;
-      const char* kb = img + s * G::KB_BYTES;
+      const char* kb = img + s * KB_BYTES;
       bf16x8 af[2][2];
 #pragma unroll
       for (int kk = 0; kk < 2; ++kk)
 #pragma unroll
         for (int i = 0; i < 2; ++i) af[i][kk] = read_frag<64, KMAJ>(kb, 16 * i, kk, lane);
       // slot d: every later slot (D - 1 k-steps) may stay in flight, and the second k-half
-      rb2_wait<(D - 1) * G::NF + G::NJ, G::NJ>(ring[d], 0);
+      rb2_wait<(D - 1) * NF + NJ, NJ>(ring[d], 0);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < G::NJ; ++j)
+        for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[d][2 * j], af[i][0], acc[i][j], 0, 0, 0);
       __builtin_amdgcn_sched_barrier(0);   // (the first half's MFMAs stay ahead of the second wait)
-      rb2_wait<(D - 1) * G::NF, G::NJ>(ring[d], 1);
+      rb2_wait<(D - 1) * NF, NJ>(ring[d], 1);
 #pragma unroll
       for (int i = 0; i < 2; ++i)
 #pragma unroll
-        for (int j = 0; j < G::NJ; ++j)
+        for (int j = 0; j < NJ; ++j)
           acc[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ring[d][2 * j + 1], af[i][1], acc[i][j], 0, 0, 0);
       // (sched_barrier: the refill stays behind this sub-step's MFMAs, which read the slot)
       __builtin_amdgcn_sched_barrier(0);
       const int sn = s + D;
       const bool inc = sn < cur.ks;
-      rb2_issue<G::NJ>(ring[d], inc ? cur.b : nxt.b, inc ? cur.ts : nxt.ts, inc ? sn : sn - cur.ks, voff);
+      rb2_issue<NJ>(ring[d], inc ? cur.b : nxt.b, inc ? cur.ts : nxt.ts, inc ? sn : sn - cur.ks, voff);
       __builtin_amdgcn_sched_barrier(0);
     }
     s0 += D;
@@ -396,7 +395,7 @@ __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
   // their use drained the ring: half of layer 0's weights fetched before the first MFMA, a
   // 4.7 us startup -- profiles/r5_rowband_stamps.txt.)
   bf16x8 ring[D][G::NF];
-  Rb2Mat cur = rb2_mat<H>(p, 0, cg);
+  Rb2Mat cur = rb2_mat<H>(p, 0, cg * G::NJ);
   {
     constexpr int MAXIT = 1024 * RB_ROWS / 8 / RB_THREADS;   // 8: input width <= 1024
     // (thread t < H / 4 loads float4 t of every layer's bias and of the head weight; the
@@ -482,14 +481,14 @@ __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
   f32x4 acc[2][G::NJ];
   // ---- forward: a_l = act(a_{l-1} W_l^T + b_l) ----
   for (int l = 0; l < nh; ++l) {
-    const Rb2Mat nxt = rb2_mat<H>(p, l + 1, cg);
+    const Rb2Mat nxt = rb2_mat<H>(p, l + 1, cg * G::NJ);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < G::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     const char* in = slot(l == 0 ? 0 : l);
     char* out = l < nh - 1 ? slot(l + 1) : slot(nh >= 2 ? 0 : 1);
-    rb2_mainloop<H, D>(ring, acc, in, cur, nxt, lane);
+    rb2_mainloop<G::NJ, D>(ring, acc, in, cur, nxt, lane);
     stamp();
     // lane holds out[16i + (lane & 15)][n0 + 16j + 4(lane >> 4) .. +3]
     const float* bl = q.bias + l * H + n0 + 4 * (lane >> 4);
@@ -529,13 +528,13 @@ __global__ void __launch_bounds__(RB_THREADS) rowband2_kernel(RowbandArgs p) {
   pend_dst = p.dz[nh - 1] + (long long)row0 * H;
   // ---- activation gradients: dZ_{l-1} = (dZ_l W_l) * act'(a_{l-1}), in place over a_{l-1} ----
   for (int l = nh - 1; l >= 1; --l) {
-    const Rb2Mat nxt = rb2_mat<H>(p, 2 * nh - l, cg);
+    const Rb2Mat nxt = rb2_mat<H>(p, 2 * nh - l, cg * G::NJ);
 #pragma unroll
     for (int i = 0; i < 2; ++i)
 #pragma unroll
       for (int j = 0; j < G::NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     char* out = slot(l);   // holds a_{l-1}
-    rb2_mainloop<H, D>(ring, acc, z, cur, nxt, lane);
+    rb2_mainloop<G::NJ, D>(ring, acc, z, cur, nxt, lane);
     stamp();
     // (every a_{l-1} read issued before the first dZ store: one LDS round trip, not 2 x NJ
     // read-after-write-ordered ones)
@@ -623,6 +622,424 @@ static hipError_t rowband2_launch(const RowbandArgs& p, hipStream_t s) {
     return hipErrorInvalidValue;
   }
   hipLaunchKernelGGL(f, dim3(rowband_blocks(p.rows)), dim3(RB_THREADS), rb2_smem(H, p.in, p.nh), s, p);
+  return hipGetLastError();
+}
+
+// =============================================================================================
+// Column-split row-band kernel: small batches (strong-scaling shards, 64 .. 4,096 rows of the
+// 512-wide proxy).  The band kernel above streams every weight byte through every band's CU --
+// 2.5 MiB per step and CU, ~4 us per matrix at the address unit's 64 B/clk -- whatever the
+// number of bands, so at 1,024 rows (32 bands on 32 CUs) it costs what it costs at 8,192.  Here
+// the C blocks of a band (C = 8 / 4 / 2 at <= 32 / 64 / 128 bands: <= 256 blocks, one per CU)
+// each own H / C output columns of every layer and stream only those weights (C x fewer bytes
+// per CU), and the band's activations are exchanged between them once per layer:
+//  * forward layer l < nh-1: the block's 32 x H/C slice of a_l goes to p.a[l] (row-major, the
+//    buffer the weight gradients read anyway) with write-through (sc1) stores; every block of the
+//    band counts in; each block then loads the whole band of a_l back (sc1 loads) into its LDS
+//    image -- the next layer's A operand;
+//  * the head: each block's partial logit dot over its own columns is exchanged (C x 32 floats)
+//    and summed in block order by every block (the same bits everywhere); dZ_{nh-1}, the head's
+//    weight-gradient partials and the bias / loss partials need only the block's own columns;
+//  * activation gradient l: the block's slice of dZ_{l-1} = (dZ_l W_l)[:, own] * act'(a_{l-1})
+//    goes to p.dz[l-1] and is exchanged like a_l (dZ_0 is not exchanged).
+// 2 nh - 1 hand-offs per step.  Each hand-off follows MI355X_MICROARCH.md "Valid forms" row 1:
+// every handed-off byte stored sc1, every storing wave drains vmcnt before the workgroup
+// barrier, one lane's agent-scope atomic add on the band's phase counter; one lane polls it with
+// sc1 loads (bounded: past RBS_TIMEOUT it records the timeout in the sticky error word
+// xsync[0] and goes on -- no block ever waits without bound), the block joins it at a
+// barrier, every load of the handed-off bytes is an sc1 load.  The last block of a band to
+// finish resets the band's counters (graph-replayable).  Grid <= 256 blocks of 256 / 512 threads:
+// the blocks of a band are consecutive ids (dispatched together).  The weight stream and its
+// D-deep register ring are the band kernel's (rb2_mainloop), for NJ 16-column tiles per wave.
+// (Reference: dataParallelTraining_NN_MPI.py:99-146 -- the fixed dataset split over P ranks, so
+// a rank's step shrinks as P grows.)
+// =============================================================================================
+constexpr int RBS_SYNC = 32;                // ints per band: phase counters [0, 2nh-1), done [31]
+constexpr int RBS_MAXB = 128;               // bands (4,096 rows)
+constexpr int RBS_XS = 32 + RBS_MAXB * RBS_SYNC;   // sync words at the start of the workspace
+constexpr long long RBS_TIMEOUT = 200000;   // 100 MHz ticks (2 ms) before a wait gives up
+
+static int g_rbs_groups = -1;   // NNMPI_RB_SPLIT: 0 off, 2 / 4 / 8 force C, else automatic
+static int rbs_groups(int rows) {
+  if (g_rbs_groups < 0) {
+    const char* e = knob_env("NNMPI_RB_SPLIT");
+    g_rbs_groups = (e && e[0] >= '0' && e[0] <= '9') ? std::atoi(e) : 1;
+  }
+  const int nb = (rows + RB_ROWS - 1) / RB_ROWS;
+  if (g_rbs_groups == 0 || nb > RBS_MAXB) return 0;
+  if (g_rbs_groups == 2 || g_rbs_groups == 4 || g_rbs_groups == 8)
+    return nb * g_rbs_groups <= 256 ? g_rbs_groups : 0;
+  for (int c = 8; c >= 2; c >>= 1)
+    if (nb * c <= 256) return c;
+  return 0;
+}
+void set_rb_split(int v) { g_rbs_groups = v; }
+
+__host__ __device__ __forceinline__ int rbs_smem(int in, int nh) {
+  // the band kernel's activation slots + parameter block, then the head's column-partial scratch
+  return rb2_smem_core(512, in, nh) + 512 * 4;
+}
+
+template <int NJ, int NW, int ACT>
+__global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
+  // (ring depth: 4 k-steps, 2 at NJ = 4 -- the 4-deep ring, the accumulators and tanh's
+  // temporaries overflow the 256 VGPRs there and the compiler parks values in AGPRs, including
+  // asm-loaded ring registers before their loads land)
+  constexpr int H = 512, D = NJ >= 4 ? 2 : 4, NF = 2 * NJ, NT = 64 * NW;
+  constexpr int NC = 16 * NJ * NW;  // this block's output columns (NW waves x NJ tiles of 16)
+  constexpr int C = H / NC;         // blocks per band
+  constexpr int TPC = NT / NC;      // head partials: threads per column
+  constexpr int TPR = NT / RB_ROWS; // head logits / dZ: threads per row
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int band = blockIdx.x / C, c = blockIdx.x % C;
+  const int row0 = band * RB_ROWS, nvalid = min(RB_ROWS, p.rows - row0);
+  const int nh = p.nh, IN = p.in;
+  const int c0 = c * NC;                  // the block's first column
+  const int n0 = c0 + w * 16 * NJ;        // the wave's first column
+  constexpr int SL = RB_ROWS * H * 2;     // (IN <= H)
+  auto slot = [&](int i) { return smem + i * SL; };
+  const int nslot = max(nh, 2);
+  const Rb2Par q = rb2_par(smem + nslot * SL, H, nh);
+  float* red = reinterpret_cast<float*>(smem + rb2_smem_core(H, IN, nh));   // [TPC][NC]
+  int* err = p.xsync;
+  int* sy = p.xsync + 32 + band * RBS_SYNC;
+  if (blockIdx.x == 0 && p.zero_words)
+    for (int i = tid; i < p.n_zero; i += NT) p.zero_words[i] = 0;
+
+  // ---- hand-off primitives ----
+  auto arrive = [&](int ph) {   // after this block's sc1 stores of phase ph
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    __syncthreads();
+    if (tid == 0) __hip_atomic_fetch_add(sy + ph, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  };
+  auto wait = [&](int ph) {
+    if (tid == 0) {
+      const long long t0 = __builtin_amdgcn_s_memrealtime();
+      while (ld_sc1_i(sy + ph) < C) {
+        if (__builtin_amdgcn_s_memrealtime() - t0 > RBS_TIMEOUT) {
+          __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          break;
+        }
+        __builtin_amdgcn_s_sleep(1);
+      }
+    }
+    __syncthreads();
+  };
+  // the whole band of a handed-off [rows][H] matrix into an LDS image (padding rows zero)
+  auto gather = [&](const bf16* src, char* img) {
+    constexpr int IT = RB_ROWS * H / 8 / NT;
+    bf16x8 v[IT];
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      const int id = tid + it * NT;
+      const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
+      v[it] = ld_sc1_b16(src + (long long)(row0 + min(r, nvalid - 1)) * H + kb * 64 + k8 * 8);
+    }
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+#pragma unroll
+    for (int it = 0; it < IT; ++it) {
+      asm volatile("" : "+v"(v[it]));
+      const int id = tid + it * NT;
+      const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
+      bf16x8 x = v[it];
+      if (r >= nvalid) {
+#pragma unroll
+        for (int e = 0; e < 8; ++e) x[e] = (bf16)0.f;
+      }
+      *reinterpret_cast<bf16x8*>(img + kb * (RB_ROWS * 128) + kmaj_off(r, k8)) = x;
+    }
+    __syncthreads();
+  };
+  // the wave's own 32 x 16NJ tile of an LDS image -> dst rows (sc1, 16-byte pieces; the wave
+  // reads back its own LDS writes: no barrier)
+  auto put = [&](const char* img, bf16* dst) {
+    // (a compiler fence: the bf16x8 reads below alias the epilogue's bf16x4 LDS writes)
+    asm volatile("" ::: "memory");
+    const int r = lane >> 1;
+#pragma unroll
+    for (int jj = 0; jj < NJ; ++jj) {
+      const int k = n0 + 8 * ((lane & 1) + 2 * jj);
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(img + rb_off(r, k));
+      if (r < nvalid) {
+        typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+        const u32x4 d = __builtin_bit_cast(u32x4, v);
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n s_nop 1" ::"v"(dst + (long long)(row0 + r) * H + k), "v"(d)
+                     : "memory");
+      }
+    }
+  };
+
+  // ---- startup: operands, the band's input rows, the ring's first D k-steps (band kernel) ----
+  bf16x8 ring[D][NF];
+  Rb2Mat cur = rb2_mat<H>(p, 0, n0 / 16);
+  {
+    constexpr int MAXIT = H * RB_ROWS / 8 / NT;
+    f32x4 bq[RB_MAXL], wq;
+    float yq, bhq;
+    bf16x8 xv[MAXIT];
+    if (tid < H / 4) {
+#pragma unroll
+      for (int l = 0; l < RB_MAXL; ++l)
+        if (l < nh)
+          asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(bq[l]) : "v"(tid * 16), "s"(p.b[l]));
+      asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(wq) : "v"(tid * 16), "s"(p.wh));
+    }
+    if (tid < RB_ROWS)
+      asm volatile("global_load_dword %0, %1, %2" : "=v"(yq) : "v"(min(tid, nvalid - 1) * 4), "s"(p.y + row0));
+    if (tid == 0) asm volatile("global_load_dword %0, %1, %2" : "=v"(bhq) : "v"(0), "s"(p.bh));
+    const int nit = IN * RB_ROWS / 8 / NT;
+    const bf16* xb = p.X + (long long)row0 * p.ldx;
+#pragma unroll
+    for (int it = 0; it < MAXIT; ++it) {
+      if (it < nit) {
+        const int id = tid + it * NT;
+        const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
+        asm volatile("global_load_dwordx4 %0, %1, %2" : "=v"(xv[it])
+                     : "v"((min(r, nvalid - 1) * p.ldx + kb * 64 + k8 * 8) * 2), "s"(xb));
+      }
+    }
+#pragma unroll
+    for (int d = 0; d < D; ++d) rb2_issue<NJ>(ring[d], cur.b, cur.ts, d, lane * 16);
+    asm volatile("s_waitcnt vmcnt(%0)" ::"n"(D * NF));
+#pragma unroll
+    for (int l = 0; l < RB_MAXL; ++l) asm volatile("" : "+v"(bq[l]));
+    asm volatile("" : "+v"(wq), "+v"(yq), "+v"(bhq));
+#pragma unroll
+    for (int it = 0; it < MAXIT; ++it) asm volatile("" : "+v"(xv[it]));
+    char* img = slot(0);
+#pragma unroll
+    for (int it = 0; it < MAXIT; ++it) {
+      if (it < nit) {
+        const int id = tid + it * NT;
+        const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
+        bf16x8 x = xv[it];
+        if (r >= nvalid) {
+#pragma unroll
+          for (int e = 0; e < 8; ++e) x[e] = (bf16)0.f;
+        }
+        *reinterpret_cast<bf16x8*>(img + kb * (RB_ROWS * 128) + kmaj_off(r, k8)) = x;
+      }
+    }
+    if (tid < H / 4) {
+#pragma unroll
+      for (int l = 0; l < RB_MAXL; ++l)
+        if (l < nh) reinterpret_cast<f32x4*>(q.bias)[l * (H / 4) + tid] = bq[l];
+      reinterpret_cast<f32x4*>(q.wh)[tid] = wq;
+    }
+    if (tid < RB_ROWS) q.y[tid] = yq;
+    if (tid == 0) q.bh[0] = bhq;
+  }
+  __syncthreads();
+
+  f32x4 acc[2][NJ];
+  // ---- forward: slot(l + 1) receives the whole band of a_l; the last layer's own columns go
+  // to slot 0 (the input rows' slot: free by then) ----
+  for (int l = 0; l < nh; ++l) {
+    const Rb2Mat nxt = rb2_mat<H>(p, l + 1, n0 / 16);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    const bool last = l == nh - 1;
+    char* out = !last ? slot(l + 1) : slot(nh >= 2 ? 0 : 1);
+    rb2_mainloop<NJ, D>(ring, acc, slot(l), cur, nxt, lane);
+    const float* bl = q.bias + l * H + n0 + 4 * (lane >> 4);
+    f32x4 bv[NJ];
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) bv[j] = *reinterpret_cast<const f32x4*>(bl + 16 * j);
+#pragma unroll
+    for (int j = 0; j < NJ; ++j)
+#pragma unroll
+      for (int i = 0; i < 2; ++i) {
+        const f32x4 v = acc[i][j] + bv[j];
+        f32x4 a;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) a[r] = act_fwd_t<ACT>(v[r]);
+        *reinterpret_cast<bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * j + 4 * (lane >> 4))) =
+            __builtin_convertvector(a, bf16x4);
+      }
+    if (p.a[l]) put(out, p.a[l]);
+    cur = nxt;
+    if (!last) {
+      arrive(l);
+      wait(l);
+      gather(p.a[l], out);
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+      __syncthreads();
+    }
+  }
+  // ---- head: partial logits over the own columns, exchanged and summed in block order ----
+  char* z = slot(nh >= 2 ? 0 : 1);
+  {
+    const int r = tid / TPR, g = tid % TPR;
+    float dot = 0.f;
+#pragma unroll
+    for (int cc = 0; cc < NC / (8 * TPR); ++cc) {
+      const int k = c0 + 8 * (g + TPR * cc);
+      const bf16x8 v = *reinterpret_cast<const bf16x8*>(z + rb_off(r, k));
+      const f32x4 w0 = *reinterpret_cast<const f32x4*>(q.wh + k);
+      const f32x4 w1 = *reinterpret_cast<const f32x4*>(q.wh + k + 4);
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dot += (float)v[e] * w0[e];
+#pragma unroll
+      for (int e = 0; e < 4; ++e) dot += (float)v[4 + e] * w1[e];
+    }
+#pragma unroll
+    for (int sh = TPR / 2; sh >= 1; sh >>= 1) dot += __shfl_xor(dot, sh, 64);
+    if (g == 0) st_sc1_f(p.hx + ((long long)band * C + c) * RB_ROWS + r, dot);
+  }
+  arrive(nh - 1);
+  wait(nh - 1);
+  if (tid < RB_ROWS) {
+    float part[C];
+#pragma unroll
+    for (int cb = 0; cb < C; ++cb) part[cb] = ld_sc1_f(p.hx + ((long long)band * C + cb) * RB_ROWS + tid);
+    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    float dot = 0.f;
+#pragma unroll
+    for (int cb = 0; cb < C; ++cb) {
+      asm volatile("" : "+v"(part[cb]));
+      dot += part[cb];
+    }
+    const bool valid = tid < nvalid;
+    const float d = dot + q.bh[0] - q.y[tid];
+    q.dls[tid] = valid ? 2.f * d * p.inv_count : 0.f;
+    q.lss[tid] = valid ? d * d : 0.f;
+  }
+  __syncthreads();
+  // the band's head-gradient partials of the own columns (rows split over TPC threads, summed
+  // in order), the bias / loss partials by block 0 of the band
+  {
+    const int col = tid % NC, part = tid / NC, k = c0 + col;
+    constexpr int RPT = RB_ROWS / TPC;
+    float s = 0.f;
+#pragma unroll
+    for (int i = 0; i < RPT; ++i) {
+      const int r = part * RPT + i;
+      s = fmaf(q.dls[r], (float)*reinterpret_cast<const bf16*>(z + rb_off(r, k)), s);
+    }
+    red[part * NC + col] = s;
+    __syncthreads();
+    if (tid < NC) {
+      float t = red[tid];
+#pragma unroll
+      for (int pp = 1; pp < TPC; ++pp) t += red[pp * NC + tid];
+      p.wslab[(long long)band * H + c0 + tid] = t;
+    }
+    if (c == 0 && tid >= 64 && tid < 128) {
+      const int lt = tid - 64;
+      float b = lt < RB_ROWS ? q.dls[lt] : 0.f, ls = lt < RB_ROWS ? q.lss[lt] : 0.f;
+#pragma unroll
+      for (int sh = 16; sh >= 1; sh >>= 1) {
+        b += __shfl_xor(b, sh, 64);
+        ls += __shfl_xor(ls, sh, 64);
+      }
+      if (lt == 0) {
+        p.bslab[band] = b;
+        p.loss_part[band] = ls;
+      }
+    }
+  }
+  // dZ_{nh-1} of the own columns = dl * w * act'(a), in place and to p.dz[nh-1]
+  {
+    const int r = tid / TPR, g = tid % TPR;
+    const float dl = q.dls[r];
+#pragma unroll
+    for (int cc = 0; cc < NC / (8 * TPR); ++cc) {
+      const int k = c0 + 8 * (g + TPR * cc);
+      bf16x8* pz = reinterpret_cast<bf16x8*>(z + rb_off(r, k));
+      const bf16x8 v = *pz;
+      const f32x4 w0 = *reinterpret_cast<const f32x4*>(q.wh + k);
+      const f32x4 w1 = *reinterpret_cast<const f32x4*>(q.wh + k + 4);
+      bf16x8 o;
+#pragma unroll
+      for (int e = 0; e < 4; ++e) {
+        o[e] = (bf16)(dl * w0[e] * act_bwd_t<ACT>((float)v[e]));
+        o[4 + e] = (bf16)(dl * w1[e] * act_bwd_t<ACT>((float)v[4 + e]));
+      }
+      if (r < nvalid) {
+        typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+        const u32x4 dd = __builtin_bit_cast(u32x4, o);
+        asm volatile("global_store_dwordx4 %0, %1, off sc1\n s_nop 1"
+                     ::"v"(p.dz[nh - 1] + (long long)(row0 + r) * H + k), "v"(dd) : "memory");
+      }
+    }
+  }
+  if (nh >= 2) {
+    arrive(nh);
+    wait(nh);
+    gather(p.dz[nh - 1], z);
+  }
+  // ---- activation gradients: the own columns of dZ_{l-1}, over a_{l-1} in slot(l) ----
+  for (int l = nh - 1; l >= 1; --l) {
+    const Rb2Mat nxt = rb2_mat<H>(p, 2 * nh - l, n0 / 16);
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+    char* out = slot(l);
+    rb2_mainloop<NJ, D>(ring, acc, z, cur, nxt, lane);
+    bf16x4 ax[2][NJ];
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j)
+        ax[i][j] = *reinterpret_cast<const bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * j + 4 * (lane >> 4)));
+#pragma unroll
+    for (int i = 0; i < 2; ++i)
+#pragma unroll
+      for (int j = 0; j < NJ; ++j) {
+        f32x4 o;
+#pragma unroll
+        for (int r = 0; r < 4; ++r) o[r] = acc[i][j][r] * act_bwd_t<ACT>((float)ax[i][j][r]);
+        *reinterpret_cast<bf16x4*>(out + rb_off(16 * i + (lane & 15), n0 + 16 * j + 4 * (lane >> 4))) =
+            __builtin_convertvector(o, bf16x4);
+      }
+    put(out, p.dz[l - 1]);
+    cur = nxt;
+    if (l >= 2) {
+      const int ph = 2 * nh - l;
+      arrive(ph);
+      wait(ph);
+      gather(p.dz[l - 1], out);
+    }
+    z = out;
+  }
+  // ---- the last block of the band to get here resets the band's counters ----
+  asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+  __syncthreads();
+  if (tid == 0 &&
+      __hip_atomic_fetch_add(sy + RBS_SYNC - 1, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT) == C - 1) {
+    for (int i = 0; i < 2 * nh - 1; ++i) __hip_atomic_store(sy + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    __hip_atomic_store(sy + RBS_SYNC - 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+  }
+}
+
+bool rowband_split_ok(int rows, int H, int in, int nh, int act) {
+  const int c = rbs_groups(rows);
+  (void)act;
+  return rows > 0 && H == 512 && in >= 256 && in <= H && in % 256 == 0 && nh >= 1 && nh <= RB_MAXL &&
+         c > 0 && rbs_smem(in, nh) <= 160 * 1024;
+}
+
+// (NJ x NW: 1 x 4 -> 8 blocks per band, 2 x 4 -> 4, 4 x 4 -> 2)
+template <int NJ, int NW>
+static hipError_t rbs_launch(const RowbandArgs& p, hipStream_t s) {
+  using Fn = void (*)(RowbandArgs);
+  static const Fn fns[3] = {rowband_split_kernel<NJ, NW, ACT_NONE>, rowband_split_kernel<NJ, NW, ACT_RELU>,
+                            rowband_split_kernel<NJ, NW, ACT_TANH>};
+  static bool attr = false;
+  if (!attr) {
+    for (Fn f : fns)
+      (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    attr = true;
+  }
+  const Fn f = fns[p.act == ACT_RELU ? 1 : p.act == ACT_TANH ? 2 : 0];
+  const int C = 512 / (16 * NJ * NW);
+  hipLaunchKernelGGL(f, dim3(rowband_blocks(p.rows) * C), dim3(64 * NW), rbs_smem(p.in, p.nh), s, p);
   return hipGetLastError();
 }
 
@@ -728,6 +1145,17 @@ hipError_t rowband_fwd_bwd(const RowbandArgs& p0, hipStream_t s) {
   if (!p.Pf[0] || !rowband2_ok(p.rows, p.H, p.in, p.nh, 1, LOSS_MSE, p.act)) return hipErrorInvalidValue;
   for (int l = 0; l < p.nh; ++l)
     if (!p.Pf[l] || (l >= 1 && !p.Pd[l])) return hipErrorInvalidValue;
+  if (p.xsync && p.hx && rowband_split_ok(p.rows, p.H, p.in, p.nh, p.act)) {
+    // small batch: the column-split form (its hand-offs go through p.a[l], l < nh - 1)
+    for (int l = 0; l + 1 < p.nh; ++l)
+      if (!p.a[l]) return hipErrorInvalidValue;
+    switch (rbs_groups(p.rows)) {
+      case 8: return rbs_launch<1, 4>(p, s);
+      case 4: return rbs_launch<2, 4>(p, s);
+      case 2: return rbs_launch<4, 4>(p, s);
+      default: return hipErrorInvalidValue;
+    }
+  }
   switch (p.H) {
     case 256: return rowband2_launch<256>(p, s);
     case 384: return rowband2_launch<384>(p, s);
@@ -765,13 +1193,18 @@ static int rb_max_splits(int splits, int nh, int H, int rows) {
 // the slabs: zero in a fresh workspace, reset by each tile's last arrival
 static size_t rb_counters(int H, int in) { return rb_pad4((size_t)wgrad_fix_counters(H, std::max(H, in))); }
 
+// Workspace (floats): the column-split kernel's sync words (RBS_XS ints at a fixed place: they
+// must read zero between launches whatever the batch size), the head partials, the weight-
+// gradient slabs, the fixup counters, the split kernel's head exchange (G x 8 x 32).
 size_t rowband_workspace_bytes(int rows, int H, int in, int nh, int splits) {
   const size_t G = (size_t)rowband_blocks(rows);
   const int S = rb_max_splits(splits, nh, H, rows);
   const size_t head = G * H + rb_pad4(G) + rb_pad4(G);
-  return (head + (size_t)nh * S * ((size_t)H * std::max(H, in) + H) + (size_t)nh * rb_counters(H, in)) *
+  return (RBS_XS + head + (size_t)nh * S * ((size_t)H * std::max(H, in) + H) +
+          (size_t)nh * rb_counters(H, in) + G * 8 * RB_ROWS) *
          sizeof(float);
 }
+int rowband_error_word() { return 0; }   // int index into the workspace: a split-kernel wait timed out
 
 // The split-K combine of the row-band weight gradients: as its own launch (slab_multi, default)
 // or inside the weight-gradient launch (wgrad_multi_fix, NNMPI_RB_FIXUP=1: the tile's splits
@@ -794,13 +1227,15 @@ hipError_t rowband_step(const RowbandStep& st0, hipStream_t s) {
   if (!ok || !st.ws || st.phase < 0 || st.phase > 2) return hipErrorInvalidValue;
   const int H = p.H, nh = p.nh;
   const size_t G = (size_t)rowband_blocks(p.rows);
-  float* ws = st.ws;
+  p.xsync = st.split != 0 ? reinterpret_cast<int*>(st.ws) : nullptr;
+  float* ws = st.ws + RBS_XS;
   p.wslab = ws;
   p.bslab = ws + G * H;
   p.loss_part = p.bslab + rb_pad4(G);
   float* slabs = p.loss_part + rb_pad4(G);
   const size_t per = (size_t)rb_max_splits(st.splits, nh, H, p.rows) * ((size_t)H * std::max(H, p.in) + H);
   int* cnt = reinterpret_cast<int*>(slabs + (size_t)nh * per);
+  p.hx = reinterpret_cast<float*>(cnt + (size_t)nh * rb_counters(H, p.in));
   if (rb_fixup()) {
     p.zero_words = cnt;
     p.n_zero = nh * (int)rb_counters(H, p.in);

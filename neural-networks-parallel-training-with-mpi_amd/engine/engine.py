@@ -150,9 +150,12 @@ class MLPEngine:
         self._rb_fresh = False
         self._rb_ver = -1
         # A band's passes cost the same whatever the number of bands (per-CU bound: 47 us at
-        # 1,024 rows as at 8,192, profiles/r3s2_rowband_pmc.txt), so small batches (strong-scaling
-        # shards, mini-batches) keep the grouped schedule: 0.053 vs ~0.064 ms at 1,024 rows.
+        # 1,024 rows as at 8,192, profiles/r3s2_rowband_pmc.txt), so below this the band kernel
+        # is not taken; small batches (strong-scaling shards: up to 4,096 rows of the 512-wide
+        # proxy) run the column-split form instead (rowband.hip rowband_split_kernel: each band
+        # over 2-8 CUs, activations exchanged per layer), everything else the grouped schedule.
         self.rowband_min_rows = int(knob("NNMPI_ROWBAND_MIN_ROWS", "6144"))
+        self._rb_split: Dict[int, bool] = {}
         # True: the row-band step also copies out the last hidden layer's activations (debug /
         # inspection; nothing downstream reads them)
         self.rb_keep_last = False
@@ -586,7 +589,27 @@ class MLPEngine:
     def uses_rowband(self, rows: Optional[int] = None) -> bool:
         """True when a step of ``rows`` rows (default: the loaded batch) runs the row-band step."""
         rows = self.rows if rows is None else rows
-        return bool(self.rowband and rows >= max(1, self.rowband_min_rows))
+        return bool(self.rowband and (rows >= max(1, self.rowband_min_rows) or self.uses_rowband_split(rows)))
+
+    def uses_rowband_split(self, rows: Optional[int] = None) -> bool:
+        """True when a step of ``rows`` rows runs the column-split row-band kernel (small batches
+        below the band kernel's threshold)."""
+        rows = self.rows if rows is None else rows
+        if not self.rowband or rows <= 0 or rows >= max(1, self.rowband_min_rows):
+            return False
+        if rows not in self._rb_split:
+            w = self.spec.widths
+            self._rb_split[rows] = bool(hasattr(self.ops, "rowband_split_ok") and self.ops.rowband_split_ok(
+                rows, w[1], w[0], self.L - 1, self.act))
+        return self._rb_split[rows]
+
+    def check_device_errors(self):
+        """Raise if a column-split row-band step gave up a bounded wait (a band's blocks were not
+        all resident within 2 ms: its results are invalid).  Reads one device word (host sync)."""
+        if self.ws_rb is not None and any(self._rb_split.values()) and hasattr(self.ops, "rowband_error_word"):
+            i = self.ops.rowband_error_word()
+            if int(self.ws_rb[i:i + 1].view(torch.int32).item()) != 0:
+                raise RuntimeError("row-band split step: a band's hand-off wait timed out (results invalid)")
 
     def schedule_name(self) -> str:
         """The step schedule a batch of the loaded size runs (bench / result reports)."""
@@ -626,7 +649,8 @@ class MLPEngine:
         self.ops.rowband_step(self.X[:rows], self._rb_layers(), ar.weight(last), ar.bias(last),
                               self.Y[:rows], self.inv_count, ar.grad_weight(last),
                               ar.grad_bias(last), self.ws_rb, self.loss_scale, self.loss_out,
-                              self.act, sgd=sgd, phase=phase, plan=self.rb_plan, **kw)
+                              self.act, sgd=sgd, phase=phase, plan=self.rb_plan,
+                              split=1 if self.uses_rowband_split(rows) else 0, **kw)
 
     # Row-band step with per-bucket collectives on the comm stream (several ranks): the band
     # launch and the last hidden layer's + the head's weight gradients first (phase 1); their
@@ -1140,6 +1164,7 @@ class MLPEngine:
         """Local (this rank's) mean loss of the last step (host sync)."""
         if self.is_cuda:
             self.stream.synchronize()
+        self.check_device_errors()
         return float(self.loss_out[0].item())
 
     def synchronize(self):

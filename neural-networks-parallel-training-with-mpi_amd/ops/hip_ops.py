@@ -336,6 +336,16 @@ class HipOps:
         (see rowband.hip)."""
         return self.rowband_version(rows, widths, act, loss) > 0
 
+    def rowband_split_ok(self, rows: int, H: int, in_: int, nh: int, act: str = "relu") -> bool:
+        """A row-band step of ``rows`` rows runs the column-split kernel (rowband.hip
+        rowband_split_kernel: H = 512, 256 <= in <= 512, in % 256 == 0, <= 128 bands; tanh
+        only up to 64 bands)."""
+        return bool(self.lib.rowband_split_ok(int(rows), int(H), int(in_), int(nh), ACT_CODES[act]))
+
+    def rowband_error_word(self) -> int:
+        """Index (int32 words) of the split kernel's sticky wait-timeout word in the workspace."""
+        return int(self.lib.rowband_error_word())
+
     def rowband_workspace_bytes(self, rows: int, H: int, nh: int, splits: int = 0,
                                 in_: Optional[int] = None) -> int:
         return int(self.lib.rowband_workspace_bytes(int(rows), int(H), int(H if in_ is None else in_),
@@ -371,7 +381,7 @@ class HipOps:
 
     def rowband_step(self, X, layers, wh, bh, y, inv_count: float, gWh, gbh, ws, loss_scale: float,
                      loss_out, act: str, sgd=None, splits: int = 0, packed=None, phase: int = 0,
-                     plan: int = 0):
+                     plan: int = 0, split: int = -1):
         """One step body of a narrow MSE regressor in three launches.  ``layers``: per hidden
         layer ``(W16, b, a_out, dz_out, gW, gb)``.  Writes every activation and dZ, the
         gradients (or, with ``sgd``, applies the fused update at their arena positions -- and
@@ -379,7 +389,9 @@ class HipOps:
         ``loss_out[0] = loss_scale * sum of squared errors``.  ``packed``: the v2 weight images
         (must match the weights); None runs the v1 kernel.  ``phase`` 1 / 2: the band launch with
         the last hidden layer's and the head's gradients / the other layers' gradients (the
-        overlapped multi-rank schedule); ``plan``: the split-K plan (RowbandStep, kernels.h)."""
+        overlapped multi-rank schedule); ``plan``: the split-K plan (RowbandStep, kernels.h);
+        ``split``: the column-split kernel for small batches -- 0 never, 1 / -1 where it takes the
+        batch (rowband_split_ok)."""
         rows, in_ = X.shape
         nh = len(layers)
         H = layers[0][0].shape[0]
@@ -408,7 +420,8 @@ class HipOps:
         self.lib.rowband_step(_p(X), X.stride(0), rows, H, in_, ACT_CODES[act], lay, _p(wh),
                               _p(bh), _p(y), float(inv_count), _p(gWh), _p(gbh), _p(ws),
                               float(loss_scale), _p(loss_out), sgd, int(splits),
-                              self._packed_ptrs(packed), int(phase), int(plan), self.stream)
+                              self._packed_ptrs(packed), int(phase), int(plan), int(split),
+                              self.stream)
 
     # ---------------- tiny fused MLP ----------------
     def tiny_workspace_bytes(self, rows, numel) -> int:

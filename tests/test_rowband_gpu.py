@@ -52,7 +52,59 @@ def test_rowband_gradients_vs_oracle(widths, rows, act, monkeypatch):
     """Every layer's weight and bias gradient, the activations, every dZ and the loss of ONE
     row-band step (no optimizer) vs the fp32 oracle: 1e-2 relative norm per tensor (a wrong
     scale on any layer, a missed row of a partial band or a transposed weight operand fails).
-    The fragment-major weight images are built first (rowband_pack)."""
+    The fragment-major weight images are built first (rowband_pack).  The band kernel itself
+    (the column-split form off: NNMPI_RB_SPLIT=0)."""
+    from nnmpi_amd import native
+    lib = native.lib()
+    assert lib.rowband_split_ok(1024, 512, 512, 3, 1)
+    lib.set_rb_split(0)
+    try:
+        assert not lib.rowband_split_ok(rows, widths[1], widths[0], len(widths) - 2, 1)
+        _oracle_check(widths, rows, act, monkeypatch)
+    finally:
+        lib.set_rb_split(-1)
+
+
+# the column-split kernel's shapes: H = 512, in 256 / 512, 1-4 hidden layers, <= 4,096 rows
+# (8 / 4 / 2 blocks per band at <= 1,024 / 2,048 / 4,096 rows)
+_SPLIT_SHAPES = [([512, 512, 512, 512, 1], 1024, "relu", 0),
+                 ([512, 512, 512, 512, 1], 1000, "relu", 0),
+                 ([512, 512, 512, 512, 1], 2048, "relu", 0),
+                 ([512, 512, 512, 512, 1], 4096, "relu", 0),
+                 ([512, 512, 512, 512, 1], 3001, "relu", 0),
+                 ([512, 512, 512, 512, 1], 3001, "tanh", 0),
+                 ([512, 512, 512, 512, 1], 2047, "tanh", 0),
+                 ([512, 512, 1], 37, "relu", 0),
+                 ([512, 512, 512, 1], 64, "relu", 0),
+                 ([512] * 5 + [1], 2047, "relu", 0),
+                 ([256, 512, 512, 512, 1], 999, "relu", 0),
+                 ([512, 512, 512, 512, 1], 777, "tanh", 0),
+                 ([512, 512, 512, 512, 1], 1000, "relu", 4),
+                 ([512, 512, 512, 512, 1], 1000, "relu", 2),
+                 ([512, 512, 512, 512, 1], 2048, "relu", 2)]
+
+
+@pytest.mark.parametrize("widths,rows,act,groups", _SPLIT_SHAPES)
+def test_rowband_split_gradients_vs_oracle(widths, rows, act, groups, monkeypatch):
+    """The column-split row-band kernel (small batches: each band's columns over 2-8 blocks,
+    activations exchanged per layer through write-through stores and per-band counters) vs the
+    fp32 oracle, as the band kernel above; ``groups`` forces the blocks per band (0: automatic).
+    The engine takes it by itself below the band kernel's row threshold; no wait timed out."""
+    from nnmpi_amd import native
+    lib = native.lib()
+    monkeypatch.setenv("NNMPI_ROWBAND_MIN_ROWS", "6144")   # (the production threshold)
+    if groups:
+        lib.set_rb_split(groups)
+    try:
+        assert lib.rowband_split_ok(rows, widths[1], widths[0], len(widths) - 2, 1 if act == "relu" else 2)
+        eng = _oracle_check(widths, rows, act, monkeypatch)
+        assert eng.uses_rowband_split(rows) and eng.schedule_name() == "rowband"
+        eng.check_device_errors()
+    finally:
+        lib.set_rb_split(-1)
+
+
+def _oracle_check(widths, rows, act, monkeypatch):
     from nnmpi_amd.ops.hip_ops import HipOps
     from nnmpi_amd.ops.torch_ops import TorchOps
     X, Y = _data(rows, widths)
@@ -87,6 +139,8 @@ def test_rowband_gradients_vs_oracle(widths, rows, act, monkeypatch):
             rec[("dz", i)] = eng._dzl(i, rows).double().cpu().clone()
         rec["loss"] = float(eng.loss_out[0].item())
         out.append(rec)
+        if dev == "cuda":
+            geng = eng
     g, r = out
     assert g["loss"] == pytest.approx(r["loss"], rel=1e-3)
     for key in r:
@@ -95,6 +149,7 @@ def test_rowband_gradients_vs_oracle(widths, rows, act, monkeypatch):
         a, b = g[key], r[key]
         rel = float((a - b).norm() / b.norm().clamp_min(1e-30))
         assert rel < 1e-2, (key, rel)
+    return geng
 
 
 def test_rowband_engine_is_taken_and_trains_like_grouped(monkeypatch):
@@ -240,14 +295,18 @@ def test_rowband_fused_update_writes_the_weight_images(widths, monkeypatch):
             assert torch.equal(pd, qd), f"dgrad image of layer {l}"
 
 
-def test_rowband_graph_replay_is_bitwise_equal_to_eager(monkeypatch):
+@pytest.mark.parametrize("rows", [8192, 1024, 3000])
+def test_rowband_graph_replay_is_bitwise_equal_to_eager(rows, monkeypatch):
+    """Graph replay vs eager, 4 fused-update steps, bitwise (at 1,024 / 3,000 rows the
+    column-split kernel: its per-band counters reset themselves, so replays see zero)."""
     from nnmpi_amd.engine.arena import Arena
     from nnmpi_amd.engine.engine import MLPEngine
     from nnmpi_amd.models.mlp import MLPSpec, reference_init
     from nnmpi_amd.ops.hip_ops import HipOps
     from nnmpi_amd.parallel.sync import NoSync
     monkeypatch.setenv("NNMPI_ROWBAND", "1")
-    widths, rows = [512, 512, 512, 512, 1], 8192
+    monkeypatch.setenv("NNMPI_ROWBAND_MIN_ROWS", "6144")   # (the production threshold)
+    widths = [512, 512, 512, 512, 1]
     X, Y = _data(rows, widths)
     spec = MLPSpec(tuple(widths), "relu", "mse")
     out = []
@@ -257,14 +316,16 @@ def test_rowband_graph_replay_is_bitwise_equal_to_eager(monkeypatch):
         ar.bind_model(reference_init(widths, "relu", seed=5))
         eng = MLPEngine(spec, ar, HipOps("cuda"), NoSync(ar), device="cuda", dtype=torch.bfloat16,
                         rows_capacity=rows, lr=1e-3, momentum=0.9, use_graph=graph)
-        assert eng.rowband
+        assert eng.rowband and eng.uses_rowband(rows)
+        assert eng.uses_rowband_split(rows) == (rows < 6144)
         eng.load_batch(X, Y)
         eng.set_scales(1.0 / rows, 1.0 / rows, 1.0)
         for _ in range(4):
             eng.step()
         eng.synchronize()
-        out.append(ar.master.clone())
-    assert torch.equal(out[0], out[1])
+        out.append((ar.master.clone(), eng.loss()))
+    assert torch.equal(out[0][0], out[1][0])
+    assert out[0][1] == out[1][1]
 
 
 def test_bench_default_proxy_step_runs_the_rowband_schedule():
@@ -282,24 +343,30 @@ def test_bench_default_proxy_step_runs_the_rowband_schedule():
     assert d["replicas_bitwise_equal"] is True and d["final_loss"] == d["final_loss"]
 
 
-def test_small_batches_keep_the_grouped_schedule(monkeypatch):
-    """Below NNMPI_ROWBAND_MIN_ROWS (default 6,144) a step runs the grouped schedule: a band's
-    passes cost the same however few bands there are, so small batches are faster grouped."""
+def test_small_batches_pick_the_split_kernel_or_the_grouped_schedule(monkeypatch):
+    """Below NNMPI_ROWBAND_MIN_ROWS (default 6,144) the band kernel is not taken (a band's passes
+    cost the same however few bands there are): the 512-wide proxy's small batches (<= 4,096
+    rows) run the column-split kernel, other small batches the grouped schedule; one engine
+    switches between them and the band kernel by batch size."""
     from nnmpi_amd.ops.hip_ops import HipOps
     monkeypatch.delenv("NNMPI_ROWBAND_MIN_ROWS", raising=False)
     widths = [512, 512, 512, 512, 1]
     _, _, eng = _engine(widths, 8192, "cuda", HipOps("cuda"), rowband=True, monkeypatch=monkeypatch)
     X, Y = _data(8192, widths)
-    eng.load_batch(X[:1024], Y[:1024])
-    assert eng.rowband and not eng.uses_rowband() and eng.schedule_name() == "grouped"
-    eng.set_scales(1.0 / 1024, 1.0 / 1024, 1.0)
-    eng.step()
-    l_small = eng.loss()
-    eng.load_batch(X, Y)
-    assert eng.uses_rowband() and eng.schedule_name() == "rowband"
-    eng.set_scales(1.0 / 8192, 1.0 / 8192, 1.0)
-    eng.step()
-    assert l_small == l_small and eng.loss() == eng.loss()
+    seen = []
+    for rows, split, name in ((1024, True, "rowband"), (5000, False, "grouped"),
+                              (8192, False, "rowband"), (2048, True, "rowband")):
+        eng.load_batch(X[:rows], Y[:rows])
+        assert eng.uses_rowband_split() == split and eng.schedule_name() == name, rows
+        eng.set_scales(1.0 / rows, 1.0 / rows, 1.0)
+        eng.step()
+        seen.append(eng.loss())
+    assert all(v == v for v in seen)
+    _, _, e256 = _engine([256, 256, 256, 256, 1], 1024, "cuda", HipOps("cuda"), rowband=True,
+                         monkeypatch=monkeypatch)
+    X2, Y2 = _data(1024, [256, 256, 256, 256, 1])
+    e256.load_batch(X2, Y2)
+    assert not e256.uses_rowband() and e256.schedule_name() == "grouped"
 
 
 
