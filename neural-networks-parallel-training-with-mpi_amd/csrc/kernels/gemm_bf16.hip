@@ -1454,6 +1454,149 @@ hipError_t wgrad_multi_fix(const WgradArgs* jobs, int nj, const int* splits, con
   return wgm_launch(g, nb, true, s);
 }
 
+// ---- Small-batch weight gradients, update in the epilogue (the column-split row-band step) ----
+// At <= 4,096 rows wgrad_multi's split-K slabs (5 per layer at 1,024 rows) and their combine
+// launch cost more than the product: 9.8 + 8.8 us for 1.6 GFLOP on the proxy at 1,024 rows
+// (profiles/r5_rowband_split_bench.txt).  Here every layer's 64 x 64 tiles (3 x 64 = 192 blocks
+// on the proxy) reduce the whole K = rows un-split, and the epilogue applies SGD-momentum from
+// registers and rewrites the v2 weight images (one rank), or stores the gradient (several ranks);
+// extra blocks combine the head's per-band partials (the row-band head_red).  One launch where
+// the slab form takes two, and no slab round trip.
+template <int GA, int NS>
+__global__ void __launch_bounds__(SLAB_THREADS) wgrad_small_kernel(WgradMultiParams g) {
+  extern __shared__ __attribute__((aligned(1024))) char smem[];
+  if ((int)blockIdx.x >= g.gemm_blocks) {   // the head's combine
+    slab_reduce_any(g.tail_ws, g.tail, blockIdx.x - g.gemm_blocks, g.tail_nb_main, g.tail_nb_bias,
+                    reinterpret_cast<f32x4*>(smem));
+    return;
+  }
+  constexpr int MI = 2, NJ = 1;   // 64 x 64 tile, 2 x 4 waves of 32 x 16 (512 threads: the
+                                  // combine blocks' shape)
+  int bid = blockIdx.x;
+#pragma unroll
+  for (int j = 0; j < RB_MAXL; ++j) {
+    if (j >= g.nj) break;
+    if (bid < g.blocks[j]) {
+      const int t = xcd_remap(bid, g.blocks[j]);
+      if (t >= g.n[j]) break;
+      const int tx = t % g.gx[j], ty = t / g.gx[j];
+      f32x4 acc[MI * NJ], accb[MI];
+      dma_gemm_tile<64, 64, 2, 4, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, NS, GA, false, true>(
+          g.wg[j], smem, tx, ty, 0, nullptr, acc, accb);
+      const WgmFix& f = g.fix[j];
+      const int M = g.wg[j].M, N = g.wg[j].N;
+      const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 2, wn = w & 3;
+      const int m0 = ty * 64, n0 = tx * 64;
+      const bool upd = f.sg.g_base != nullptr;
+      int mm[MI * NJ], nn[MI * NJ];
+      bool ok[MI * NJ];
+#pragma unroll
+      for (int i = 0; i < MI; ++i)
+#pragma unroll
+        for (int jj = 0; jj < NJ; ++jj) {
+          const int k = i * NJ + jj;
+          mm[k] = m0 + wm * 32 + i * 16 + (lane & 15);
+          nn[k] = n0 + wn * 16 + jj * 16 + (lane >> 4) * 4;
+          ok[k] = mm[k] < M && nn[k] < N;
+        }
+      if (upd) {
+        // every fragment's master / momentum loads in flight together (one round trip), then
+        // the updates; the transposed image through LDS as 16-byte pieces (8 rows of a column)
+        SgdPre4 pre[MI * NJ];
+#pragma unroll
+        for (int k = 0; k < MI * NJ; ++k)
+          if (ok[k]) pre[k] = sgd_pre4(f.sg, f.out + (long long)mm[k] * N + nn[k]);
+        bf16* tb = reinterpret_cast<bf16*>(smem);   // [64][64] new weights of the tile
+        __syncthreads();   // (every wave is past its last read of the DMA ring)
+#pragma unroll
+        for (int k = 0; k < MI * NJ; ++k) {
+          if (!ok[k]) continue;
+          const f32x4 pn = sgd_apply4(f.sg, pre[k], acc[k]);
+          rb_pack_store4(f.pkf, nullptr, mm[k], nn[k], M, N, pn);
+          bf16x4 hv;
+#pragma unroll
+          for (int e = 0; e < 4; ++e) hv[e] = (bf16)pn[e];
+          *reinterpret_cast<bf16x4*>(tb + (mm[k] - m0) * 64 + (nn[k] - n0)) = hv;
+        }
+        if (f.pkd) {
+          __syncthreads();
+          const int c = tid & 63, g8 = tid >> 6, n = n0 + c, m = m0 + 8 * g8;
+          if (n < N && m < M) {
+            bf16x8 col;
+#pragma unroll
+            for (int r = 0; r < 8; ++r) col[r] = tb[(8 * g8 + r) * 64 + c];
+            *reinterpret_cast<bf16x8*>(f.pkd + rb_pk_off(n, m, M)) = col;
+          }
+        }
+      } else {
+#pragma unroll
+        for (int k = 0; k < MI * NJ; ++k)
+          if (ok[k]) *reinterpret_cast<f32x4*>(f.out + (long long)mm[k] * N + nn[k]) = acc[k];
+      }
+      if (tx == 0 && wn == 0 && (lane >> 4) == 0) {   // the bias gradient: the row sums
+#pragma unroll
+        for (int i = 0; i < MI; ++i) {
+          const int m = m0 + wm * 32 + i * 16 + lane;
+          if (m >= M) continue;
+          if (upd) sgd_fused_store(f.sg, f.bout + m, accb[i][0]);
+          else f.bout[m] = accb[i][0];
+        }
+      }
+      break;
+    }
+    bid -= g.blocks[j];
+  }
+}
+
+hipError_t wgrad_small(const WgradArgs* jobs, int nj, const WgmFixArgs* img, const SlabReduce* tail,
+                       hipStream_t s) {
+  if (nj < 1 || nj > RB_MAXL) return hipErrorInvalidValue;
+  WgradMultiParams g{};
+  g.nj = nj;
+  int nb = 0;
+  for (int j = 0; j < nj; ++j) {
+    const WgradArgs& a = jobs[j];
+    if (a.db == nullptr || a.dW16 != nullptr || a.M % 32 || a.N % 32) return hipErrorInvalidValue;
+    GemmParams p;
+    SlabReduce pend;
+    make_wgrad_s(a, p, pend, 1);
+    p.sg = SgdFuse{};
+    p.c16 = nullptr; p.bg16 = nullptr;
+    set_extents<XMAJ, XMAJ>(p);
+    g.wg[j] = p;
+    g.gx[j] = (p.N + 63) / 64;
+    g.tiles[j] = g.gx[j] * ((p.M + 63) / 64);
+    g.n[j] = g.tiles[j];
+    g.blocks[j] = (g.n[j] + 7) & ~7;
+    g.fix[j] = WgmFix{a.dW, a.db, a.sg, img ? img[j].pkf : nullptr, img ? img[j].pkd : nullptr, nullptr, 1};
+    nb += g.blocks[j];
+  }
+  g.gemm_blocks = nb;
+  if (tail && tail->ws && tail->S > 0) {
+    g.tail = *tail;
+    g.tail.sgd_serial = sgd_serial();
+    g.tail_ws = slab_ws(*tail);
+    int nbt = 0;
+    slab_blocks(*tail, g.tail_nb_main, g.tail_nb_bias, nbt);
+    nb += nbt;
+  }
+  // DMA ring stages (NNMPI_WGS_STAGES 2 / 3 / 4): one 64 x 64 tile per CU streams its whole K, so
+  // the ring depth is what hides the L2 round trip of each k-step
+  static const int ns = [] {
+    const char* e = knob_env("NNMPI_WGS_STAGES");
+    return (e && (e[0] == '2' || e[0] == '3')) ? e[0] - '0' : 4;
+  }();
+  const int smem = std::max(ns * (64 + 64) * GEMM_BK * 2, SLAB_PART_BYTES);
+  auto* f = ns == 2 ? wgrad_small_kernel<2, 2> : ns == 3 ? wgrad_small_kernel<2, 3> : wgrad_small_kernel<2, 4>;
+  static bool attr = false;
+  if (!attr) {
+    (void)hipFuncSetAttribute((const void*)wgrad_small_kernel<2, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+    attr = true;
+  }
+  hipLaunchKernelGGL(f, dim3(nb), dim3(SLAB_THREADS), smem, s, g);
+  return hipGetLastError();
+}
+
 struct SlabMultiParams {
   SlabReduce r[RB_MAXL + 1];
   int ws[RB_MAXL + 1], nb_main[RB_MAXL + 1], nb_bias[RB_MAXL + 1], nb[RB_MAXL + 1];

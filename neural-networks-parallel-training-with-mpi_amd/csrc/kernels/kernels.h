@@ -182,7 +182,8 @@ struct RowbandArgs {
 // the column-split row-band kernel takes this batch (H = 512, in <= 512, rows below the
 // full-band threshold): 8 blocks per 32-row band, each one 64-column slice of every layer
 bool rowband_split_ok(int rows, int H, int in, int nh, int act);
-void set_rb_split(int v);    // NNMPI_RB_SPLIT: 0 off, 2 / 4 / 8 blocks per band, else automatic
+void set_rb_split(int v);
+void set_rb_wgsmall(int v);  // NNMPI_RB_WGSMALL: small-batch weight gradients with the update fused (1) or slabs (0)    // NNMPI_RB_SPLIT: 0 off, 2 / 4 / 8 blocks per band, else automatic
 int rowband_error_word();    // int index of the split kernel's sticky wait-timeout word in the workspace
 void set_rb_store_policy(int pol);   // A/B of RowbandArgs::out_pol (-1: NNMPI_RB_STORE)
 void set_rb_fixup(int on);   // 1: split-K combine inside the weight-gradient launch (default), 0: own launch
@@ -238,6 +239,11 @@ struct WgmFixArgs {
   int* cnt;               // per-tile counter words (wgrad_fix_counters of them), zero
 };
 int wgrad_fix_counters(int M, int N);
+// Small-batch weight gradients of several layers in ONE launch: 64 x 64 tiles over the whole K
+// (no split), SGD-momentum + the row-band v2 images (img[j], may be null) in the epilogue when
+// jobs[j].sg is set (else the gradient), the head's combine `tail` (may be null) in extra blocks.
+hipError_t wgrad_small(const WgradArgs* jobs, int nj, const WgmFixArgs* img, const SlabReduce* tail,
+                       hipStream_t s);
 hipError_t wgrad_multi_fix(const WgradArgs* jobs, int nj, const int* splits, const WgmFixArgs* fix,
                            const SlabReduce* tail, hipStream_t s);
 

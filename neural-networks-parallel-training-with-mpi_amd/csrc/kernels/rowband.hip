@@ -1220,6 +1220,16 @@ static bool rb_fixup() {
   return g_rb_fixup == 1;
 }
 
+// Small batches (the column-split kernel's): the weight gradients as 64 x 64 tiles over the whole
+// K with the update in their epilogue and the head's combine in the same launch (wgrad_small) --
+// NNMPI_RB_WGSMALL=0 keeps the split-K slabs + combine launch (A/B).
+static int g_rb_wgsmall = -1;
+void set_rb_wgsmall(int v) { g_rb_wgsmall = v; }
+static bool rb_wgsmall() {
+  if (g_rb_wgsmall < 0) g_rb_wgsmall = rb_env("NNMPI_RB_WGSMALL", 1) ? 1 : 0;
+  return g_rb_wgsmall == 1;
+}
+
 hipError_t rowband_step(const RowbandStep& st0, hipStream_t s) {
   RowbandStep st = st0;
   RowbandArgs& p = st.fb;
@@ -1261,6 +1271,14 @@ hipError_t rowband_step(const RowbandStep& st0, hipStream_t s) {
   }
   const SlabReduce head_red{p.wslab, (int)G, H, 1, H, st.gWh, H, p.bslab, 1, st.gbh, p.loss_part,
                             (int)G, st.loss_scale, st.loss_out, st.sg};
+  if (nj > 0 && p.xsync && rb_wgsmall() && rowband_split_ok(p.rows, H, p.in, nh, p.act)) {
+    WgmFixArgs im[RB_MAXL];
+    const bool img = st.sg.g_base && p.Pf[0];
+    for (int l = l0; l < l1; ++l)
+      im[l - l0] = WgmFixArgs{img ? const_cast<bf16*>(p.Pf[l]) : nullptr,
+                              img && l >= 1 ? const_cast<bf16*>(p.Pd[l]) : nullptr, nullptr};
+    return wgrad_small(jobs, nj, im, head ? &head_red : nullptr, s);
+  }
   if (nj > 0 && rb_fixup()) {
     // one launch: every layer's weight gradient, its split-K combine + update in the tile's last
     // split, and the head's combine in extra blocks

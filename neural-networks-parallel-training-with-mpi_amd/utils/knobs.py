@@ -34,6 +34,9 @@ KNOBS = {
     "NNMPI_PP_PREFETCH": "SGD-operand prefetch in the 256x256 weight gradient",
     "NNMPI_RB_BANDMAP": "XCD-contiguous band order of the row-band kernel",
     "NNMPI_RB_STORE": "row-band copy-out store policy (0 plain, 1 nt, 2 sc1)",
+    "NNMPI_RB_SPLIT": "column-split row-band kernel for small batches: 0 off, 2 / 4 / 8 blocks per band, else auto",
+    "NNMPI_RB_WGSMALL": "small-batch row-band weight gradients: 1 un-split tiles with the update fused, 0 split-K slabs",
+    "NNMPI_WGS_STAGES": "small-batch weight-gradient DMA ring stages (2 / 3 / 4)",
     "NNMPI_RB_FIXUP": "row-band split-K combine inside the weight-gradient launch (0: own launch)",
     "NNMPI_GEMM": "GEMM main loop (1 register-staged, 2 LDS-DMA)",
     "NNMPI_SLAB_STORE": "split-K slab store policy",

@@ -104,6 +104,40 @@ def test_rowband_split_gradients_vs_oracle(widths, rows, act, groups, monkeypatc
         lib.set_rb_split(-1)
 
 
+@pytest.mark.parametrize("rows", [1024, 2047])
+def test_rowband_small_wgrad_matches_the_slab_form(rows, monkeypatch):
+    """The small-batch weight gradients (wgrad_small: un-split 64 x 64 tiles, SGD-momentum and
+    the weight images in the epilogue, the head's combine in the same launch) against the split-K
+    slabs + combine launch (NNMPI_RB_WGSMALL=0): three fused-update steps, parameters within
+    1e-5 relative (different summation order), losses within 1e-4."""
+    from nnmpi_amd import native
+    from nnmpi_amd.ops.hip_ops import HipOps
+    lib = native.lib()
+    monkeypatch.setenv("NNMPI_ROWBAND_MIN_ROWS", "6144")
+    widths = [512, 512, 512, 512, 1]
+    X, Y = _data(rows, widths)
+    res = []
+    try:
+        for small in (1, 0):
+            assert lib.set_rb_wgsmall(small)
+            _, ar, eng = _engine(widths, rows, "cuda", HipOps("cuda"), lr=1e-3, momentum=0.9,
+                                 rowband=True, monkeypatch=monkeypatch)
+            assert eng.uses_rowband_split(rows)
+            eng.load_batch(X, Y)
+            eng.set_scales(1.0 / rows, 1.0 / rows, 1.0)
+            losses = []
+            for _ in range(3):
+                eng.step()
+                losses.append(eng.loss())
+            res.append((ar.master.double().cpu(), losses))
+    finally:
+        lib.set_rb_wgsmall(-1)
+    (p1, l1), (p2, l2) = res
+    assert float((p1 - p2).norm() / p2.norm()) < 1e-5
+    for a, b in zip(l1, l2):
+        assert a == pytest.approx(b, rel=1e-4)
+
+
 def _oracle_check(widths, rows, act, monkeypatch):
     from nnmpi_amd.ops.hip_ops import HipOps
     from nnmpi_amd.ops.torch_ops import TorchOps
@@ -177,18 +211,22 @@ def test_rowband_engine_is_taken_and_trains_like_grouped(monkeypatch):
     assert l1[-1] < l1[0]
 
 
-def test_rowband_fused_update_is_bitwise_equal_to_separate_pass(monkeypatch):
+@pytest.mark.parametrize("split", [False, True])
+def test_rowband_fused_update_is_bitwise_equal_to_separate_pass(split, monkeypatch):
     """One rank: the combines apply SGD-momentum themselves; bitwise the same parameters as the
     row-band gradients followed by the standalone optimizer pass (same slab sums, same pinned
-    update arithmetic)."""
+    update arithmetic).  ``split``: the small-batch path (column-split kernel + the un-split
+    weight gradients with the update in their epilogue, wgrad_small)."""
     from nnmpi_amd.ops.hip_ops import HipOps
     widths, rows = [512, 512, 512, 512, 1], 1500
+    if split:
+        monkeypatch.setenv("NNMPI_ROWBAND_MIN_ROWS", "6144")
     X, Y = _data(rows, widths)
     res = []
     for fuse in (True, False):
         _, ar, eng = _engine(widths, rows, "cuda", HipOps("cuda"), lr=1e-3, momentum=0.9,
                              fuse_sgd=fuse, rowband=True, monkeypatch=monkeypatch)
-        assert eng.rowband
+        assert eng.rowband and eng.uses_rowband_split(rows) == split
         eng.load_batch(X, Y)
         eng.set_scales(1.0 / rows, 1.0 / rows, 1.0)
         for _ in range(3):
@@ -267,19 +305,23 @@ def test_rowband_half_width_wgrad_tile_is_bitwise_equal(widths, rows, monkeypatc
     assert res[0][3] == res[1][3]
 
 
-@pytest.mark.parametrize("widths", [[512, 512, 512, 512, 1], [256, 256, 256, 1],
-                                    [768, 1024, 1024, 1], [384, 384, 384, 1]])
-def test_rowband_fused_update_writes_the_weight_images(widths, monkeypatch):
+@pytest.mark.parametrize("widths,rows", [([512, 512, 512, 512, 1], 8192), ([256, 256, 256, 1], 8192),
+                                         ([768, 1024, 1024, 1], 8192), ([384, 384, 384, 1], 8192),
+                                         ([512, 512, 512, 512, 1], 1024), ([256, 512, 512, 1], 2000)])
+def test_rowband_fused_update_writes_the_weight_images(widths, rows, monkeypatch):
     """The combines that apply the update also rewrite the v2 weight images (the forward image
     directly, the transposed dgrad image staged through LDS where a block holds whole rows):
-    after a few steps they equal a fresh pack of the new bf16 weights, bit for bit."""
+    after a few steps they equal a fresh pack of the new bf16 weights, bit for bit.  At 1,024 /
+    2,000 rows: the small-batch path's weight-gradient epilogue (wgrad_small) writes them."""
     from nnmpi_amd.ops.hip_ops import HipOps
-    rows = 8192
+    if rows < 6144:
+        monkeypatch.setenv("NNMPI_ROWBAND_MIN_ROWS", "6144")
     X, Y = _data(rows, widths)
     ops = HipOps("cuda")
     _, ar, eng = _engine(widths, rows, "cuda", ops, lr=1e-3, momentum=0.9, fuse_sgd=True,
                          rowband=True, monkeypatch=monkeypatch)
     assert eng.rowband and eng.rb_version == 2
+    assert eng.uses_rowband_split(rows) == (rows < 6144)
     eng.load_batch(X, Y)
     eng.set_scales(1.0 / rows, 1.0 / rows, 1.0)
     for _ in range(3):
