@@ -559,10 +559,10 @@ def run(a, job):
             # for several) against the other algorithm
             ranked = sorted((k for k in tune_algo), key=lambda k: tune[k])[:2]
             for key in ranked:
-                c = next(c for c in cands if c[0] == key)
+                cand = next(x for x in cands if x[0] == key)
                 alt = ("rccl" if tune_algo[key] != "rccl" else
                        ("acc32" if grad_dtype == "bf16" else "ordered"))
-                try_cand(f"{key}+{alt}", c[1], c[2], c[3], red=alt)
+                try_cand(f"{key}+{alt}", cand[1], cand[2], cand[3], red=alt)
         if gpu:
             torch.cuda.empty_cache()
         # the chosen engine idled while the other candidates ran: warm it again (untimed, like
