@@ -184,7 +184,8 @@ struct RowbandArgs {
 bool rowband_split_ok(int rows, int H, int in, int nh, int act);
 void set_rb_split(int v);
 void set_rb_wgsmall(int v);  // NNMPI_RB_WGSMALL: small-batch weight gradients with the update fused (1) or slabs (0)    // NNMPI_RB_SPLIT: 0 off, 2 / 4 / 8 blocks per band, else automatic
-int rowband_error_word();    // int index of the split kernel's sticky wait-timeout word in the workspace
+int rowband_error_word();
+int rowband_split_stamp_slots();   // diagnostic stamps per block of the split kernel (set_rowband_stamps)    // int index of the split kernel's sticky wait-timeout word in the workspace
 void set_rb_store_policy(int pol);   // A/B of RowbandArgs::out_pol (-1: NNMPI_RB_STORE)
 void set_rb_fixup(int on);   // 1: split-K combine inside the weight-gradient launch (default), 0: own launch
 // diagnostic: every later v2 row-band launch records per-wave phase stamps into buf

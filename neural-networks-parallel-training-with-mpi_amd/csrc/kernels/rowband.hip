@@ -655,6 +655,7 @@ static hipError_t rowband2_launch(const RowbandArgs& p, hipStream_t s) {
 // a rank's step shrinks as P grows.)
 // =============================================================================================
 constexpr int RBS_SYNC = 32;                // ints per band: phase counters [0, 2nh-1), done [31]
+constexpr int RBS_NST = 48;                 // diagnostic stamps per block
 constexpr int RBS_MAXB = 128;               // bands (4,096 rows)
 constexpr int RBS_XS = 32 + RBS_MAXB * RBS_SYNC;   // sync words at the start of the workspace
 constexpr long long RBS_TIMEOUT = 200000;   // 100 MHz ticks (2 ms) before a wait gives up
@@ -677,14 +678,17 @@ void set_rb_split(int v) { g_rbs_groups = v; }
 
 __host__ __device__ __forceinline__ int rbs_smem(int in, int nh) {
   // the band kernel's activation slots + parameter block, then the head's column-partial scratch
-  return rb2_smem_core(512, in, nh) + 512 * 4;
+  return rb2_smem_core(512, in, nh) + 512 * 4 + RBS_NST * 8;
 }
 
-template <int NJ, int NW, int ACT>
+template <int NJ, int NW, int ACT, bool ST = false>
 __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
   // (ring depth: 4 k-steps, 2 at NJ = 4 -- the 4-deep ring, the accumulators and tanh's
   // temporaries overflow the 256 VGPRs there and the compiler parks values in AGPRs, including
   // asm-loaded ring registers before their loads land)
+  // (an 8-deep ring at one tile per wave -- a block's whole slice of the next matrix in flight
+  // during a hand-off -- measured no faster: the ~1 us main loop is the MFMA / LDS dependency
+  // chain of 4 MFMAs per k-step, not the weight fetch; profiles/r5_split_stamps.txt)
   constexpr int H = 512, D = NJ >= 4 ? 2 : 4, NF = 2 * NJ, NT = 64 * NW;
   constexpr int NC = 16 * NJ * NW;  // this block's output columns (NW waves x NJ tiles of 16)
   constexpr int C = H / NC;         // blocks per band
@@ -703,6 +707,17 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
   const int nslot = max(nh, 2);
   const Rb2Par q = rb2_par(smem + nslot * SL, H, nh);
   float* red = reinterpret_cast<float*>(smem + rb2_smem_core(H, IN, nh));   // [TPC][NC]
+  // diagnostic phase stamps (ST: wave 0's shader clock at every phase boundary, LDS table after
+  // the head scratch, copied to p.stamps[block][RBS_NST] at exit; scripts/r5_split_stamps.py)
+  unsigned long long* stl = reinterpret_cast<unsigned long long*>(smem + rb2_smem_core(H, IN, nh) + 512 * 4);
+  int si = 0;
+  auto stamp = [&]() {
+    if constexpr (ST) {
+      if (tid == 0 && si < RBS_NST) stl[si] = __builtin_amdgcn_s_memtime();
+      ++si;
+    }
+  };
+  stamp();
   int* err = p.xsync;
   int* sy = p.xsync + 32 + band * RBS_SYNC;
   if (blockIdx.x == 0 && p.zero_words)
@@ -710,9 +725,11 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
 
   // ---- hand-off primitives ----
   auto arrive = [&](int ph) {   // after this block's sc1 stores of phase ph
+    stamp();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
     if (tid == 0) __hip_atomic_fetch_add(sy + ph, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    stamp();
   };
   auto wait = [&](int ph) {
     if (tid == 0) {
@@ -726,6 +743,7 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
       }
     }
     __syncthreads();
+    stamp();
   };
   // the whole band of a handed-off [rows][H] matrix into an LDS image (padding rows zero)
   auto gather = [&](const bf16* src, char* img) {
@@ -751,6 +769,7 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
       *reinterpret_cast<bf16x8*>(img + kb * (RB_ROWS * 128) + kmaj_off(r, k8)) = x;
     }
     __syncthreads();
+    stamp();
   };
   // the wave's own 32 x 16NJ tile of an LDS image -> dst rows (sc1, 16-byte pieces; the wave
   // reads back its own LDS writes: no barrier)
@@ -832,6 +851,7 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
     if (tid == 0) q.bh[0] = bhq;
   }
   __syncthreads();
+  stamp();
 
   f32x4 acc[2][NJ];
   // ---- forward: slot(l + 1) receives the whole band of a_l; the last layer's own columns go
@@ -845,6 +865,7 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
     const bool last = l == nh - 1;
     char* out = !last ? slot(l + 1) : slot(nh >= 2 ? 0 : 1);
     rb2_mainloop<NJ, D>(ring, acc, slot(l), cur, nxt, lane);
+    stamp();
     const float* bl = q.bias + l * H + n0 + 4 * (lane >> 4);
     f32x4 bv[NJ];
 #pragma unroll
@@ -982,6 +1003,7 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
       for (int j = 0; j < NJ; ++j) acc[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
     char* out = slot(l);
     rb2_mainloop<NJ, D>(ring, acc, z, cur, nxt, lane);
+    stamp();
     bf16x4 ax[2][NJ];
 #pragma unroll
     for (int i = 0; i < 2; ++i)
@@ -1016,6 +1038,11 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
     for (int i = 0; i < 2 * nh - 1; ++i) __hip_atomic_store(sy + i, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     __hip_atomic_store(sy + RBS_SYNC - 1, 0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
   }
+  if constexpr (ST) {
+    stamp();
+    __syncthreads();
+    for (int i = tid; i < RBS_NST; i += NT) p.stamps[(long long)blockIdx.x * RBS_NST + i] = stl[i];
+  }
 }
 
 bool rowband_split_ok(int rows, int H, int in, int nh, int act) {
@@ -1037,7 +1064,16 @@ static hipError_t rbs_launch(const RowbandArgs& p, hipStream_t s) {
       (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
-  const Fn f = fns[p.act == ACT_RELU ? 1 : p.act == ACT_TANH ? 2 : 0];
+  Fn f = fns[p.act == ACT_RELU ? 1 : p.act == ACT_TANH ? 2 : 0];
+  if (p.stamps) {   // diagnostic stamps: relu only
+    if (p.act != ACT_RELU) return hipErrorInvalidValue;
+    f = rowband_split_kernel<NJ, NW, ACT_RELU, true>;
+    static bool sattr = false;
+    if (!sattr) {
+      (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      sattr = true;
+    }
+  }
   const int C = 512 / (16 * NJ * NW);
   hipLaunchKernelGGL(f, dim3(rowband_blocks(p.rows) * C), dim3(64 * NW), rbs_smem(p.in, p.nh), s, p);
   return hipGetLastError();
@@ -1127,6 +1163,7 @@ static int rb_band_map() {
 static unsigned long long* g_rb_stamps = nullptr;
 void set_rowband_stamps(unsigned long long* buf) { g_rb_stamps = buf; }
 int rowband_stamp_slots() { return RB_WAVES * RB_NST; }
+int rowband_split_stamp_slots() { return RBS_NST; }
 
 // copy-out store policy (RowbandArgs::out_pol): NNMPI_RB_STORE=0/1/2 (experiments)
 static int g_rb_store = -1;
