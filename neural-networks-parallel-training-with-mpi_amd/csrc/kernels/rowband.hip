@@ -1053,6 +1053,14 @@ bool rowband_split_ok(int rows, int H, int in, int nh, int act) {
 }
 
 // (NJ x NW: 1 x 4 -> 8 blocks per band, 2 x 4 -> 4, 4 x 4 -> 2)
+// waves per block at 4 / 2 blocks per band: 8 (1 / 2 tiles per wave) or 4 (2 / 4 tiles per wave;
+// NNMPI_RB_SPLIT_WAVES=4, A/B).  Measured 24.6 vs 25.9 us at 2,048 rows and 32.4 vs 33.9 us at
+// 4,096 (profiles/r5_split_waves_ab.txt).
+static int g_rbs_waves = -1;
+static int rbs_waves() {
+  if (g_rbs_waves < 0) g_rbs_waves = rb_env("NNMPI_RB_SPLIT_WAVES", 8) == 4 ? 4 : 8;
+  return g_rbs_waves;
+}
 template <int NJ, int NW>
 static hipError_t rbs_launch(const RowbandArgs& p, hipStream_t s) {
   using Fn = void (*)(RowbandArgs);
@@ -1188,8 +1196,8 @@ hipError_t rowband_fwd_bwd(const RowbandArgs& p0, hipStream_t s) {
       if (!p.a[l]) return hipErrorInvalidValue;
     switch (rbs_groups(p.rows)) {
       case 8: return rbs_launch<1, 4>(p, s);
-      case 4: return rbs_launch<2, 4>(p, s);
-      case 2: return rbs_launch<4, 4>(p, s);
+      case 4: return rbs_waves() == 8 ? rbs_launch<1, 8>(p, s) : rbs_launch<2, 4>(p, s);
+      case 2: return rbs_waves() == 8 ? rbs_launch<2, 8>(p, s) : rbs_launch<4, 4>(p, s);
       default: return hipErrorInvalidValue;
     }
   }
@@ -1308,7 +1316,10 @@ hipError_t rowband_step(const RowbandStep& st0, hipStream_t s) {
   }
   const SlabReduce head_red{p.wslab, (int)G, H, 1, H, st.gWh, H, p.bslab, 1, st.gbh, p.loss_part,
                             (int)G, st.loss_scale, st.loss_out, st.sg};
-  if (nj > 0 && p.xsync && rb_wgsmall() && rowband_split_ok(p.rows, H, p.in, nh, p.act)) {
+  // (<= 2,048 rows: above, the un-split k loop -- ~0.35 us per 64 rows -- loses to the split-K
+  // slabs + combine: 4,096 rows 31.3 vs 16.8 + 9.1 us, 3,000 rows 25.5 vs 14.7 + 9.1;
+  // profiles/r5_wgrad_small_ab.txt)
+  if (nj > 0 && p.xsync && rb_wgsmall() && p.rows <= 2048 && rowband_split_ok(p.rows, H, p.in, nh, p.act)) {
     WgmFixArgs im[RB_MAXL];
     const bool img = st.sg.g_base && p.Pf[0];
     for (int l = l0; l < l1; ++l)

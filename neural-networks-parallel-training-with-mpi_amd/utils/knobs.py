@@ -35,6 +35,7 @@ KNOBS = {
     "NNMPI_RB_BANDMAP": "XCD-contiguous band order of the row-band kernel",
     "NNMPI_RB_STORE": "row-band copy-out store policy (0 plain, 1 nt, 2 sc1)",
     "NNMPI_RB_SPLIT": "column-split row-band kernel for small batches: 0 off, 2 / 4 / 8 blocks per band, else auto",
+    "NNMPI_RB_SPLIT_WAVES": "column-split row-band kernel: waves per block at 4 / 2 blocks per band (4 or 8)",
     "NNMPI_RB_WGSMALL": "small-batch row-band weight gradients: 1 un-split tiles with the update fused, 0 split-K slabs",
     "NNMPI_WGS_STAGES": "small-batch weight-gradient DMA ring stages (2 / 3 / 4)",
     "NNMPI_RB_FIXUP": "row-band split-K combine inside the weight-gradient launch (0: own launch)",
