@@ -270,6 +270,28 @@ def test_no_mfma_result_read_without_wait_states():
     assert _isa_check.scan_library(_build.ext_path()) == []
 
 
+def test_rowband_split_host_selection():
+    """Which batches the column-split row-band kernel takes (rowband.hip rowband_split_ok, no GPU
+    needed): the 512-wide hidden layers, input width 256 / 512, 1-4 hidden layers, up to 128
+    bands (4,096 rows) at 2-8 blocks per band, relu / tanh / none; its sync words sit at the
+    start of the workspace (the sticky wait-timeout word is int 0), which every batch size
+    reserves."""
+    from nnmpi_amd import native
+    lib = native.lib()
+    relu, tanh = 1, 2
+    for rows in (1, 37, 1000, 1024, 2048, 3001, 4096):
+        assert lib.rowband_split_ok(rows, 512, 512, 3, relu), rows
+        assert lib.rowband_split_ok(rows, 512, 512, 3, tanh), rows
+    assert lib.rowband_split_ok(999, 512, 256, 1, relu) and lib.rowband_split_ok(999, 512, 512, 4, relu)
+    for args in ((4097, 512, 512, 3), (8192, 512, 512, 3), (0, 512, 512, 3), (1024, 256, 256, 3),
+                 (1024, 1024, 1024, 2), (1024, 512, 128, 3), (1024, 512, 1024, 3),
+                 (1024, 512, 384, 3), (1024, 512, 512, 5)):
+        assert not lib.rowband_split_ok(*args, relu), args
+    assert lib.rowband_error_word() == 0
+    # (the sync area is a fixed prefix: a one-row batch already needs it)
+    assert lib.rowband_workspace_bytes(1, 512, 512, 3, 0) >= (32 + 128 * 32) * 4
+
+
 def test_rowband_host_sizing_invariants():
     """Host-side sizing of the row-band step (rowband.hip), no GPU needed: the engine sizes the
     workspace once for its row capacity and then runs batches of any size up to it, so the bytes
