@@ -1465,9 +1465,17 @@ hipError_t wgrad_multi_fix(const WgradArgs* jobs, int nj, const int* splits, con
 template <int GA, int NS>
 __global__ void __launch_bounds__(SLAB_THREADS) wgrad_small_kernel(WgradMultiParams g) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
+  // diagnostic (set_wgrad_multi_stamps, scripts/r5_wgs_stamps.py): per block the real-time
+  // counter at entry, after the GEMM, at exit
+  unsigned long long* stp = g.stamps ? g.stamps + blockIdx.x * 4 : nullptr;
+  if (stp && threadIdx.x == 0) stp[0] = __builtin_amdgcn_s_memrealtime();
   if ((int)blockIdx.x >= g.gemm_blocks) {   // the head's combine
     slab_reduce_any(g.tail_ws, g.tail, blockIdx.x - g.gemm_blocks, g.tail_nb_main, g.tail_nb_bias,
                     reinterpret_cast<f32x4*>(smem));
+    if (stp) {
+      __syncthreads();
+      if (threadIdx.x == 0) stp[2] = __builtin_amdgcn_s_memrealtime();
+    }
     return;
   }
   constexpr int MI = 2, NJ = 1;   // 64 x 64 tile, 2 x 4 waves of 32 x 16 (512 threads: the
@@ -1480,9 +1488,6 @@ __global__ void __launch_bounds__(SLAB_THREADS) wgrad_small_kernel(WgradMultiPar
       const int t = xcd_remap(bid, g.blocks[j]);
       if (t >= g.n[j]) break;
       const int tx = t % g.gx[j], ty = t / g.gx[j];
-      f32x4 acc[MI * NJ], accb[MI];
-      dma_gemm_tile<64, 64, 2, 4, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, NS, GA, false, true>(
-          g.wg[j], smem, tx, ty, 0, nullptr, acc, accb);
       const WgmFix& f = g.fix[j];
       const int M = g.wg[j].M, N = g.wg[j].N;
       const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 2, wn = w & 3;
@@ -1499,13 +1504,35 @@ __global__ void __launch_bounds__(SLAB_THREADS) wgrad_small_kernel(WgradMultiPar
           nn[k] = n0 + wn * 16 + jj * 16 + (lane >> 4) * 4;
           ok[k] = mm[k] < M && nn[k] < N;
         }
+      // Every operand of the update -- the weights' and the biases' master / momentum values --
+      // is loaded BEFORE the main loop (the oldest loads: the ring's counted vmcnt waits retire
+      // them first), so the epilogue has no dependent round trip left (per-block stamps: the
+      // epilogue was 3.4 us of a 10.3 us block with the loads after the GEMM and the bias update
+      // one more round trip behind them; scripts/r5_wgs_stamps.py)
+      const bool dob = tx == 0 && wn == 0 && (lane >> 4) == 0;   // the bias lanes
+      SgdPre4 pre[MI * NJ];
+      float bp[MI], bm[MI];
+      long long boff[MI];
       if (upd) {
-        // every fragment's master / momentum loads in flight together (one round trip), then
-        // the updates; the transposed image through LDS as 16-byte pieces (8 rows of a column)
-        SgdPre4 pre[MI * NJ];
 #pragma unroll
         for (int k = 0; k < MI * NJ; ++k)
           if (ok[k]) pre[k] = sgd_pre4(f.sg, f.out + (long long)mm[k] * N + nn[k]);
+        if (dob) {
+#pragma unroll
+          for (int i = 0; i < MI; ++i) {
+            const int m = m0 + wm * 32 + i * 16 + lane;
+            boff[i] = (f.bout + min(m, M - 1)) - f.sg.g_base;
+            bp[i] = f.sg.p_base[boff[i]];
+            bm[i] = f.sg.m_base[boff[i]];
+          }
+        }
+      }
+      f32x4 acc[MI * NJ], accb[MI];
+      dma_gemm_tile<64, 64, 2, 4, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, NS, GA, false, true>(
+          g.wg[j], smem, tx, ty, 0, nullptr, acc, accb);
+      if (stp && threadIdx.x == 0) stp[1] = __builtin_amdgcn_s_memrealtime();
+      if (upd) {
+        // the updates; the transposed image through LDS as 16-byte pieces (8 rows of a column)
         bf16* tb = reinterpret_cast<bf16*>(smem);   // [64][64] new weights of the tile
         __syncthreads();   // (every wave is past its last read of the DMA ring)
 #pragma unroll
@@ -1533,18 +1560,30 @@ __global__ void __launch_bounds__(SLAB_THREADS) wgrad_small_kernel(WgradMultiPar
         for (int k = 0; k < MI * NJ; ++k)
           if (ok[k]) *reinterpret_cast<f32x4*>(f.out + (long long)mm[k] * N + nn[k]) = acc[k];
       }
-      if (tx == 0 && wn == 0 && (lane >> 4) == 0) {   // the bias gradient: the row sums
+      if (dob) {   // the bias gradient: the row sums (sgd_fused_store's arithmetic, operands early)
 #pragma unroll
         for (int i = 0; i < MI; ++i) {
           const int m = m0 + wm * 32 + i * 16 + lane;
           if (m >= M) continue;
-          if (upd) sgd_fused_store(f.sg, f.bout + m, accb[i][0]);
-          else f.bout[m] = accb[i][0];
+          if (upd) {
+            float bb = bm[i];
+            const float pn = sgd_elem(bp[i], accb[i][0], bb, f.sg.hp[0], f.sg.hp[1], f.sg.hp[2], f.sg.hp[3],
+                                      f.sg.hp[4], f.sg.nesterov != 0, f.sg.first != 0);
+            f.sg.p_base[boff[i]] = pn;
+            if (f.sg.hp[1] != 0.f) f.sg.m_base[boff[i]] = bb;
+            if (f.sg.s_base) f.sg.s_base[boff[i]] = (bf16)pn;
+          } else {
+            f.bout[m] = accb[i][0];
+          }
         }
       }
       break;
     }
     bid -= g.blocks[j];
+  }
+  if (stp) {
+    __syncthreads();
+    if (threadIdx.x == 0) stp[2] = __builtin_amdgcn_s_memrealtime();
   }
 }
 
@@ -1580,6 +1619,7 @@ hipError_t wgrad_small(const WgradArgs* jobs, int nj, const WgmFixArgs* img, con
     slab_blocks(*tail, g.tail_nb_main, g.tail_nb_bias, nbt);
     nb += nbt;
   }
+  g.stamps = g_wgm_stamps;
   // DMA ring stages (NNMPI_WGS_STAGES 2 / 3 / 4): one 64 x 64 tile per CU streams its whole K, so
   // the ring depth is what hides the L2 round trip of each k-step
   static const int ns = [] {
