@@ -1620,17 +1620,23 @@ hipError_t wgrad_small(const WgradArgs* jobs, int nj, const WgmFixArgs* img, con
     nb += nbt;
   }
   g.stamps = g_wgm_stamps;
-  // DMA ring stages (NNMPI_WGS_STAGES 2 / 3 / 4): one 64 x 64 tile per CU streams its whole K, so
-  // the ring depth is what hides the L2 round trip of each k-step
+  // DMA ring stages (NNMPI_WGS_STAGES 2 / 3 / 4 / 6 / 8; default 4).  One 64 x 64 tile per CU
+  // streams its whole K at ~0.43 us per 16 KiB k-step (per-block stamps), but deeper rings do not
+  // help -- 6 / 8 stages 14.5 / 14.8 us vs 14.0 at 1,024 rows (profiles/r5_wgrad_small_ab.txt):
+  // the per-CU LDS-DMA fill rate (MI355X_MICROARCH.md "ldsdma-fill", ~25 GB/s per loader wave),
+  // not the round trip, bounds it
   static const int ns = [] {
     const char* e = knob_env("NNMPI_WGS_STAGES");
-    return (e && (e[0] == '2' || e[0] == '3')) ? e[0] - '0' : 4;
+    const int v = (e && e[0] >= '2' && e[0] <= '8') ? e[0] - '0' : 4;
+    return (v == 5 || v == 7) ? v + 1 : v;
   }();
   const int smem = std::max(ns * (64 + 64) * GEMM_BK * 2, SLAB_PART_BYTES);
-  auto* f = ns == 2 ? wgrad_small_kernel<2, 2> : ns == 3 ? wgrad_small_kernel<2, 3> : wgrad_small_kernel<2, 4>;
+  auto* f = ns == 2 ? wgrad_small_kernel<2, 2> : ns == 3 ? wgrad_small_kernel<2, 3>
+          : ns == 4 ? wgrad_small_kernel<2, 4> : ns == 6 ? wgrad_small_kernel<2, 6> : wgrad_small_kernel<2, 8>;
   static bool attr = false;
   if (!attr) {
-    (void)hipFuncSetAttribute((const void*)wgrad_small_kernel<2, 4>, hipFuncAttributeMaxDynamicSharedMemorySize, 64 * 1024);
+    for (auto* k : {wgrad_small_kernel<2, 4>, wgrad_small_kernel<2, 6>, wgrad_small_kernel<2, 8>})
+      (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   hipLaunchKernelGGL(f, dim3(nb), dim3(SLAB_THREADS), smem, s, g);

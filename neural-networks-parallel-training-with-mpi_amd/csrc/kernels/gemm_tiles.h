@@ -113,6 +113,21 @@ __device__ __forceinline__ constexpr int waitcnt_vm(int n) {
 template <int N>
 __device__ __forceinline__ void wait_vm() { __builtin_amdgcn_s_waitcnt(waitcnt_vm(N)); }
 
+// Retire a ring stage while min(newer, MAXN) newer stages (PT vector-memory ops each) stay in
+// flight (deep DMA rings, NS > 4).
+template <int PT, int MAXN>
+__device__ __forceinline__ void wait_vm_newer(int newer) {
+  if constexpr (MAXN > 0) {
+    if (newer >= MAXN) {
+      wait_vm<MAXN * PT>();
+      return;
+    }
+    wait_vm_newer<PT, MAXN - 1>(newer);
+  } else {
+    wait_vm<0>();
+  }
+}
+
 // XOR swizzle of the 16-byte chunk index for XMAJ images (rows of BX bf16).
 template <int BX>
 __device__ __forceinline__ int swz_x(int k) {
@@ -724,7 +739,9 @@ __device__ __forceinline__ void dma_gemm_tile(const GemmParams& p, char* smem, i
   for (int t = 0; t < nt; ++t) {
     // retire stage t: allow the (newer) stages t+1 .. min(t+NS-2, nt-1) to stay in flight
     const int newer = min(NS - 2, nt - 1 - t);
-    if constexpr (NS >= 4) {
+    if constexpr (NS >= 5) {
+      wait_vm_newer<PER_TILE, NS - 2>(newer);
+    } else if constexpr (NS >= 4) {
       if (newer >= 2) wait_vm<2 * PER_TILE>();
       else if (newer == 1) wait_vm<PER_TILE>();
       else wait_vm<0>();
