@@ -1631,11 +1631,20 @@ hipError_t wgrad_small(const WgradArgs* jobs, int nj, const WgmFixArgs* img, con
     return (v == 5 || v == 7) ? v + 1 : v;
   }();
   const int smem = std::max(ns * (64 + 64) * GEMM_BK * 2, SLAB_PART_BYTES);
+  // LDS read mode of the tile (dma_gemm_tile ASYNC_TR, NNMPI_WGS_ASYNC 2 / 3 / 4): 4 -- the
+  // refill's DMA pieces issued between the k-halves' MFMAs -- measured 13.4 vs 14.2 us (mode 2)
+  // at 1,024 rows and 18.7 vs 19.6 us at 2,048 (profiles/r5_wgrad_small_ab.txt)
+  static const int ga = [] {
+    const char* e = knob_env("NNMPI_WGS_ASYNC");
+    return (e && (e[0] == '2' || e[0] == '3')) ? e[0] - '0' : 4;
+  }();
   auto* f = ns == 2 ? wgrad_small_kernel<2, 2> : ns == 3 ? wgrad_small_kernel<2, 3>
-          : ns == 4 ? wgrad_small_kernel<2, 4> : ns == 6 ? wgrad_small_kernel<2, 6> : wgrad_small_kernel<2, 8>;
+          : ns == 4 ? (ga == 3 ? wgrad_small_kernel<3, 4> : ga == 4 ? wgrad_small_kernel<4, 4> : wgrad_small_kernel<2, 4>)
+          : ns == 6 ? wgrad_small_kernel<2, 6> : wgrad_small_kernel<2, 8>;
   static bool attr = false;
   if (!attr) {
-    for (auto* k : {wgrad_small_kernel<2, 4>, wgrad_small_kernel<2, 6>, wgrad_small_kernel<2, 8>})
+    for (auto* k : {wgrad_small_kernel<2, 4>, wgrad_small_kernel<3, 4>, wgrad_small_kernel<4, 4>,
+                    wgrad_small_kernel<2, 6>, wgrad_small_kernel<2, 8>})
       (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }

@@ -37,6 +37,7 @@ KNOBS = {
     "NNMPI_RB_SPLIT": "column-split row-band kernel for small batches: 0 off, 2 / 4 / 8 blocks per band, else auto",
     "NNMPI_RB_SPLIT_WAVES": "column-split row-band kernel: waves per block at 4 / 2 blocks per band (4 or 8)",
     "NNMPI_RB_WGSMALL": "small-batch row-band weight gradients: 1 un-split tiles with the update fused, 0 split-K slabs",
+    "NNMPI_WGS_ASYNC": "small-batch weight-gradient LDS read mode (2 / 3 / 4, dma_gemm_tile ASYNC_TR)",
     "NNMPI_WGS_STAGES": "small-batch weight-gradient DMA ring stages (2 / 3 / 4 / 6 / 8)",
     "NNMPI_RB_FIXUP": "row-band split-K combine inside the weight-gradient launch (0: own launch)",
     "NNMPI_GEMM": "GEMM main loop (1 register-staged, 2 LDS-DMA)",
