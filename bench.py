@@ -431,16 +431,29 @@ def run(a, job):
             x = float(t.item())
         return x
 
+    def device_ok(eng) -> bool:
+        """False (and the reason on stderr) when the engine's sticky device error word is set."""
+        try:
+            eng.check_device_errors()
+            return True
+        except RuntimeError as exc:
+            print(f"[bench] rank {rank}: {exc}", file=sys.stderr, flush=True)
+            return False
+
     def timed(eng, n, chunk):
         """Wall time of n steps, max over ranks (graphs captured beforehand)."""
         eng.prepare_steps(n, chunk)
         barrier()
         t0 = time.perf_counter()
         eng.run_steps(n, chunk)
-        eng.synchronize()
+        eng.synchronize(check=False)
         if gpu:
             torch.cuda.synchronize()
         el = time.perf_counter() - t0
+        # a column-split step that gave up a hand-off wait produced invalid results: the
+        # measurement is void on every rank (inf wins the max below)
+        if not device_ok(eng):
+            el = float("inf")
         pg.barrier()
         return max_over_ranks(el)
 
@@ -539,6 +552,11 @@ def run(a, job):
             e = build(m, data, bucket_mb=bmb, chunk_tiles=ct, bf16_reduce=red)
             e.run_steps(a.warmup, chunk_for(a.warmup))
             tm = min(timed(e, a.tune_steps, chunk_for(a.tune_steps)) for _ in range(2))
+            if not math.isfinite(tm):
+                # a candidate whose step gave up a device wait is never chosen
+                tune[key] = None
+                del e
+                return
             tune[key] = round(tm / a.tune_steps * 1e3, 5)
             algo = getattr(e.sync, "bf16_reduce" if grad_dtype == "bf16" else "f32_reduce", None)
             if m != "zero1" and algo:
@@ -557,12 +575,14 @@ def run(a, job):
             # (a slow default algorithm must not decide which schedule wins): each one's default
             # (bf16: acc32, one rounding; fp32: rccl for one bucket, the rank-ordered all-to-all
             # for several) against the other algorithm
-            ranked = sorted((k for k in tune_algo), key=lambda k: tune[k])[:2]
+            ranked = sorted((k for k in tune_algo if tune[k] is not None), key=lambda k: tune[k])[:2]
             for key in ranked:
                 cand = next(x for x in cands if x[0] == key)
                 alt = ("rccl" if tune_algo[key] != "rccl" else
                        ("acc32" if grad_dtype == "bf16" else "ordered"))
                 try_cand(f"{key}+{alt}", cand[1], cand[2], cand[3], red=alt)
+        if eng is None:
+            raise RuntimeError("every gradient-sync candidate gave up a device wait (invalid steps)")
         if gpu:
             torch.cuda.empty_cache()
         # the chosen engine idled while the other candidates ran: warm it again (untimed, like
@@ -586,12 +606,13 @@ def run(a, job):
     barrier()
     t0 = time.perf_counter()
     eng.run_steps(a.steps, chunk)
-    eng.synchronize()
+    eng.synchronize(check=False)
     if gpu:
         torch.cuda.synchronize()
     t1 = time.perf_counter()
     pg.barrier()
     elapsed = max_over_ranks(t1 - t0)
+    # (raises on a timed-out column-split hand-off: no line is printed for an invalid step)
     loss = eng.loss()
     ms = elapsed / a.steps * 1e3
     value = n_global * a.steps / elapsed
@@ -662,6 +683,9 @@ def run(a, job):
             e = build("none", data, comm=False)
             e.run_steps(min(a.warmup, 10) + 1, chunk_for(min(a.warmup, 10)))
             res["comp_ms"] = timed(e, n_ex, chunk_for(n_ex)) / n_ex * 1e3
+            if not math.isfinite(res["comp_ms"]):
+                res["comp_ms"] = None
+                raise RuntimeError("a column-split hand-off wait timed out: single-GPU step invalid")
 
         def strong_scaling():
             # strong scaling: the reference's fixed dataset (the 1-GPU shard, 8192 rows for the
@@ -672,6 +696,8 @@ def run(a, job):
                       chunk_tiles=chunk_tiles, bf16_reduce=bf16_reduce)
             e.run_steps(min(a.warmup, 10) + 1, chunk_for(min(a.warmup, 10)))
             s_ms = timed(e, n_ex, chunk_for(n_ex)) / n_ex * 1e3
+            if not math.isfinite(s_ms):
+                raise RuntimeError("a column-split hand-off wait timed out: strong-scaling step invalid")
             comp_ms = res["comp_ms"]
             # S(1): the single-GPU step of the whole dataset = the compute-only step above
             # (weak scaling gives every rank rows_pg rows, the last one rows_pg - 1)

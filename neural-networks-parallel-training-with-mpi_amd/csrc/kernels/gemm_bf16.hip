@@ -872,8 +872,11 @@ struct WgradMultiParams {
   int tail_ws, tail_nb_main, tail_nb_bias;
 };
 // diagnostic (scripts/r5_wg_stamps.py): every later wgrad_multi launch records per-block stamps
+// (the stamped twins are compiled into the experiments library only)
 static unsigned long long* g_wgm_stamps = nullptr;
+#if NNMPI_EXPERIMENTS_BUILD
 void set_wgrad_multi_stamps(unsigned long long* buf) { g_wgm_stamps = buf; }
+#endif
 
 // NS: LDS stages of the DMA ring.  The launch holds about one block per CU (3 jobs x 16 tiles x 5
 // splits = 240 blocks on the proxy step), so no second block hides a k-step's DMA wait; a
@@ -1269,6 +1272,7 @@ __global__ void __launch_bounds__(GRP_THREADS, (NS == 0 || GA >= 3 || FIX || ST)
 // 128 x 128 tile at one block per CU: wait 320 + barrier 88 + DMA issue 412 + reads and MFMAs
 // 892 cycles, in lockstep -- profiles/r5_wgrad_kstep_stamps.txt).  Same K split, same slab
 // layout, same per-element accumulation order: bitwise the 128 x 128 tile's slabs.
+#if NNMPI_EXPERIMENTS_BUILD
 constexpr int WGH_BM = 128, WGH_BN = 64, WGH_WGM = 2, WGH_WGN = 2;
 constexpr int WGH_THREADS = 64 * WGH_WGM * WGH_WGN;
 constexpr int WGH_SMEM = 2 * (WGH_BM + WGH_BN) * GEMM_BK * 2;
@@ -1301,14 +1305,22 @@ static int wgm_tile() {
   }
   return g_wgm_tile;
 }
+#else
+static constexpr int wgm_tile() { return 0; }
+#endif
 
 // Kernel variant of a wgrad_multi launch: DMA ring stages (NNMPI_WG_STAGES 2 / 3 / 4, or 0 =
 // register-staged, NNMPI_WG_REG=1), LDS read mode (dma_gemm_tile ASYNC_TR; NNMPI_WGM_ASYNC or
 // set_group_async), in-launch fixup, diagnostic stamps.
 template <int GA, int NS>
 static void* wgm_fn(bool fix, bool st) {
+#if NNMPI_EXPERIMENTS_BUILD
   if (fix) return st ? (void*)wgrad_multi_kernel<GA, NS, true, true> : (void*)wgrad_multi_kernel<GA, NS, false, true>;
   return st ? (void*)wgrad_multi_kernel<GA, NS, true, false> : (void*)wgrad_multi_kernel<GA, NS, false, false>;
+#else
+  // (the production library: neither the in-launch fixup nor the stamped twin)
+  return (fix || st) ? nullptr : (void*)wgrad_multi_kernel<GA, NS, false, false>;
+#endif
 }
 
 static hipError_t wgm_launch(const WgradMultiParams& g, int nb, bool fix, hipStream_t s) {
@@ -1322,11 +1334,16 @@ static hipError_t wgm_launch(const WgradMultiParams& g, int nb, bool fix, hipStr
   if (ga < 2) ga = 2;                  // (the compiler-scheduled / whole-stage read modes retired)
   const bool st = g.stamps != nullptr;
   void* f = nullptr;
+#if NNMPI_EXPERIMENTS_BUILD
   if (ns == 0) f = st ? (void*)wgrad_multi_kernel<2, 0, true> : (void*)wgrad_multi_kernel<2, 0>;
+#else
+  if (ns == 0) f = st ? nullptr : (void*)wgrad_multi_kernel<2, 0>;
+#endif
   else if (ns == 3) f = ga == 2 ? wgm_fn<2, 3>(fix, st) : ga == 3 ? wgm_fn<3, 3>(fix, st) : wgm_fn<4, 3>(fix, st);
   else if (ns == WGM_NS) f = ga == 2 ? wgm_fn<2, WGM_NS>(fix, st) : ga == 3 ? wgm_fn<3, WGM_NS>(fix, st)
                                                                    : wgm_fn<4, WGM_NS>(fix, st);
   else f = ga == 2 ? wgm_fn<2, 2>(fix, st) : ga == 3 ? wgm_fn<3, 2>(fix, st) : wgm_fn<4, 2>(fix, st);
+  if (!f) return hipErrorNotSupported;
   const int smem = (ns == 0 ? 2 : ns) * (GRP_BM + GRP_BN) * GEMM_BK * 2;
   static void* attr_done[64] = {};
   bool seen = false;
@@ -1374,13 +1391,18 @@ hipError_t wgrad_multi(const WgradArgs* jobs, int nj, const int* splits, SlabRed
     set_extents<XMAJ, XMAJ>(p);
     p.store_pol = slab_store_pol();
     g.wg[j] = p;
+#if NNMPI_EXPERIMENTS_BUILD
     const int bn = wgm_tile() == 1 ? WGH_BN : GRP_BN;
+#else
+    const int bn = GRP_BN;
+#endif
     g.gx[j] = (p.N + bn - 1) / bn;
     g.tiles[j] = g.gx[j] * ((p.M + GRP_BM - 1) / GRP_BM);
     g.n[j] = g.tiles[j] * sp;
     g.blocks[j] = (g.n[j] + 7) & ~7;
     nb += g.blocks[j];
   }
+#if NNMPI_EXPERIMENTS_BUILD
   if (wgm_tile() == 1) {
     static const int env_ga = [] {
       const char* e = knob_env("NNMPI_WGM_ASYNC");
@@ -1400,19 +1422,23 @@ hipError_t wgrad_multi(const WgradArgs* jobs, int nj, const int* splits, SlabRed
                        WGH_SMEM, s, g);
     return hipGetLastError();
   }
+#endif
   g.stamps = g_wgm_stamps;
   return wgm_launch(g, nb, false, s);
 }
 
+#if NNMPI_EXPERIMENTS_BUILD
 int wgrad_fix_counters(int M, int N) {
   return ((M + GRP_BM - 1) / GRP_BM) * ((N + GRP_BN - 1) / GRP_BN) * WGM_CW;
 }
+#endif
 
 // The row-band step's weight gradients with the in-launch fixup (one launch, no combine launch):
 // jobs as wgrad_multi; fix[j] says where job j's result goes (its out / bout / sg / images; cnt =
 // its tile counters, zero); `tail` (may have S == 0 / null loss): an extra combine run by blocks
 // appended to the grid (the head's per-band partials).
-hipError_t wgrad_multi_fix(const WgradArgs* jobs, int nj, const int* splits, const WgmFixArgs* fix,
+#if NNMPI_EXPERIMENTS_BUILD
+hipError_t wgrad_multi_fix(const WgradArgs* jobs, int nj, const int* splits, const WgOut* fix,
                            const SlabReduce* tail, hipStream_t s) {
   if (nj < 1 || nj > RB_MAXL) return hipErrorInvalidValue;
   WgradMultiParams g{};
@@ -1453,6 +1479,7 @@ hipError_t wgrad_multi_fix(const WgradArgs* jobs, int nj, const int* splits, con
   g.stamps = g_wgm_stamps;
   return wgm_launch(g, nb, true, s);
 }
+#endif
 
 // ---- Small-batch weight gradients, update in the epilogue (the column-split row-band step) ----
 // At <= 4,096 rows wgrad_multi's split-K slabs (5 per layer at 1,024 rows) and their combine
@@ -1467,7 +1494,7 @@ __global__ void __launch_bounds__(SLAB_THREADS) wgrad_small_kernel(WgradMultiPar
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   // diagnostic (set_wgrad_multi_stamps, scripts/r5_wgs_stamps.py): per block the real-time
   // counter at entry, after the GEMM, at exit
-  unsigned long long* stp = g.stamps ? g.stamps + blockIdx.x * 4 : nullptr;
+  unsigned long long* stp = (NNMPI_EXPERIMENTS_BUILD && g.stamps) ? g.stamps + blockIdx.x * 4 : nullptr;
   if (stp && threadIdx.x == 0) stp[0] = __builtin_amdgcn_s_memrealtime();
   if ((int)blockIdx.x >= g.gemm_blocks) {   // the head's combine
     slab_reduce_any(g.tail_ws, g.tail, blockIdx.x - g.gemm_blocks, g.tail_nb_main, g.tail_nb_bias,
@@ -1587,7 +1614,7 @@ __global__ void __launch_bounds__(SLAB_THREADS) wgrad_small_kernel(WgradMultiPar
   }
 }
 
-hipError_t wgrad_small(const WgradArgs* jobs, int nj, const WgmFixArgs* img, const SlabReduce* tail,
+hipError_t wgrad_small(const WgradArgs* jobs, int nj, const WgOut* img, const SlabReduce* tail,
                        hipStream_t s) {
   if (nj < 1 || nj > RB_MAXL) return hipErrorInvalidValue;
   WgradMultiParams g{};
@@ -1708,6 +1735,7 @@ hipError_t wide_pair(const WgradArgs& w1, const DgradArgs* dg, const WgradArgs* 
   return exp_wide_pair(w1, dg, w2, s);
 }
 
+#if NNMPI_EXPERIMENTS_BUILD
 // diagnostic: the 128x128 forward with per-block stamps (experiments translation unit)
 hipError_t linear_fwd_bf16_stamped(const bf16* X, int ldx, const bf16* W, int ldw, const float* bias,
                                    bf16* Y, int ldy, int M, int N, int K, unsigned long long* stamps,
@@ -1715,6 +1743,7 @@ hipError_t linear_fwd_bf16_stamped(const bf16* X, int ldx, const bf16* W, int ld
   if (!exp_fwd_stamped) return hipErrorNotSupported;
   return exp_fwd_stamped(X, ldx, W, ldw, bias, Y, ldy, M, N, K, stamps, s);
 }
+#endif
 
 bool experiments_built() { return exp_wide_pair != nullptr; }
 

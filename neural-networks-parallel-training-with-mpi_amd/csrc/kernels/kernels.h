@@ -1,6 +1,7 @@
 // Host-side launch API of the gfx950 kernels (all launches are asynchronous on `stream`, make
 // no allocation and no host synchronisation, so every one of them is hipGraph-capturable).
 #pragma once
+#include "knobs.h"
 #include <hip/hip_runtime.h>
 #include <stddef.h>
 #include <stdint.h>
@@ -73,8 +74,8 @@ void set_pp256_order(int epi, int idx);   // 256x256 kernel tile order per epilo
 void set_store_policy(int p);
 void set_slab_store_policy(int p);   // split-K slab stores of the grouped backward (-2: env)  // LDS-epilogue output stores: 0 plain, 1 nt, 2 sc1 (experiments)
 void set_head_xcd_rows(int v);  // head kernels: rows of XCD-remapped logical blocks (experiment)
-// diagnostic: the default 128x128 forward kernel with per-block entry/exit real-time stamps
-// (stamps: 2 * grid uint64, 100 MHz counter)
+// diagnostic (experiments library): the default 128x128 forward kernel with per-block
+// entry/exit real-time stamps (stamps: 2 * grid uint64, 100 MHz counter)
 hipError_t linear_fwd_bf16_stamped(const bf16* X, int ldx, const bf16* W, int ldw, const float* bias,
                                    bf16* Y, int ldy, int M, int N, int K, unsigned long long* stamps,
                                    hipStream_t s);
@@ -178,16 +179,19 @@ struct RowbandArgs {
   // counter + error word (zero, self-resetting) and the head's partial-dot exchange buffer
   int* xsync = nullptr;
   float* hx = nullptr;
+  int rbs_bands = 0;   // (set by the launch) bands; rbs_map: XCD-grouped block map, grid padded
+  int rbs_map = 0;     // to whole 8-band groups; rbs_local: plain hand-off stores for a band whose
+  int rbs_local = 0;   // blocks all report one XCC id
 };
 // the column-split row-band kernel takes this batch (H = 512, in <= 512, rows below the
 // full-band threshold): 8 blocks per 32-row band, each one 64-column slice of every layer
 bool rowband_split_ok(int rows, int H, int in, int nh, int act);
-void set_rb_split(int v);
-void set_rb_wgsmall(int v);  // NNMPI_RB_WGSMALL: small-batch weight gradients with the update fused (1) or slabs (0)    // NNMPI_RB_SPLIT: 0 off, 2 / 4 / 8 blocks per band, else automatic
-int rowband_error_word();
-int rowband_split_stamp_slots();   // diagnostic stamps per block of the split kernel (set_rowband_stamps)    // int index of the split kernel's sticky wait-timeout word in the workspace
+void set_rb_split(int v);    // NNMPI_RB_SPLIT: 0 off, 2 / 4 / 8 blocks per band, else automatic
+void set_rb_wgsmall(int v);  // NNMPI_RB_WGSMALL: small-batch weight gradients with the update fused (1) or slabs (0)
+int rowband_error_word();    // int index of the split kernel's sticky wait-timeout word in the workspace
+int rowband_split_stamp_slots();   // diagnostic stamps per block of the split kernel (set_rowband_stamps)
 void set_rb_store_policy(int pol);   // A/B of RowbandArgs::out_pol (-1: NNMPI_RB_STORE)
-void set_rb_fixup(int on);   // 1: split-K combine inside the weight-gradient launch (default), 0: own launch
+void set_rb_fixup(int on);   // experiments library: 1 = split-K combine inside the weight-gradient launch, 0 = own launch (default)
 // diagnostic: every later v2 row-band launch records per-wave phase stamps into buf
 // (rowband_blocks(rows) x rowband_stamp_slots() uint64; null = off)
 void set_rowband_stamps(unsigned long long* buf);
@@ -235,18 +239,22 @@ hipError_t slab_reduce_multi(const SlabReduce* r, int nr, hipStream_t s);
 // last at a tile sums the tile's slabs (slab_multi's order: bitwise the same result) and applies
 // the update (job.sg) or stores the gradient (job.dW / job.db), plus the row-band images; `tail`
 // (may be null) is one more combine run by extra blocks of the same launch.
-struct WgmFixArgs {
+struct WgOut {
   bf16* pkf; bf16* pkd;   // with job.sg: the updated W's fragment-major images (null: none)
-  int* cnt;               // per-tile counter words (wgrad_fix_counters of them), zero
+  int* cnt;               // in-launch fixup (experiments library): per-tile counter words, zero
 };
+#if NNMPI_EXPERIMENTS_BUILD
 int wgrad_fix_counters(int M, int N);
+#endif
 // Small-batch weight gradients of several layers in ONE launch: 64 x 64 tiles over the whole K
 // (no split), SGD-momentum + the row-band v2 images (img[j], may be null) in the epilogue when
 // jobs[j].sg is set (else the gradient), the head's combine `tail` (may be null) in extra blocks.
-hipError_t wgrad_small(const WgradArgs* jobs, int nj, const WgmFixArgs* img, const SlabReduce* tail,
+hipError_t wgrad_small(const WgradArgs* jobs, int nj, const WgOut* img, const SlabReduce* tail,
                        hipStream_t s);
-hipError_t wgrad_multi_fix(const WgradArgs* jobs, int nj, const int* splits, const WgmFixArgs* fix,
+#if NNMPI_EXPERIMENTS_BUILD
+hipError_t wgrad_multi_fix(const WgradArgs* jobs, int nj, const int* splits, const WgOut* fix,
                            const SlabReduce* tail, hipStream_t s);
+#endif
 
 // ---- fp32 GEMM (gemm_f32.hip) ----
 hipError_t linear_fwd_f32(const float* X, int ldx, const float* W, int ldw, const float* bias,

@@ -8,6 +8,7 @@
 // Hyper-parameters are read from device memory so a captured hipGraph picks up LR changes.
 #include "common.h"
 #include "kernels.h"
+#include "knobs.h"
 
 #include <algorithm>
 
@@ -64,6 +65,137 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, TG* __r
   }
 }
 
+// The optimizer pass that also refreshes the row-band v2 weight images (the multi-rank row-band
+// step: its update follows the all-reduce, so the combines cannot apply it).  The matrices that
+// have images are cut into 32 x 32 tiles, one per block: each thread updates one float4 of a row
+// (master, momentum, bf16 shadow, the forward image's 8-byte piece) and parks the new bf16 values
+// in LDS; the transposed image is then written as 16-byte pieces (8 rows of one column) -- where
+// the element-wise pass above does one 64-bit division per float4 per matrix to place it and
+// four scattered 2-byte stores for the transposed image.  Blocks past the tiles run the
+// element-wise update over the rest of the range (biases, the head, padding).
+struct SgdTileJob {
+  int n;                               // matrices with images
+  long long start[RB_MAXL_PK];         // element offset in the pass's range (% 4 == 0)
+  int M[RB_MAXL_PK], N[RB_MAXL_PK];    // (% 32 == 0)
+  bf16* pkf[RB_MAXL_PK];
+  bf16* pkd[RB_MAXL_PK];
+  int tx[RB_MAXL_PK], t0[RB_MAXL_PK + 1];   // tiles per row of tiles; first tile of matrix t
+  long long ps[RB_MAXL_PK + 1], pe[RB_MAXL_PK + 1];   // the other float4 ranges [ps, pe)
+  int np;
+};
+
+template <typename TG>
+__global__ void __launch_bounds__(256) sgd_tiles_kernel(float* __restrict__ p, TG* __restrict__ g,
+                                                        float* __restrict__ buf, bf16* __restrict__ shadow,
+                                                        const float* __restrict__ hp, int nesterov,
+                                                        int first, int zero_grad, SgdTileJob j) {
+  const float lr = hp[0], mom = hp[1], damp = hp[2], wd = hp[3], gs = hp[4];
+  auto upd = [&](long long i) -> f32x4 {
+    f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
+    const f32x4 gv = load_grad4(g, i);
+    f32x4 bv = (mom != 0.f && !first) ? reinterpret_cast<f32x4*>(buf)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int r = 0; r < 4; ++r) {
+      float bb = bv[r];
+      pv[r] = sgd_elem(pv[r], gv[r], bb, lr, mom, damp, wd, gs, nesterov != 0, first != 0);
+      bv[r] = bb;
+    }
+    if (mom != 0.f) reinterpret_cast<f32x4*>(buf)[i] = bv;
+    reinterpret_cast<f32x4*>(p)[i] = pv;
+    if (shadow) {
+      bf16x4 sv;
+#pragma unroll
+      for (int r = 0; r < 4; ++r) sv[r] = (bf16)pv[r];
+      reinterpret_cast<bf16x4*>(shadow)[i] = sv;
+    }
+    if constexpr (sizeof(TG) == 4) {
+      if (zero_grad) reinterpret_cast<f32x4*>(g)[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    }
+    return pv;
+  };
+  const int tid = threadIdx.x;
+  const int bid = blockIdx.x;
+  if (bid >= j.t0[j.n]) {   // the element-wise rest, grid-stride over its blocks
+    const long long nb = gridDim.x - j.t0[j.n];
+    for (int q = 0; q < j.np; ++q)
+      for (long long i = j.ps[q] + (long long)(bid - j.t0[j.n]) * 256 + tid; i < j.pe[q]; i += nb * 256)
+        (void)upd(i);
+    return;
+  }
+  int t = 0;
+  while (t + 1 < j.n && bid >= j.t0[t + 1]) ++t;
+  const int tile = bid - j.t0[t], M = j.M[t], N = j.N[t];
+  const int m0 = (tile / j.tx[t]) * 32, n0 = (tile % j.tx[t]) * 32;
+  const int r = tid >> 3, c4 = tid & 7, m = m0 + r, n = n0 + 4 * c4;
+  __shared__ bf16 tb[32][32 + 8];   // (+8: the column reads below hit different banks)
+  const f32x4 pv = upd((j.start[t] + (long long)m * N + n) / 4);
+  bf16x4 hv;
+#pragma unroll
+  for (int e = 0; e < 4; ++e) hv[e] = (bf16)pv[e];
+  if (j.pkf[t]) *reinterpret_cast<bf16x4*>(j.pkf[t] + rb_pk_off(m, n, N)) = hv;
+  if (j.pkd[t]) {
+    *reinterpret_cast<bf16x4*>(&tb[r][4 * c4]) = hv;
+    __syncthreads();
+    if (tid < 128) {   // column c, rows m0 + 8 g8 .. + 7 -> one 16-byte piece of the W^T image
+      const int c = tid & 31, g8 = tid >> 5;
+      bf16x8 col;
+#pragma unroll
+      for (int e = 0; e < 8; ++e) col[e] = tb[8 * g8 + e][c];
+      *reinterpret_cast<bf16x8*>(j.pkd[t] + rb_pk_off(n0 + c, m0 + 8 * g8, M)) = col;
+    }
+  }
+}
+
+// The tile job of a pass over n elements with the images of `pk` (false: a shape the tiles do not
+// cover -- the element-wise kernel takes it).
+static bool sgd_tile_job(const SgdPack& pk, long long n, SgdTileJob& j) {
+  j = SgdTileJob{};
+  j.n = pk.n;
+  int tiles = 0;
+  // matrices in arena order, each inside the range
+  int ord[RB_MAXL_PK];
+  for (int t = 0; t < pk.n; ++t) ord[t] = t;
+  std::sort(ord, ord + pk.n, [&](int a, int b) { return pk.start[a] < pk.start[b]; });
+  long long at = 0;
+  for (int k = 0; k < pk.n; ++k) {
+    const int t = ord[k];
+    const long long s = pk.start[t], e = s + (long long)pk.M[t] * pk.N[t];
+    if (s < at || e > n || pk.M[t] % 32 || pk.N[t] % 32 || s % 4) return false;
+    j.start[k] = s; j.M[k] = pk.M[t]; j.N[k] = pk.N[t];
+    j.pkf[k] = pk.pkf[t]; j.pkd[k] = pk.pkd[t];
+    j.tx[k] = pk.N[t] / 32;
+    j.t0[k] = tiles;
+    tiles += (pk.M[t] / 32) * (pk.N[t] / 32);
+    if (s > at) { j.ps[j.np] = at / 4; j.pe[j.np] = s / 4; ++j.np; }
+    at = e;
+  }
+  j.t0[pk.n] = tiles;
+  if (at < n) { j.ps[j.np] = at / 4; j.pe[j.np] = n / 4; ++j.np; }
+  return true;
+}
+
+template <typename TG>
+static hipError_t sgd_tiles_launch(float* p, TG* g, float* buf, bf16* shadow, long long n,
+                                   const float* hp, int nesterov, int first, int zero_grad,
+                                   const SgdTileJob& j, hipStream_t s) {
+  long long rest = 0;
+  for (int q = 0; q < j.np; ++q) rest += j.pe[q] - j.ps[q];
+  const int nb_rest = rest > 0 ? (int)std::min<long long>((rest + 255) / 256, 64) : 0;
+  hipLaunchKernelGGL(sgd_tiles_kernel<TG>, dim3(j.t0[j.n] + nb_rest), dim3(256), 0, s, p, g, buf,
+                     shadow, hp, nesterov, first, zero_grad, j);
+  return hipGetLastError();
+}
+
+static int g_sgd_tiles = -1;   // NNMPI_SGD_TILES=0: the element-wise image refresh (A/B)
+void set_sgd_tiles(int v) { g_sgd_tiles = v; }   // -1: re-read the knob
+static bool sgd_tiles_on() {
+  if (g_sgd_tiles < 0) {
+    const char* e = knob_env("NNMPI_SGD_TILES");
+    g_sgd_tiles = (e && e[0] == '0') ? 0 : 1;
+  }
+  return g_sgd_tiles == 1;
+}
+
 static int grid_for(long long n, int per_thread = 1) {
   const long long b = (n / per_thread + 255) / 256;
   return (int)std::max<long long>(1, std::min<long long>(b, 2048));
@@ -82,6 +214,9 @@ hipError_t sgd_momentum(float* p, float* g, float* buf, bf16* shadow, long long 
                         const SgdPack* pack) {
   if (n % 4 != 0 || !pack_ok(pack)) return hipErrorInvalidValue;
   const SgdPack pk = pack ? *pack : SgdPack{};
+  SgdTileJob j;
+  if (pk.n > 0 && sgd_tiles_on() && sgd_tile_job(pk, n, j))
+    return sgd_tiles_launch<float>(p, g, buf, shadow, n, hp, nesterov, first, zero_grad, j, s);
   hipLaunchKernelGGL(sgd_kernel<float>, dim3(grid_for(n / 4)), dim3(256), 0, s, p, g, buf, shadow,
                      n / 4, hp, nesterov, first, zero_grad, pk);
   return hipGetLastError();
@@ -104,6 +239,9 @@ hipError_t sgd_momentum_bf16grad(float* p, const bf16* g, float* buf, bf16* shad
                                  const SgdPack* pack) {
   if (n % 4 != 0 || !pack_ok(pack)) return hipErrorInvalidValue;
   const SgdPack pk = pack ? *pack : SgdPack{};
+  SgdTileJob j;
+  if (pk.n > 0 && sgd_tiles_on() && sgd_tile_job(pk, n, j))
+    return sgd_tiles_launch<const bf16>(p, g, buf, shadow, n, hp, nesterov, first, 0, j, s);
   hipLaunchKernelGGL(sgd_kernel<const bf16>, dim3(grid_for(n / 4)), dim3(256), 0, s, p, g, buf,
                      shadow, n / 4, hp, nesterov, first, 0, pk);
   return hipGetLastError();

@@ -606,8 +606,8 @@ static hipError_t rowband2_launch(const RowbandArgs& p, hipStream_t s) {
   }
   const Fn f = fns[p.act == ACT_RELU ? 1 : p.act == ACT_TANH ? 2 : 0];
   if (p.stamps) {
-    // diagnostic phase stamps: H = 512, relu only
-    if constexpr (H == 512) {
+    // diagnostic phase stamps: H = 512, relu only (experiments library)
+    if constexpr (H == 512 && NNMPI_EXPERIMENTS_BUILD) {
       if (p.act != ACT_RELU || rb2_smem(H, p.in, p.nh, true) > 160 * 1024) return hipErrorInvalidValue;
       static bool sattr = false;
       if (!sattr) {
@@ -697,8 +697,21 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   const int tid = threadIdx.x, lane = tid & 63;
   const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
-  const int band = blockIdx.x / C, c = blockIdx.x % C;
-  const int row0 = band * RB_ROWS, nvalid = min(RB_ROWS, p.rows - row0);
+  // Block -> (band, column group).  XCD-grouped map (p.rbs_map): blocks are dealt round-robin
+  // over the 8 XCDs (b and b + 8 share one -- observed placement, speed only), so the C blocks of
+  // a band are C consecutive ids among those with the same b % 8 and its hand-offs can stay in
+  // one L2; the grid is padded to a multiple of 8 bands (padding bands exit at once).  Else the
+  // C blocks of a band are consecutive ids (one per XCD at C = 8).
+  int band, c;
+  if (p.rbs_map) {
+    const int x = blockIdx.x & 7, j = blockIdx.x >> 3;
+    band = (j / C) * 8 + x;
+    c = j % C;
+  } else {
+    band = blockIdx.x / C;
+    c = blockIdx.x % C;
+  }
+  const int row0 = band * RB_ROWS, nvalid = max(0, min(RB_ROWS, p.rows - row0));
   const int nh = p.nh, IN = p.in;
   const int c0 = c * NC;                  // the block's first column
   const int n0 = c0 + w * 16 * NJ;        // the wave's first column
@@ -722,28 +735,68 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
   int* sy = p.xsync + 32 + band * RBS_SYNC;
   if (blockIdx.x == 0 && p.zero_words)
     for (int i = tid; i < p.n_zero; i += NT) p.zero_words[i] = 0;
+  if (band >= p.rbs_bands) return;   // a padding band of the XCD-grouped map: no block of it works
+  // The first hand-off's counter (phase 0) also says where the band runs: each block adds
+  // 1 << 4 * (its XCC id), so the word holds per-XCC arrival counts (C <= 8 < 16 per nibble).
+  // When every block of the band sits on one XCC, the later hand-offs store PLAIN (the bytes stay
+  // in that XCD's L2, which the consumers' sc1 loads read) instead of write-through -- decided
+  // from the hardware's XCC ids, not from the dispatch order the band map hopes for; a band that
+  // spans XCCs keeps the write-through form.
+  const unsigned xcc = __builtin_amdgcn_s_getreg(20 | (31 << 11)) & 7;   // HW_REG_XCC_ID
+  bool local = false;   // (uniform in the block: set after phase 0 from the counter's final value)
 
   // ---- hand-off primitives ----
-  auto arrive = [&](int ph) {   // after this block's sc1 stores of phase ph
+  auto arrive = [&](int ph) {   // after this block's stores of phase ph
     stamp();
     asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
     __syncthreads();
-    if (tid == 0) __hip_atomic_fetch_add(sy + ph, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+    if (tid == 0)
+      __hip_atomic_fetch_add(sy + ph, ph == 0 ? 1 << (4 * xcc) : 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
     stamp();
+  };
+  int* lflag = reinterpret_cast<int*>(red);   // (LDS word: phase 0's placement verdict)
+  auto arrivals = [&](int ph, int v) {
+    if (ph != 0) return v;
+    int n = 0;
+#pragma unroll
+    for (int x = 0; x < 8; ++x) n += (v >> (4 * x)) & 15;
+    return n;
   };
   auto wait = [&](int ph) {
     if (tid == 0) {
       const long long t0 = __builtin_amdgcn_s_memrealtime();
-      while (ld_sc1_i(sy + ph) < C) {
+      int v;
+      while (arrivals(ph, v = ld_sc1_i(sy + ph)) < C) {
         if (__builtin_amdgcn_s_memrealtime() - t0 > RBS_TIMEOUT) {
           __hip_atomic_fetch_or(err, 1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_AGENT);
+          v = 0;   // (a timed-out band keeps the write-through form)
           break;
         }
         __builtin_amdgcn_s_sleep(1);
       }
+      // every block of the band counted on ONE XCC: exactly one nonzero nibble
+      if (ph == 0) {
+        int nz = 0;
+#pragma unroll
+        for (int x = 0; x < 8; ++x) nz += ((v >> (4 * x)) & 15) != 0;
+        lflag[0] = p.rbs_local && nz == 1;
+      }
     }
     __syncthreads();
+    if (ph == 0) {
+      local = lflag[0] != 0;
+      __syncthreads();   // (the word is the head scratch later)
+    }
     stamp();
+  };
+  // a 16-byte piece of a handed-off matrix: plain when the band is on one XCC, else write-through
+  auto st16 = [&](bf16* dst, bf16x8 v) {
+    typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
+    const u32x4 d = __builtin_bit_cast(u32x4, v);
+    if (local)
+      asm volatile("global_store_dwordx4 %0, %1, off\n s_nop 1" ::"v"(dst), "v"(d) : "memory");
+    else
+      asm volatile("global_store_dwordx4 %0, %1, off sc1\n s_nop 1" ::"v"(dst), "v"(d) : "memory");
   };
   // the whole band of a handed-off [rows][H] matrix into an LDS image (padding rows zero)
   auto gather = [&](const bf16* src, char* img) {
@@ -781,12 +834,7 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
     for (int jj = 0; jj < NJ; ++jj) {
       const int k = n0 + 8 * ((lane & 1) + 2 * jj);
       const bf16x8 v = *reinterpret_cast<const bf16x8*>(img + rb_off(r, k));
-      if (r < nvalid) {
-        typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
-        const u32x4 d = __builtin_bit_cast(u32x4, v);
-        asm volatile("global_store_dwordx4 %0, %1, off sc1\n s_nop 1" ::"v"(dst + (long long)(row0 + r) * H + k), "v"(d)
-                     : "memory");
-      }
+      if (r < nvalid) st16(dst + (long long)(row0 + r) * H + k, v);
     }
   };
 
@@ -910,7 +958,11 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
     }
 #pragma unroll
     for (int sh = TPR / 2; sh >= 1; sh >>= 1) dot += __shfl_xor(dot, sh, 64);
-    if (g == 0) st_sc1_f(p.hx + ((long long)band * C + c) * RB_ROWS + r, dot);
+    if (g == 0) {
+      float* hp = p.hx + ((long long)band * C + c) * RB_ROWS + r;
+      if (local) *hp = dot;
+      else st_sc1_f(hp, dot);
+    }
   }
   arrive(nh - 1);
   wait(nh - 1);
@@ -981,12 +1033,7 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
         o[e] = (bf16)(dl * w0[e] * act_bwd_t<ACT>((float)v[e]));
         o[4 + e] = (bf16)(dl * w1[e] * act_bwd_t<ACT>((float)v[4 + e]));
       }
-      if (r < nvalid) {
-        typedef __attribute__((ext_vector_type(4))) unsigned u32x4;
-        const u32x4 dd = __builtin_bit_cast(u32x4, o);
-        asm volatile("global_store_dwordx4 %0, %1, off sc1\n s_nop 1"
-                     ::"v"(p.dz[nh - 1] + (long long)(row0 + r) * H + k), "v"(dd) : "memory");
-      }
+      if (r < nvalid) st16(p.dz[nh - 1] + (long long)(row0 + r) * H + k, o);
     }
   }
   if (nh >= 2) {
@@ -1045,21 +1092,84 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
   }
 }
 
+template <int NJ, int NW>
+static hipError_t rbs_launch(const RowbandArgs& p, hipStream_t s);
+template <int NJ, int NW>
+static int rbs_occupancy(int smem);
+static int rbs_waves();
+static int rbs_map();
+
+// The split kernel's blocks of a band wait for each other, so the grid must fit the chip at the
+// kernel's occupancy (all blocks resident at once when nothing else holds CUs; with CUs held by
+// another stream a band still completes once resident bands exit -- the bounded wait covers the
+// rest).  The occupancy query is made once per (form, LDS size).
+static bool rbs_fits(int rows, int in, int nh) {
+  const int C = rbs_groups(rows);
+  if (C <= 0) return false;
+  const int smem = rbs_smem(in, nh);
+  int per_cu = 0;
+  switch (C) {
+    case 8: per_cu = rbs_occupancy<1, 4>(smem); break;
+    case 4: per_cu = rbs_waves() == 8 ? rbs_occupancy<1, 8>(smem) : rbs_occupancy<2, 4>(smem); break;
+    case 2: per_cu = rbs_waves() == 8 ? rbs_occupancy<2, 8>(smem) : rbs_occupancy<4, 4>(smem); break;
+    default: return false;
+  }
+  static int cus = 0;
+  if (cus == 0) {
+    int dev = 0, n = 0;
+    if (hipGetDeviceCount(&n) != hipSuccess || n == 0 || hipGetDevice(&dev) != hipSuccess ||
+        hipDeviceGetAttribute(&cus, hipDeviceAttributeMultiprocessorCount, dev) != hipSuccess)
+      cus = -1;
+  }
+  if (cus < 0) return true;   // no device (a CPU process): the shape predicate alone
+  const int nb = rowband_blocks(rows);
+  const long long grid = (long long)(rbs_map() ? (nb + 7) / 8 * 8 : nb) * C;
+  return per_cu > 0 && grid <= (long long)per_cu * cus;
+}
+
 bool rowband_split_ok(int rows, int H, int in, int nh, int act) {
   const int c = rbs_groups(rows);
-  (void)act;
+  (void)act;   // every activation (relu / tanh / none) has a form
   return rows > 0 && H == 512 && in >= 256 && in <= H && in % 256 == 0 && nh >= 1 && nh <= RB_MAXL &&
-         c > 0 && rbs_smem(in, nh) <= 160 * 1024;
+         c > 0 && rbs_smem(in, nh) <= 160 * 1024 && rbs_fits(rows, in, nh);
 }
 
 // (NJ x NW: 1 x 4 -> 8 blocks per band, 2 x 4 -> 4, 4 x 4 -> 2)
 // waves per block at 4 / 2 blocks per band: 8 (1 / 2 tiles per wave) or 4 (2 / 4 tiles per wave;
 // NNMPI_RB_SPLIT_WAVES=4, A/B).  Measured 24.6 vs 25.9 us at 2,048 rows and 32.4 vs 33.9 us at
 // 4,096 (profiles/r5_split_waves_ab.txt).
+// The XCD-grouped band map (NNMPI_RB_SPLIT_MAP, default 1) and, under it, plain stores for the
+// hand-offs of a band found on one XCC (NNMPI_RB_SPLIT_LOCAL, default 1); A/B knobs.
+static int rbs_map() {
+  static const int v = rb_env("NNMPI_RB_SPLIT_MAP", 1) ? 1 : 0;
+  return v;
+}
+static int rbs_local() {
+  static const int v = rb_env("NNMPI_RB_SPLIT_LOCAL", 1) ? 1 : 0;
+  return v;
+}
 static int g_rbs_waves = -1;
 static int rbs_waves() {
   if (g_rbs_waves < 0) g_rbs_waves = rb_env("NNMPI_RB_SPLIT_WAVES", 8) == 4 ? 4 : 8;
   return g_rbs_waves;
+}
+template <int NJ, int NW>
+static int rbs_occupancy(int smem) {
+  static int cached_smem = -1, cached = 0;
+  int ndev = 0;
+  if (hipGetDeviceCount(&ndev) != hipSuccess || ndev == 0) return 0;
+  if (cached_smem != smem) {
+    int n = 0;
+    // (the attribute must allow the dynamic LDS size before the query can answer for it)
+    (void)hipFuncSetAttribute((const void*)rowband_split_kernel<NJ, NW, ACT_RELU>,
+                              hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&n, rowband_split_kernel<NJ, NW, ACT_RELU>, 64 * NW,
+                                                     smem) != hipSuccess)
+      n = 0;
+    cached_smem = smem;
+    cached = n;
+  }
+  return cached;
 }
 template <int NJ, int NW>
 static hipError_t rbs_launch(const RowbandArgs& p, hipStream_t s) {
@@ -1073,7 +1183,8 @@ static hipError_t rbs_launch(const RowbandArgs& p, hipStream_t s) {
     attr = true;
   }
   Fn f = fns[p.act == ACT_RELU ? 1 : p.act == ACT_TANH ? 2 : 0];
-  if (p.stamps) {   // diagnostic stamps: relu only
+  if (p.stamps) {   // diagnostic stamps: relu only (experiments library)
+#if NNMPI_EXPERIMENTS_BUILD
     if (p.act != ACT_RELU) return hipErrorInvalidValue;
     f = rowband_split_kernel<NJ, NW, ACT_RELU, true>;
     static bool sattr = false;
@@ -1081,9 +1192,17 @@ static hipError_t rbs_launch(const RowbandArgs& p, hipStream_t s) {
       (void)hipFuncSetAttribute((const void*)f, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
       sattr = true;
     }
+#else
+    return hipErrorNotSupported;
+#endif
   }
   const int C = 512 / (16 * NJ * NW);
-  hipLaunchKernelGGL(f, dim3(rowband_blocks(p.rows) * C), dim3(64 * NW), rbs_smem(p.in, p.nh), s, p);
+  RowbandArgs q = p;
+  q.rbs_bands = rowband_blocks(p.rows);
+  q.rbs_map = rbs_map();
+  q.rbs_local = q.rbs_map && rbs_local();
+  const int nbp = q.rbs_map ? (q.rbs_bands + 7) / 8 * 8 : q.rbs_bands;
+  hipLaunchKernelGGL(f, dim3(nbp * C), dim3(64 * NW), rbs_smem(p.in, p.nh), s, q);
   return hipGetLastError();
 }
 
@@ -1167,11 +1286,14 @@ static int rb_band_map() {
   return g_rb_band_map;
 }
 
-// diagnostic: phase stamps of the v2 kernel into this buffer (rowband_blocks x 8 x RB_NST uint64)
+// diagnostic: phase stamps of the v2 kernel into this buffer (rowband_blocks x 8 x RB_NST uint64;
+// the stamped kernel twins exist in the experiments library only)
 static unsigned long long* g_rb_stamps = nullptr;
+#if NNMPI_EXPERIMENTS_BUILD
 void set_rowband_stamps(unsigned long long* buf) { g_rb_stamps = buf; }
 int rowband_stamp_slots() { return RB_WAVES * RB_NST; }
 int rowband_split_stamp_slots() { return RBS_NST; }
+#endif
 
 // copy-out store policy (RowbandArgs::out_pol): NNMPI_RB_STORE=0/1/2 (experiments)
 static int g_rb_store = -1;
@@ -1236,7 +1358,11 @@ static int rb_max_splits(int splits, int nh, int H, int rows) {
 
 // per-tile arrival counters of the in-launch fixup (wgrad_multi_fix), one set per layer, after
 // the slabs: zero in a fresh workspace, reset by each tile's last arrival
+#if NNMPI_EXPERIMENTS_BUILD
 static size_t rb_counters(int H, int in) { return rb_pad4((size_t)wgrad_fix_counters(H, std::max(H, in))); }
+#else
+static size_t rb_counters(int, int) { return 0; }
+#endif
 
 // Workspace (floats): the column-split kernel's sync words (RBS_XS ints at a fixed place: they
 // must read zero between launches whatever the batch size), the head partials, the weight-
@@ -1257,6 +1383,8 @@ int rowband_error_word() { return 0; }   // int index into the workspace: a spli
 // step: 37.4 us for the fused launch vs 25.4 + 9.1 us for the two (profiles/r5_wgrad_fixup_ab.txt)
 // -- the combine moves the same slab and optimizer bytes at the same per-CU rate either way, and
 // the fused form adds the wait for a tile's last split -- so it stays off.
+// (experiments library only)
+#if NNMPI_EXPERIMENTS_BUILD
 static int g_rb_fixup = -1;
 constexpr int RB_FIXUP_DEFAULT = 0;
 void set_rb_fixup(int on) { g_rb_fixup = on; }
@@ -1264,6 +1392,9 @@ static bool rb_fixup() {
   if (g_rb_fixup < 0) g_rb_fixup = rb_env("NNMPI_RB_FIXUP", RB_FIXUP_DEFAULT) ? 1 : 0;
   return g_rb_fixup == 1;
 }
+#else
+static constexpr bool rb_fixup() { return false; }
+#endif
 
 // Small batches (the column-split kernel's): the weight gradients as 64 x 64 tiles over the whole
 // K with the update in their epilogue and the head's combine in the same launch (wgrad_small) --
@@ -1320,26 +1451,28 @@ hipError_t rowband_step(const RowbandStep& st0, hipStream_t s) {
   // slabs + combine: 4,096 rows 31.3 vs 16.8 + 9.1 us, 3,000 rows 25.5 vs 14.7 + 9.1;
   // profiles/r5_wgrad_small_ab.txt)
   if (nj > 0 && p.xsync && rb_wgsmall() && p.rows <= 2048 && rowband_split_ok(p.rows, H, p.in, nh, p.act)) {
-    WgmFixArgs im[RB_MAXL];
+    WgOut im[RB_MAXL];
     const bool img = st.sg.g_base && p.Pf[0];
     for (int l = l0; l < l1; ++l)
-      im[l - l0] = WgmFixArgs{img ? const_cast<bf16*>(p.Pf[l]) : nullptr,
+      im[l - l0] = WgOut{img ? const_cast<bf16*>(p.Pf[l]) : nullptr,
                               img && l >= 1 ? const_cast<bf16*>(p.Pd[l]) : nullptr, nullptr};
     return wgrad_small(jobs, nj, im, head ? &head_red : nullptr, s);
   }
+#if NNMPI_EXPERIMENTS_BUILD
   if (nj > 0 && rb_fixup()) {
     // one launch: every layer's weight gradient, its split-K combine + update in the tile's last
     // split, and the head's combine in extra blocks
-    WgmFixArgs fx[RB_MAXL];
+    WgOut fx[RB_MAXL];
     for (int l = l0; l < l1; ++l) {
       const bool img = st.sg.g_base && p.Pf[0];
-      fx[l - l0] = WgmFixArgs{img ? const_cast<bf16*>(p.Pf[l]) : nullptr,
+      fx[l - l0] = WgOut{img ? const_cast<bf16*>(p.Pf[l]) : nullptr,
                               img && l >= 1 ? const_cast<bf16*>(p.Pd[l]) : nullptr,
                               cnt + (size_t)l * rb_counters(H, p.in)};
     }
     const hipError_t ef = wgrad_multi_fix(jobs, nj, sp, fx, head ? &head_red : nullptr, s);
     if (ef != hipErrorNotSupported) return ef;   // (more splits than the fixup takes: below)
   }
+#endif
   if (nj > 0) {
     e = wgrad_multi(jobs, nj, sp, red, s);
     if (e != hipSuccess) return e;

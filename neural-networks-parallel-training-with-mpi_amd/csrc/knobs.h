@@ -5,6 +5,13 @@
 #pragma once
 #include <cstdlib>
 
+// 1 in the experiments library only (_build.py, NNMPI_BUILD_EXPERIMENTS=1): the diagnostic
+// stamped kernel twins, the in-launch split-K fixup and the half-width weight-gradient tile --
+// measured, kept for re-measurement, never on the training path -- are compiled in only there.
+#ifndef NNMPI_EXPERIMENTS_BUILD
+#define NNMPI_EXPERIMENTS_BUILD 0
+#endif
+
 namespace nnmpi {
 
 inline bool experiments_on() {

@@ -608,7 +608,12 @@ class MLPEngine:
         all resident within 2 ms: its results are invalid).  Reads one device word (host sync)."""
         if self.ws_rb is not None and any(self._rb_split.values()) and hasattr(self.ops, "rowband_error_word"):
             i = self.ops.rowband_error_word()
-            if int(self.ws_rb[i:i + 1].view(torch.int32).item()) != 0:
+            word = self.ws_rb[i:i + 1].view(torch.int32)
+            if int(word.item()) != 0:
+                # sticky until read: clear it so one timed-out step is reported once
+                with torch.no_grad():
+                    word.zero_()
+                torch.cuda.synchronize(self.device)
                 raise RuntimeError("row-band split step: a band's hand-off wait timed out (results invalid)")
 
     def schedule_name(self) -> str:
@@ -1167,9 +1172,16 @@ class MLPEngine:
         self.check_device_errors()
         return float(self.loss_out[0].item())
 
-    def synchronize(self):
+    def synchronize(self, check: bool = True):
+        """Wait for the engine's stream.  ``check``: then raise if a column-split row-band step
+        gave up a hand-off wait since the last check (one device word read; only once a split
+        step has run) -- every host sync of the training paths sees a timed-out step instead of
+        training on.  A timed region passes check=False and calls check_device_errors() after
+        its clock stops."""
         if self.is_cuda:
             self.stream.synchronize()
+            if check:
+                self.check_device_errors()
 
     @property
     def flops_per_step(self) -> float:

@@ -338,8 +338,9 @@ class HipOps:
 
     def rowband_split_ok(self, rows: int, H: int, in_: int, nh: int, act: str = "relu") -> bool:
         """A row-band step of ``rows`` rows runs the column-split kernel (rowband.hip
-        rowband_split_kernel: H = 512, 256 <= in <= 512, in % 256 == 0, <= 128 bands; tanh
-        only up to 64 bands)."""
+        rowband_split_kernel: H = 512, 256 <= in <= 512, in % 256 == 0, 1-4 hidden layers,
+        <= 128 bands of 32 rows, any activation; the C++ predicate also requires the grid to fit
+        the chip at its occupancy, so every block of a band can be resident together)."""
         return bool(self.lib.rowband_split_ok(int(rows), int(H), int(in_), int(nh), ACT_CODES[act]))
 
     def rowband_error_word(self) -> int:

@@ -63,6 +63,11 @@ def derived(m, us):
     if m.get("SQ_INSTS_LDS", 0) > 0 and "SQ_LDS_BANK_CONFLICT" in m:
         out.append(f"LDS bank-conflict cycles per LDS instruction "
                    f"{m['SQ_LDS_BANK_CONFLICT'] / m['SQ_INSTS_LDS']:.2f}")
+    if "FETCH_SIZE" in m and us > 0:
+        out.append(f"HBM/MALL fetch {m['FETCH_SIZE'] / 1e3:8.2f} MB ({m['FETCH_SIZE'] / 1e3 / us:6.2f} TB/s "
+                   "over the dispatch)")   # FETCH_SIZE is in KB
+    if "WRITE_SIZE" in m and us > 0:
+        out.append(f"write {m['WRITE_SIZE'] / 1e3:8.2f} MB ({m['WRITE_SIZE'] / 1e3 / us:6.2f} TB/s)")
     if m.get("SQ_WAVE_CYCLES", 0) > 0 and "SQ_WAIT_ANY" in m:
         out.append(f"wave cycles waiting {100 * m['SQ_WAIT_ANY'] / m['SQ_WAVE_CYCLES']:5.1f} %")
     return out

@@ -251,9 +251,14 @@ def test_rowband_in_launch_fixup_is_bitwise_equal_to_combine_launch(widths, rows
     with the fused update (one rank) and with gradients + the optimizer pass."""
     from nnmpi_amd import native
     from nnmpi_amd.ops.hip_ops import HipOps
+    lib = native.lib()
+    if not lib.experiments_built():
+        # production library: the in-launch fixup is not compiled in, its switch refuses
+        with pytest.raises(RuntimeError, match="experiments build only"):
+            lib.set_rb_fixup(1)
+        pytest.skip("in-launch fixup: experiments library only (NNMPI_BUILD_EXPERIMENTS=1)")
     X, Y = _data(rows, widths)
     res = []
-    lib = native.lib()
     monkeypatch.setenv("NNMPI_ROWBAND_MIN_ROWS", "1")
     try:
         for fix in (1, 0):
@@ -283,9 +288,13 @@ def test_rowband_half_width_wgrad_tile_is_bitwise_equal(widths, rows, monkeypatc
     and images after three fused-update steps."""
     from nnmpi_amd import native
     from nnmpi_amd.ops.hip_ops import HipOps
+    lib = native.lib()
+    if not lib.experiments_built():
+        with pytest.raises(RuntimeError, match="experiments build only"):
+            lib.set_wgm_tile(1)
+        pytest.skip("half-width tile: experiments library only (NNMPI_BUILD_EXPERIMENTS=1)")
     X, Y = _data(rows, widths)
     res = []
-    lib = native.lib()
     monkeypatch.setenv("NNMPI_ROWBAND_MIN_ROWS", "1")
     try:
         for tile in (1, 0):
@@ -335,6 +344,47 @@ def test_rowband_fused_update_writes_the_weight_images(widths, rows, monkeypatch
         assert torch.equal(pf, qf), f"forward image of layer {l}"
         if pd is not None:
             assert torch.equal(pd, qd), f"dgrad image of layer {l}"
+
+
+@pytest.mark.parametrize("widths,rows,fuse", [([512, 512, 512, 512, 1], 8192, False),
+                                              ([256, 512, 512, 512, 1], 1000, False),
+                                              ([512] * 5 + [1], 2000, False),
+                                              ([768, 768, 768, 1], 6144, False)])
+def test_rowband_optimizer_pass_writes_the_weight_images(widths, rows, fuse, monkeypatch):
+    """The optimizer pass of the multi-rank row-band step (gradients first, then ops.sgd with
+    the images: here fuse_sgd=False at one rank runs exactly that pass) refreshes the v2 images
+    through the tiled kernel (optim.hip sgd_tiles_kernel): after three steps the images equal a
+    fresh pack of the new bf16 weights, and master / momentum / shadow / images / loss are bitwise
+    those of the element-wise pass (NNMPI_SGD_TILES=0)."""
+    from nnmpi_amd.ops.hip_ops import HipOps
+    if rows < 6144:
+        monkeypatch.setenv("NNMPI_ROWBAND_MIN_ROWS", "6144")
+    X, Y = _data(rows, widths)
+    res = []
+    for tiles in ("1", "0"):
+        monkeypatch.setenv("NNMPI_SGD_TILES", tiles)
+        from nnmpi_amd import native
+        native.lib().set_sgd_tiles(-1)
+        ops = HipOps("cuda")
+        _, ar, eng = _engine(widths, rows, "cuda", ops, lr=1e-3, momentum=0.9, fuse_sgd=fuse,
+                             rowband=True, monkeypatch=monkeypatch)
+        assert eng.rowband and eng.rb_version == 2
+        eng.load_batch(X, Y)
+        eng.set_scales(1.0 / rows, 1.0 / rows, 1.0)
+        for _ in range(3):
+            eng.step()
+        eng.synchronize()
+        nh = len(widths) - 2
+        buf, fresh = ops.rowband_packed(widths[1], widths[0], nh, "cuda")
+        ops.rowband_pack([ar.compute_weight(i) for i in range(nh)], fresh)
+        torch.cuda.synchronize()
+        assert torch.equal(eng._rb_buf, buf), f"images (tiles={tiles}) differ from a fresh pack"
+        res.append((ar.master.clone(), ar.momentum.clone(), ar.shadow.clone(), eng._rb_buf.clone(),
+                    eng.loss()))
+    native.lib().set_sgd_tiles(-1)
+    for a, b in zip(res[0][:4], res[1][:4]):
+        assert torch.equal(a, b)
+    assert res[0][4] == res[1][4]
 
 
 @pytest.mark.parametrize("rows", [8192, 1024, 3000])
