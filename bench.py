@@ -367,12 +367,14 @@ def run(a, job):
             labels = None
         return part, X.to(dtype), Y, labels
 
-    def build(mode, data, comm=True, bucket_mb=None, chunk_tiles=0, bf16_reduce=None):
+    def build(mode, data, comm=True, bucket_mb=None, chunk_tiles=0, bf16_reduce=None, gdt=None):
         """One arena + gradient-sync strategy + engine over ``data`` (a shard()).
         mode: inline | overlap | overlap_rowband | zero1 | none (no gradient synchronisation);
         chunk_tiles: 256x256 tiles per output-row chunk bucket at least (0: the default);
         bf16_reduce: the all-reduce algorithm, "rccl" for RCCL's own ring / tree (None: the
-        default -- acc32 for a bf16 payload, ordered for an fp32 one)."""
+        default -- acc32 for a bf16 payload, ordered for an fp32 one); gdt: the gradient payload
+        dtype of this candidate (None: the job's)."""
+        gdt = gdt or grad_dtype
         part, X, Y, labels = data
         rows = part.rows(rank)
         model = reference_init(widths, "relu", seed=0, device=dev if (big and gpu) else None)
@@ -393,9 +395,9 @@ def run(a, job):
             if zero1:
                 sync = ShardedSync(arena, world, rank, native_comm=native_comm)
             else:
-                bf16 = grad_dtype == "bf16"
+                bf16 = gdt == "bf16"
                 sync = NativeRcclSync(arena, native_comm, world, inline=(mode == "inline"),
-                                      grad_dtype=grad_dtype,
+                                      grad_dtype=gdt,
                                       bf16_reduce=bf16_reduce if bf16 else None,
                                       f32_reduce=None if bf16 else bf16_reduce)
         else:
@@ -405,9 +407,9 @@ def run(a, job):
                 sync = ShardedSync(arena, world, rank, group=comm_group)
             else:
                 sync = (make_shm_sync(arena, comm_group, world, rank)
-                        if shm_sync_ok(dev.type, world, job.local_world, grad_dtype) else None)
+                        if shm_sync_ok(dev.type, world, job.local_world, gdt) else None)
                 if sync is None:
-                    sync = TorchDistSync(arena, comm_group, world, grad_dtype=grad_dtype)
+                    sync = TorchDistSync(arena, comm_group, world, grad_dtype=gdt)
         eng = MLPEngine(spec, arena, make_ops(), sync, device=dev, dtype=dtype,
                         rows_capacity=max(rows, 1), lr=a.lr, momentum=0.9,
                         use_graph=not a.no_graph, overlap=not a.no_overlap,
@@ -545,11 +547,16 @@ def run(a, job):
                 # the row-band step with its last layer's bucket reduced during the other
                 # layers' weight gradients (engine._step_body_rowband_overlap)
                 cands.append(("overlap_rowband", "overlap_rowband", a.bucket_mb, ct0))
+            if gpu and world > 1 and a.grad_dtype == "auto" and native_comm is not None:
+                # the inline all-reduce with half the bytes on the links (bf16 payload, fp32
+                # sums on each element's owner: one rounding whatever P is)
+                cands.append(("inline_bf16", "inline", None, ct0, "bf16"))
+        cands = [x if len(x) == 5 else x + (None,) for x in cands]
 
-        def try_cand(key, m, bmb, ct, red=None):
+        def try_cand(key, m, bmb, ct, gdt=None, red=None):
             nonlocal eng, best_t, mode, bucket_mb, chunk_tiles, bf16_reduce, best
             milestone(f"tune {key}")
-            e = build(m, data, bucket_mb=bmb, chunk_tiles=ct, bf16_reduce=red)
+            e = build(m, data, bucket_mb=bmb, chunk_tiles=ct, bf16_reduce=red, gdt=gdt)
             e.run_steps(a.warmup, chunk_for(a.warmup))
             tm = min(timed(e, a.tune_steps, chunk_for(a.tune_steps)) for _ in range(2))
             if not math.isfinite(tm):
@@ -558,18 +565,18 @@ def run(a, job):
                 del e
                 return
             tune[key] = round(tm / a.tune_steps * 1e3, 5)
-            algo = getattr(e.sync, "bf16_reduce" if grad_dtype == "bf16" else "f32_reduce", None)
+            algo = getattr(e.sync, "bf16_reduce" if (gdt or grad_dtype) == "bf16" else "f32_reduce", None)
             if m != "zero1" and algo:
                 tune_algo[key] = algo
             # every rank sees the same max-over-ranks times, so every rank keeps the same mode
             if eng is None or tm < best_t:
                 eng, best_t, mode, bucket_mb, chunk_tiles = e, tm, key, (bmb or a.bucket_mb), ct
-                bf16_reduce, best = red, (key, m, bmb, ct)
+                bf16_reduce, best = red, (key, m, bmb, ct, gdt)
             del e
 
         tune_algo = {}
-        for key, m, bmb, ct in cands:
-            try_cand(key, m, bmb, ct)
+        for key, m, bmb, ct, gdt in cands:
+            try_cand(key, m, bmb, ct, gdt)
         if native_comm is not None:
             # the all-reduce algorithm is tuned too, under the TWO fastest all-reduce schedules
             # (a slow default algorithm must not decide which schedule wins): each one's default
@@ -579,8 +586,8 @@ def run(a, job):
             for key in ranked:
                 cand = next(x for x in cands if x[0] == key)
                 alt = ("rccl" if tune_algo[key] != "rccl" else
-                       ("acc32" if grad_dtype == "bf16" else "ordered"))
-                try_cand(f"{key}+{alt}", cand[1], cand[2], cand[3], red=alt)
+                       ("acc32" if (cand[4] or grad_dtype) == "bf16" else "ordered"))
+                try_cand(f"{key}+{alt}", cand[1], cand[2], cand[3], cand[4], red=alt)
         if eng is None:
             raise RuntimeError("every gradient-sync candidate gave up a device wait (invalid steps)")
         if gpu:
@@ -619,6 +626,8 @@ def run(a, job):
     mode_name = mode
     # (the tuner's key names the candidate; best[1] is its schedule)
     mode = best[1] if best is not None else mode
+    if best is not None and best[4]:
+        grad_dtype = best[4]      # the chosen candidate's payload (wire bytes, the JSON line)
     sharded = mode == "zero1"
     n_buckets = len(eng.arena.buckets)
     wire = comm_volume(eng.arena.numel, world, grad_dtype, sharded=sharded,
@@ -693,7 +702,8 @@ def run(a, job):
             nonlocal strong
             sdata = shard(rows_pg)
             e = build(mode if mode != "none" else "inline", sdata, bucket_mb=bucket_mb,
-                      chunk_tiles=chunk_tiles, bf16_reduce=bf16_reduce)
+                      chunk_tiles=chunk_tiles, bf16_reduce=bf16_reduce,
+                      gdt=best[4] if best is not None else None)
             e.run_steps(min(a.warmup, 10) + 1, chunk_for(min(a.warmup, 10)))
             s_ms = timed(e, n_ex, chunk_for(n_ex)) / n_ex * 1e3
             if not math.isfinite(s_ms):

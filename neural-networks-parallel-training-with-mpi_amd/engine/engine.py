@@ -710,12 +710,17 @@ class MLPEngine:
             self.sync.launch_bucket(b, self.stream)
         self.sync.finish()
         self._mark("comm")
+        # (every gradient element the pass reads is rewritten by the next step's launches -- the
+        # combines store whole layer gradients, the arena's padding is never written and stays
+        # zero -- so the pass does not zero the gradient behind itself: 3 MB less to write on the
+        # 512-wide proxy)
         if self.rb_packed is not None:
             # the optimizer pass also rewrites the v2 weight images from the updated weights
-            ops.sgd(ar, self.hp, self.nesterov, first, images=dict(enumerate(self.rb_packed)))
+            ops.sgd(ar, self.hp, self.nesterov, first, zero_grad=False,
+                    images=dict(enumerate(self.rb_packed)))
             self._rb_fresh = True
         else:
-            ops.sgd(ar, self.hp, self.nesterov, first)
+            ops.sgd(ar, self.hp, self.nesterov, first, zero_grad=False)
 
     # Grouped schedule: the backward of layer i is ONE launch holding three independent jobs —
     # dgrad_i, wgrad_i (split-K partial slabs) and the slab combine of layer i+1 (with the SGD

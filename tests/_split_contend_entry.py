@@ -17,13 +17,19 @@ def main():
     import nnmpi_amd  # noqa: F401
     from test_split_contention_gpu import _run
     steps = 20
+
+    def wait_for(name):
+        t0 = time.monotonic()
+        while not os.path.exists(os.path.join(d, name)):
+            if time.monotonic() - t0 > 150:
+                raise SystemExit(f"the other process never wrote {name}")
+            time.sleep(0.005)
+    # the solo runs one after the other (process 0 first), then both runs together
+    if rank == 1:
+        wait_for("solo0")
     solo = _run(rows, steps)
-    open(os.path.join(d, f"ready{rank}"), "w").close()
-    t0 = time.monotonic()
-    while not all(os.path.exists(os.path.join(d, f"ready{r}")) for r in (0, 1)):
-        if time.monotonic() - t0 > 120:
-            raise SystemExit("the other process never became ready")
-        time.sleep(0.005)
+    open(os.path.join(d, f"solo{rank}"), "w").close()
+    wait_for(f"solo{1 - rank}")
     errors = 0
     try:
         busy = _run(rows, steps)
