@@ -84,16 +84,16 @@ struct SgdTileJob {
   int np;
 };
 
-template <typename TG>
+template <typename TG, int RT>
 __global__ void __launch_bounds__(256) sgd_tiles_kernel(float* __restrict__ p, TG* __restrict__ g,
                                                         float* __restrict__ buf, bf16* __restrict__ shadow,
                                                         const float* __restrict__ hp, int nesterov,
                                                         int first, int zero_grad, SgdTileJob j) {
+  // RT: 32-row groups per tile (a thread updates RT float4s, every load of the tile in flight
+  // before the first update)
   const float lr = hp[0], mom = hp[1], damp = hp[2], wd = hp[3], gs = hp[4];
-  auto upd = [&](long long i) -> f32x4 {
-    f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
-    const f32x4 gv = load_grad4(g, i);
-    f32x4 bv = (mom != 0.f && !first) ? reinterpret_cast<f32x4*>(buf)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+  const bool useb = mom != 0.f && !first;
+  auto apply = [&](long long i, f32x4 pv, f32x4 gv, f32x4 bv) -> f32x4 {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float bb = bv[r];
@@ -113,30 +113,45 @@ __global__ void __launch_bounds__(256) sgd_tiles_kernel(float* __restrict__ p, T
     }
     return pv;
   };
+  const f32x4 z4 = {0.f, 0.f, 0.f, 0.f};
   const int tid = threadIdx.x;
   const int bid = blockIdx.x;
   if (bid >= j.t0[j.n]) {   // the element-wise rest, grid-stride over its blocks
     const long long nb = gridDim.x - j.t0[j.n];
     for (int q = 0; q < j.np; ++q)
       for (long long i = j.ps[q] + (long long)(bid - j.t0[j.n]) * 256 + tid; i < j.pe[q]; i += nb * 256)
-        (void)upd(i);
+        (void)apply(i, reinterpret_cast<f32x4*>(p)[i], load_grad4(g, i),
+                    useb ? reinterpret_cast<f32x4*>(buf)[i] : z4);
     return;
   }
   int t = 0;
   while (t + 1 < j.n && bid >= j.t0[t + 1]) ++t;
   const int tile = bid - j.t0[t], M = j.M[t], N = j.N[t];
-  const int m0 = (tile / j.tx[t]) * 32, n0 = (tile % j.tx[t]) * 32;
-  const int r = tid >> 3, c4 = tid & 7, m = m0 + r, n = n0 + 4 * c4;
-  __shared__ bf16 tb[32][32 + 8];   // (+8: the column reads below hit different banks)
-  const f32x4 pv = upd((j.start[t] + (long long)m * N + n) / 4);
-  bf16x4 hv;
+  const int m0 = (tile / j.tx[t]) * (32 * RT), n0 = (tile % j.tx[t]) * 32;
+  const int r = tid >> 3, c4 = tid & 7, n = n0 + 4 * c4;
+  __shared__ bf16 tb[32 * RT][32 + 8];   // (+8: the column reads below hit different banks)
+  long long idx[RT];
+  f32x4 pv[RT], gv[RT], bv[RT];
 #pragma unroll
-  for (int e = 0; e < 4; ++e) hv[e] = (bf16)pv[e];
-  if (j.pkf[t]) *reinterpret_cast<bf16x4*>(j.pkf[t] + rb_pk_off(m, n, N)) = hv;
+  for (int q = 0; q < RT; ++q) {
+    idx[q] = (j.start[t] + (long long)(m0 + r + 32 * q) * N + n) / 4;
+    pv[q] = reinterpret_cast<f32x4*>(p)[idx[q]];
+    gv[q] = load_grad4(g, idx[q]);
+    bv[q] = useb ? reinterpret_cast<f32x4*>(buf)[idx[q]] : z4;
+  }
+#pragma unroll
+  for (int q = 0; q < RT; ++q) {
+    const int m = m0 + r + 32 * q;
+    const f32x4 nv = apply(idx[q], pv[q], gv[q], bv[q]);
+    bf16x4 hv;
+#pragma unroll
+    for (int e = 0; e < 4; ++e) hv[e] = (bf16)nv[e];
+    if (j.pkf[t]) *reinterpret_cast<bf16x4*>(j.pkf[t] + rb_pk_off(m, n, N)) = hv;
+    if (j.pkd[t]) *reinterpret_cast<bf16x4*>(&tb[r + 32 * q][4 * c4]) = hv;
+  }
   if (j.pkd[t]) {
-    *reinterpret_cast<bf16x4*>(&tb[r][4 * c4]) = hv;
     __syncthreads();
-    if (tid < 128) {   // column c, rows m0 + 8 g8 .. + 7 -> one 16-byte piece of the W^T image
+    if (tid < 128 * RT) {   // column c, rows m0 + 8 g8 .. + 7 -> one 16-byte piece of the W^T image
       const int c = tid & 31, g8 = tid >> 5;
       bf16x8 col;
 #pragma unroll
@@ -148,7 +163,7 @@ __global__ void __launch_bounds__(256) sgd_tiles_kernel(float* __restrict__ p, T
 
 // The tile job of a pass over n elements with the images of `pk` (false: a shape the tiles do not
 // cover -- the element-wise kernel takes it).
-static bool sgd_tile_job(const SgdPack& pk, long long n, SgdTileJob& j) {
+static bool sgd_tile_job(const SgdPack& pk, long long n, SgdTileJob& j, int rt) {
   j = SgdTileJob{};
   j.n = pk.n;
   int tiles = 0;
@@ -160,12 +175,12 @@ static bool sgd_tile_job(const SgdPack& pk, long long n, SgdTileJob& j) {
   for (int k = 0; k < pk.n; ++k) {
     const int t = ord[k];
     const long long s = pk.start[t], e = s + (long long)pk.M[t] * pk.N[t];
-    if (s < at || e > n || pk.M[t] % 32 || pk.N[t] % 32 || s % 4) return false;
+    if (s < at || e > n || pk.M[t] % (32 * rt) || pk.N[t] % 32 || s % 4) return false;
     j.start[k] = s; j.M[k] = pk.M[t]; j.N[k] = pk.N[t];
     j.pkf[k] = pk.pkf[t]; j.pkd[k] = pk.pkd[t];
     j.tx[k] = pk.N[t] / 32;
     j.t0[k] = tiles;
-    tiles += (pk.M[t] / 32) * (pk.N[t] / 32);
+    tiles += (pk.M[t] / (32 * rt)) * (pk.N[t] / 32);
     if (s > at) { j.ps[j.np] = at / 4; j.pe[j.np] = s / 4; ++j.np; }
     at = e;
   }
@@ -177,13 +192,23 @@ static bool sgd_tile_job(const SgdPack& pk, long long n, SgdTileJob& j) {
 template <typename TG>
 static hipError_t sgd_tiles_launch(float* p, TG* g, float* buf, bf16* shadow, long long n,
                                    const float* hp, int nesterov, int first, int zero_grad,
-                                   const SgdTileJob& j, hipStream_t s) {
+                                   const SgdTileJob& j, int rt, hipStream_t s) {
   long long rest = 0;
   for (int q = 0; q < j.np; ++q) rest += j.pe[q] - j.ps[q];
   const int nb_rest = rest > 0 ? (int)std::min<long long>((rest + 255) / 256, 64) : 0;
-  hipLaunchKernelGGL(sgd_tiles_kernel<TG>, dim3(j.t0[j.n] + nb_rest), dim3(256), 0, s, p, g, buf,
-                     shadow, hp, nesterov, first, zero_grad, j);
+  auto* f = rt == 2 ? sgd_tiles_kernel<TG, 2> : sgd_tiles_kernel<TG, 1>;
+  hipLaunchKernelGGL(f, dim3(j.t0[j.n] + nb_rest), dim3(256), 0, s, p, g, buf, shadow, hp, nesterov,
+                     first, zero_grad, j);
   return hipGetLastError();
+}
+
+// 32-row groups per tile (NNMPI_SGD_TILE_RT=1 / 2, experiments)
+static int sgd_tile_rt() {
+  static const int v = [] {
+    const char* e = knob_env("NNMPI_SGD_TILE_RT");
+    return (e && e[0] == '1') ? 1 : 2;
+  }();
+  return v;
 }
 
 static int g_sgd_tiles = -1;   // NNMPI_SGD_TILES=0: the element-wise image refresh (A/B)
@@ -215,8 +240,9 @@ hipError_t sgd_momentum(float* p, float* g, float* buf, bf16* shadow, long long 
   if (n % 4 != 0 || !pack_ok(pack)) return hipErrorInvalidValue;
   const SgdPack pk = pack ? *pack : SgdPack{};
   SgdTileJob j;
-  if (pk.n > 0 && sgd_tiles_on() && sgd_tile_job(pk, n, j))
-    return sgd_tiles_launch<float>(p, g, buf, shadow, n, hp, nesterov, first, zero_grad, j, s);
+  int rt = sgd_tile_rt();
+  if (pk.n > 0 && sgd_tiles_on() && (sgd_tile_job(pk, n, j, rt) || sgd_tile_job(pk, n, j, rt = 1)))
+    return sgd_tiles_launch<float>(p, g, buf, shadow, n, hp, nesterov, first, zero_grad, j, rt, s);
   hipLaunchKernelGGL(sgd_kernel<float>, dim3(grid_for(n / 4)), dim3(256), 0, s, p, g, buf, shadow,
                      n / 4, hp, nesterov, first, zero_grad, pk);
   return hipGetLastError();
@@ -240,8 +266,9 @@ hipError_t sgd_momentum_bf16grad(float* p, const bf16* g, float* buf, bf16* shad
   if (n % 4 != 0 || !pack_ok(pack)) return hipErrorInvalidValue;
   const SgdPack pk = pack ? *pack : SgdPack{};
   SgdTileJob j;
-  if (pk.n > 0 && sgd_tiles_on() && sgd_tile_job(pk, n, j))
-    return sgd_tiles_launch<const bf16>(p, g, buf, shadow, n, hp, nesterov, first, 0, j, s);
+  int rt = sgd_tile_rt();
+  if (pk.n > 0 && sgd_tiles_on() && (sgd_tile_job(pk, n, j, rt) || sgd_tile_job(pk, n, j, rt = 1)))
+    return sgd_tiles_launch<const bf16>(p, g, buf, shadow, n, hp, nesterov, first, 0, j, rt, s);
   hipLaunchKernelGGL(sgd_kernel<const bf16>, dim3(grid_for(n / 4)), dim3(256), 0, s, p, g, buf,
                      shadow, n / 4, hp, nesterov, first, 0, pk);
   return hipGetLastError();

@@ -154,7 +154,11 @@ class MLPEngine:
         # is not taken; small batches (strong-scaling shards: up to 4,096 rows of the 512-wide
         # proxy) run the column-split form instead (rowband.hip rowband_split_kernel: each band
         # over 2-8 CUs, activations exchanged per layer), everything else the grouped schedule.
-        self.rowband_min_rows = int(knob("NNMPI_ROWBAND_MIN_ROWS", "6144"))
+        # 512-wide shards of 4,097-6,143 rows: the band kernel (the column-split form stops at
+        # 4,096 rows) -- 0.0629 / 0.0641 / 0.0670 ms at 4,500 / 5,000 / 6,000 rows vs the grouped
+        # schedule's 0.0811 / 0.0822 / 0.0868 (profiles/r6_rowband_threshold.txt); other widths
+        # keep the measured 6,144
+        self.rowband_min_rows = int(knob("NNMPI_ROWBAND_MIN_ROWS", "4097" if w[1] == 512 else "6144"))
         self._rb_split: Dict[int, bool] = {}
         # True: the row-band step also copies out the last hidden layer's activations (debug /
         # inspection; nothing downstream reads them)

@@ -436,17 +436,19 @@ def test_bench_default_proxy_step_runs_the_rowband_schedule():
 
 
 def test_small_batches_pick_the_split_kernel_or_the_grouped_schedule(monkeypatch):
-    """Below NNMPI_ROWBAND_MIN_ROWS (default 6,144) the band kernel is not taken (a band's passes
-    cost the same however few bands there are): the 512-wide proxy's small batches (<= 4,096
-    rows) run the column-split kernel, other small batches the grouped schedule; one engine
-    switches between them and the band kernel by batch size."""
+    """Below NNMPI_ROWBAND_MIN_ROWS (default 4,097 for 512-wide hidden layers, 6,144 otherwise)
+    the band kernel is not taken (a band's passes cost the same however few bands there are): the
+    512-wide proxy's small batches (<= 4,096 rows) run the column-split kernel and 4,097 rows up
+    the band kernel (5,000 rows: no grouped schedule left, profiles/r6_rowband_threshold.txt),
+    other widths' small batches the grouped schedule; one engine switches between the kernels by
+    batch size."""
     from nnmpi_amd.ops.hip_ops import HipOps
     monkeypatch.delenv("NNMPI_ROWBAND_MIN_ROWS", raising=False)
     widths = [512, 512, 512, 512, 1]
     _, _, eng = _engine(widths, 8192, "cuda", HipOps("cuda"), rowband=True, monkeypatch=monkeypatch)
     X, Y = _data(8192, widths)
     seen = []
-    for rows, split, name in ((1024, True, "rowband"), (5000, False, "grouped"),
+    for rows, split, name in ((1024, True, "rowband"), (5000, False, "rowband"),
                               (8192, False, "rowband"), (2048, True, "rowband")):
         eng.load_batch(X[:rows], Y[:rows])
         assert eng.uses_rowband_split() == split and eng.schedule_name() == name, rows
