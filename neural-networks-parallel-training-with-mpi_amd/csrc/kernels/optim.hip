@@ -202,11 +202,12 @@ static hipError_t sgd_tiles_launch(float* p, TG* g, float* buf, bf16* shadow, lo
   return hipGetLastError();
 }
 
-// 32-row groups per tile (NNMPI_SGD_TILE_RT=1 / 2, experiments)
+// 32-row groups per tile (NNMPI_SGD_TILE_RT=1 / 2, experiments): one per thread measured 6.16 vs
+// 6.39 us with two at 3.15 M parameters (profiles/r6_wgrad_small_ksplit_ab.txt)
 static int sgd_tile_rt() {
   static const int v = [] {
     const char* e = knob_env("NNMPI_SGD_TILE_RT");
-    return (e && e[0] == '1') ? 1 : 2;
+    return (e && e[0] == '2') ? 2 : 1;
   }();
   return v;
 }
