@@ -582,7 +582,11 @@ def run(a, job):
             # (a slow default algorithm must not decide which schedule wins): each one's default
             # (bf16: acc32, one rounding; fp32: rccl for one bucket, the rank-ordered all-to-all
             # for several) against the other algorithm
-            ranked = sorted((k for k in tune_algo if tune[k] is not None), key=lambda k: tune[k])[:2]
+            # (the bf16-payload inline candidate keeps its one-rounding acc32 reduction: RCCL's
+            # bf16 ring rounds the partial sum at every hop, an error that grows with P)
+            ranked = sorted((k for k in tune_algo if tune[k] is not None and
+                             next(x for x in cands if x[0] == k)[4] != "bf16"),
+                            key=lambda k: tune[k])[:2]
             for key in ranked:
                 cand = next(x for x in cands if x[0] == key)
                 alt = ("rccl" if tune_algo[key] != "rccl" else

@@ -36,6 +36,13 @@ namespace nnmpi {
 // ------------------------------------------------------------------------------------------
 constexpr int MF_TEAMS = 2, MF_WAVES = 4 * MF_TEAMS;
 constexpr int MF_PH = 512;   // columns per weight-gradient phase
+// dlogits staging [team][16 rows][16 outputs] fp32 with padded strides: the weight gradient's
+// A-operand reads (lane: output r, rows 8g .. 8g+7 of the two groups) put lanes of different g at
+// bank offsets 0 / 32 / 16 / 48 instead of all at 0 (4-way conflicts with a 16-float row stride)
+constexpr int MF_DLB_ROW = 20, MF_DLB_TEAM = 336;   // (336 = 16 x 20 + 16: the team offset is 16 banks)
+// the block's gW partial image [16][in] fp32 in LDS: row stride in + 4 (rows 4g + i of the
+// writing lanes land 16 banks apart)
+constexpr int MF_GROW_PAD = 4;
 
 template <int IN>
 struct MfLds {
@@ -45,8 +52,8 @@ struct MfLds {
   static constexpr int WT = WLO + 16 * WROW * 2;            // [IN][16] bf16
   static constexpr int STAGE = WT + IN * 16 * 2;            // [32][MF_PH] bf16, swizzled
   static constexpr int PART = STAGE + 32 * MF_PH * 2;       // [waves][64] f32x4
-  static constexpr int DLB = PART + MF_WAVES * 64 * 16;     // [team][16 rows][16 outs] fp32
-  static constexpr int SUMS = DLB + MF_TEAMS * 256 * 4;     // loss [team]
+  static constexpr int DLB = PART + MF_WAVES * 64 * 16;     // [team][16 rows][16 outs] fp32 (padded)
+  static constexpr int SUMS = DLB + MF_TEAMS * MF_DLB_TEAM * 4;   // loss [team]
   static constexpr int BYTES = SUMS + 64;
 };
 
@@ -229,7 +236,7 @@ __global__ void __launch_bounds__(64 * MF_WAVES) head_mo_fused_kernel(HeadArgs p
     }
     if (w == 0) {
       if (valid && g == 0) block_loss += row_loss;
-      *reinterpret_cast<f32x4*>(dlb + team * 256 + r * 16 + 4 * g) = f32x4{dl[0], dl[1], dl[2], dl[3]};
+      *reinterpret_cast<f32x4*>(dlb + team * MF_DLB_TEAM + r * MF_DLB_ROW + 4 * g) = f32x4{dl[0], dl[1], dl[2], dl[3]};
     }
     __syncthreads();   // both groups' dlogits published
     if (base == g_beg) stamp(3);
@@ -237,8 +244,8 @@ __global__ void __launch_bounds__(64 * MF_WAVES) head_mo_fused_kernel(HeadArgs p
     if (DZ != nullptr) {
       bf16x8 bdl = zero8;   // B operand: dl[row r][outputs 8g .. 8g+7] in bf16
       if (g < 2) {
-        const f32x4 d0 = *reinterpret_cast<const f32x4*>(dlb + team * 256 + r * 16 + 8 * g);
-        const f32x4 d1 = *reinterpret_cast<const f32x4*>(dlb + team * 256 + r * 16 + 8 * g + 4);
+        const f32x4 d0 = *reinterpret_cast<const f32x4*>(dlb + team * MF_DLB_TEAM + r * MF_DLB_ROW + 8 * g);
+        const f32x4 d1 = *reinterpret_cast<const f32x4*>(dlb + team * MF_DLB_TEAM + r * MF_DLB_ROW + 8 * g + 4);
 #pragma unroll
         for (int e = 0; e < 4; ++e) { bdl[e] = (bf16)d0[e]; bdl[e + 4] = (bf16)d1[e]; }
       }
@@ -275,7 +282,7 @@ __global__ void __launch_bounds__(64 * MF_WAVES) head_mo_fused_kernel(HeadArgs p
 #pragma unroll
     for (int e = 0; e < 8; ++e) {
       const int k = 8 * g + e;   // block row 0..31: group k >> 4, row k & 15
-      const float v = dlb[(k >> 4) * 256 + (k & 15) * 16 + r];
+      const float v = dlb[(k >> 4) * MF_DLB_TEAM + (k & 15) * MF_DLB_ROW + r];
       if (wv == 0) bsum += v;
       ahi[e] = (bf16)v;
       alo[e] = (bf16)(v - (float)ahi[e]);
@@ -314,13 +321,14 @@ __global__ void __launch_bounds__(64 * MF_WAVES) head_mo_fused_kernel(HeadArgs p
     for (int t = 0; t < 4; ++t)
 #pragma unroll
       for (int i = 0; i < 4; ++i)
-        gimg[(4 * g + i) * in + ph * MF_PH + (wv * 4 + t) * 16 + r] = gacc[ph][t][i];
+        gimg[(4 * g + i) * (in + MF_GROW_PAD) + ph * MF_PH + (wv * 4 + t) * 16 + r] = gacc[ph][t][i];
   __syncthreads();
   {
-    const int n4 = out * in / 4;
+    const int n4 = out * in / 4, r4 = in / 4;
     float* dst = gws + (long long)blockIdx.x * out * in;
     for (int v = tid; v < n4; v += 64 * MF_WAVES)
-      reinterpret_cast<f32x4*>(dst)[v] = reinterpret_cast<const f32x4*>(gimg)[v];
+      reinterpret_cast<f32x4*>(dst)[v] =
+          *reinterpret_cast<const f32x4*>(gimg + (v / r4) * (in + MF_GROW_PAD) + 4 * (v % r4));
   }
   bsum += __shfl_xor(bsum, 16, 64);
   bsum += __shfl_xor(bsum, 32, 64);

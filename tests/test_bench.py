@@ -143,18 +143,24 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
     assert d["config"]["comm"] == "rccl" and mode.split("+")[0] in ("inline", "zero1", "overlap",
                                                                    "overlap_rowband")
     t = d["config"]["comm_tune_ms_per_step"]
-    assert {"inline", "zero1", "overlap", "overlap_rowband"} <= set(t)
-    # fp32 payload: under the two fastest all-reduce schedules both algorithms (the default and
-    # the other one) are timed; the chosen one is recorded (ZeRO-1 reduce-scatters: none)
-    assert d["config"]["grad_dtype"] == "fp32"
+    assert t is not None, (d.get("fallback"), d.get("attempts"))   # (measured by the tuner)
+    assert {"inline", "zero1", "overlap", "overlap_rowband", "inline_bf16"} <= set(t)
+    # the fp32-payload candidates and the bf16-payload inline one: under the two fastest
+    # all-reduce schedules both algorithms (the default and the other one) are timed; the chosen
+    # one is recorded (ZeRO-1 reduce-scatters: none)
+    bf16 = mode.split("+")[0] == "inline_bf16"
+    assert d["config"]["grad_dtype"] == ("bf16" if bf16 else "fp32")
     zero1 = mode == "zero1"
     alg = d["config"]["comm_tune_algorithm"]
     alts = [k for k in t if "+" in k]
     assert len(alts) == 2, t
     for k in alts:
         base, alt = k.split("+")
-        assert alt in ("rccl", "ordered") and alg[k] == alt != alg[base], (k, alg)
-    assert d["config"]["f32_reduce"] == (None if zero1 else alg[mode]), (mode, alg)
+        assert base != "inline_bf16" and alt in ("rccl", "ordered") and alg[k] == alt != alg[base], (k, alg)
+    if bf16:
+        assert d["config"]["bf16_reduce"] == alg[mode] == "acc32", (mode, alg)
+    else:
+        assert d["config"]["f32_reduce"] == (None if zero1 else alg[mode]), (mode, alg)
     assert d["parallel_efficiency"] is not None and d["comm_bus_gbps"] is not None
     assert d["strong_scaling"]["global_batch"] == 8192
     assert d["final_loss"] == d["final_loss"]
