@@ -141,7 +141,7 @@ def test_bench_two_rank_rehearsal_on_one_gpu():
     assert d["n_gpus"] == 2 and d["rccl_ranks"] == 2 and d["shared_gpu_rehearsal"]
     mode = d["config"]["comm_mode"]
     assert d["config"]["comm"] == "rccl" and mode.split("+")[0] in ("inline", "zero1", "overlap",
-                                                                   "overlap_rowband")
+                                                                   "overlap_rowband", "inline_bf16")
     t = d["config"]["comm_tune_ms_per_step"]
     assert t is not None, (d.get("fallback"), d.get("attempts"))   # (measured by the tuner)
     assert {"inline", "zero1", "overlap", "overlap_rowband", "inline_bf16"} <= set(t)
