@@ -643,13 +643,17 @@ static hipError_t rowband2_launch(const RowbandArgs& p, hipStream_t s) {
 //  * activation gradient l: the block's slice of dZ_{l-1} = (dZ_l W_l)[:, own] * act'(a_{l-1})
 //    goes to p.dz[l-1] and is exchanged like a_l (dZ_0 is not exchanged).
 // 2 nh - 1 hand-offs per step.  Each hand-off follows MI355X_MICROARCH.md "Valid forms" row 1:
-// every handed-off byte stored sc1, every storing wave drains vmcnt before the workgroup
-// barrier, one lane's agent-scope atomic add on the band's phase counter; one lane polls it with
-// sc1 loads (bounded: past RBS_TIMEOUT it records the timeout in the sticky error word
-// xsync[0] and goes on -- no block ever waits without bound), the block joins it at a
-// barrier, every load of the handed-off bytes is an sc1 load.  The last block of a band to
-// finish resets the band's counters (graph-replayable).  Grid <= 256 blocks of 256 / 512 threads:
-// the blocks of a band are consecutive ids (dispatched together).  The weight stream and its
+// the handed-off bytes stored write-through (sc1) -- or plain where every block of the band
+// reported the same XCC id in the first hand-off's counter (the consumers' sc1 loads then read
+// that XCD's L2) -- every storing wave drains vmcnt before the workgroup barrier, one lane's
+// agent-scope atomic add on the band's phase counter; one lane polls it with sc1 loads (bounded:
+// past RBS_TIMEOUT it records the timeout in the sticky error word xsync[0] and goes on -- no
+// block ever waits without bound), the block joins it at a barrier, every load of the handed-off
+// bytes is an sc1 load.  The last block of a band to finish resets the band's counters
+// (graph-replayable).  Grid <= 256 blocks of 256 / 512 threads (host: <= blocks per CU x CUs at
+// the kernel's occupancy); the C blocks of a band share blockIdx.x % 8 (one XCD under round-robin
+// dispatch).  (Computing the whole head in every block from a gathered a_{nh-1} -- one hand-off
+// fewer -- measured no faster: profiles/r6_split_head_handoff_ab.txt.)  The weight stream and its
 // D-deep register ring are the band kernel's (rb2_mainloop), for NJ 16-column tiles per wave.
 // (Reference: dataParallelTraining_NN_MPI.py:99-146 -- the fixed dataset split over P ranks, so
 // a rank's step shrinks as P grows.)
