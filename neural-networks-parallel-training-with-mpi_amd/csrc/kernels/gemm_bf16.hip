@@ -870,6 +870,10 @@ struct WgradMultiParams {
   int gemm_blocks;              // FIX: blocks past this one run the extra combine `tail`
   SlabReduce tail;              // (the row-band head's per-band partials)
   int tail_ws, tail_nb_main, tail_nb_bias;
+  const bf16* kA[RB_MAXL];      // wgrad_small's image path: K-major fragment images of dZ (A)
+  const bf16* kB[RB_MAXL];      // and of the layer input (B); kbands bands
+  int kbands;
+  int gm;                       // image path: tile rows of an XCD's patch (grouped_tile)
 };
 // diagnostic (scripts/r5_wg_stamps.py): every later wgrad_multi launch records per-block stamps
 // (the stamped twins are compiled into the experiments library only)
@@ -1489,7 +1493,93 @@ hipError_t wgrad_multi_fix(const WgradArgs* jobs, int nj, const int* splits, con
 // registers and rewrites the v2 weight images (one rank), or stores the gradient (several ranks);
 // extra blocks combine the head's per-band partials (the row-band head_red).  One launch where
 // the slab form takes two, and no slab round trip.
-template <int GA, int NS>
+//
+// Image path (KPW > 0; the split kernel wrote the operands as K-major MFMA fragments, RowbandArgs
+// ka / kz): no LDS operand stage at all.  Each of the 8 waves takes KPW = kbands / 8 consecutive
+// 32-row k-blocks and computes the whole 64 x 64 tile over them -- 4 + 4 one-KiB fragments per
+// k-block, each a single 16-byte load per lane straight into an MFMA operand, DEP k-blocks in
+// flight -- then the 8 partial tiles are summed in wave order through LDS into the LDS-DMA
+// path's register layout, and the same epilogue runs.  (The LDS-DMA tile streams its operands
+// at ~38 GB/s per CU, profiles/r5_wgrad_small_ab.txt.)
+template <int KPW>
+__device__ __forceinline__ void wgs_kimg_tile(const bf16* __restrict__ za, const bf16* __restrict__ xb,
+                                              int nkb, int gm0, int gn0, bool bias, char* smem,
+                                              f32x4 (&acc)[2], f32x4 (&accb)[2]) {
+  constexpr int DEP = KPW <= 4 ? KPW : 3;
+  const int tid = threadIdx.x, lane = tid & 63;
+  const int w = __builtin_amdgcn_readfirstlane(tid >> 6);
+  const int kb0 = w * KPW;
+  f32x4 pa[4][4], pb[4];
+#pragma unroll
+  for (int i = 0; i < 4; ++i) {
+    pb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+#pragma unroll
+    for (int j = 0; j < 4; ++j) pa[i][j] = f32x4{0.f, 0.f, 0.f, 0.f};
+  }
+  bf16x8 ones;
+#pragma unroll
+  for (int e = 0; e < 8; ++e) ones[e] = (bf16)1.0f;
+  const bf16x8* fa = reinterpret_cast<const bf16x8*>(za) + lane;
+  const bf16x8* fb = reinterpret_cast<const bf16x8*>(xb) + lane;
+  bf16x8 ra[DEP][4], rb[DEP][4];
+  auto load = [&](int t, int sl) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) {
+      ra[sl][i] = fa[((long long)(gm0 + i) * nkb + kb0 + t) * 64];
+      rb[sl][i] = fb[((long long)(gn0 + i) * nkb + kb0 + t) * 64];
+    }
+  };
+#pragma unroll
+  for (int t = 0; t < DEP; ++t) load(t, t);
+#pragma unroll
+  for (int t = 0; t < KPW; ++t) {
+    const int sl = t % DEP;
+#pragma unroll
+    for (int i = 0; i < 4; ++i)
+#pragma unroll
+      for (int j = 0; j < 4; ++j) pa[i][j] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(rb[sl][j], ra[sl][i], pa[i][j], 0, 0, 0);
+    if (bias) {
+#pragma unroll
+      for (int i = 0; i < 4; ++i) pb[i] = __builtin_amdgcn_mfma_f32_16x16x32_bf16(ones, ra[sl][i], pb[i], 0, 0, 0);
+    }
+    // (sched_barrier: the refill stays behind this k-block's MFMAs -- the compiler would hoist
+    // every load of the unrolled loop and spill past 4 k-blocks in flight)
+    __builtin_amdgcn_sched_barrier(0);
+    if (t + DEP < KPW) load(t + DEP, sl);
+    __builtin_amdgcn_sched_barrier(0);
+  }
+  // the partial tiles in wave order: part[w][i][j][lane], bias partials bp[w][i][16]
+  f32x4* part = reinterpret_cast<f32x4*>(smem);
+  float* bp = reinterpret_cast<float*>(part + 8 * 16 * 64);
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+#pragma unroll
+    for (int j = 0; j < 4; ++j) part[((w * 4 + i) * 4 + j) * 64 + lane] = pa[i][j];
+  if (bias && lane < 16) {
+#pragma unroll
+    for (int i = 0; i < 4; ++i) bp[(w * 4 + i) * 16 + lane] = pb[i][0];
+  }
+  __syncthreads();
+  // the LDS-DMA tile's layout: wave (wm, wn) = (w >> 2, w & 3) holds m-groups 2 wm + i, n-group wn
+  const int wm = w >> 2, wn = w & 3;
+#pragma unroll
+  for (int i = 0; i < 2; ++i) {
+    f32x4 t = part[((0 * 4 + 2 * wm + i) * 4 + wn) * 64 + lane];
+#pragma unroll
+    for (int v = 1; v < 8; ++v) t += part[((v * 4 + 2 * wm + i) * 4 + wn) * 64 + lane];
+    acc[i] = t;
+    accb[i] = f32x4{0.f, 0.f, 0.f, 0.f};
+    if (bias && lane < 16) {
+      float b = bp[(0 * 4 + 2 * wm + i) * 16 + lane];
+#pragma unroll
+      for (int v = 1; v < 8; ++v) b += bp[(v * 4 + 2 * wm + i) * 16 + lane];
+      accb[i][0] = b;
+    }
+  }
+}
+constexpr int WGS_KIMG_SMEM = 8 * 16 * 64 * 16 + 8 * 4 * 16 * 4;
+
+template <int GA, int NS, int KPW = 0>
 __global__ void __launch_bounds__(SLAB_THREADS) wgrad_small_kernel(WgradMultiParams g) {
   extern __shared__ __attribute__((aligned(1024))) char smem[];
   // diagnostic (set_wgrad_multi_stamps, scripts/r5_wgs_stamps.py): per block the real-time
@@ -1514,7 +1604,11 @@ __global__ void __launch_bounds__(SLAB_THREADS) wgrad_small_kernel(WgradMultiPar
     if (bid < g.blocks[j]) {
       const int t = xcd_remap(bid, g.blocks[j]);
       if (t >= g.n[j]) break;
-      const int tx = t % g.gx[j], ty = t / g.gx[j];
+      // (image path: an XCD's 8 consecutive tiles as a 2 x 4 patch -- 2 dZ + 4 input panels
+      // through its L2 instead of 1 + 8 for a row of tiles; the main loop streams at the chip's
+      // fetch rate, profiles/r6_wgrad_small_kimg.txt)
+      int tx, ty;
+      grouped_tile(t, g.gx[j], g.tiles[j] / g.gx[j], KPW > 0 ? g.gm : 1, tx, ty);
       const WgmFix& f = g.fix[j];
       const int M = g.wg[j].M, N = g.wg[j].N;
       const int tid = threadIdx.x, lane = tid & 63, w = tid >> 6, wm = w >> 2, wn = w & 3;
@@ -1555,8 +1649,12 @@ __global__ void __launch_bounds__(SLAB_THREADS) wgrad_small_kernel(WgradMultiPar
         }
       }
       f32x4 acc[MI * NJ], accb[MI];
-      dma_gemm_tile<64, 64, 2, 4, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, NS, GA, false, true>(
-          g.wg[j], smem, tx, ty, 0, nullptr, acc, accb);
+      if constexpr (KPW > 0) {
+        wgs_kimg_tile<KPW>(g.kA[j], g.kB[j], g.kbands, ty * 4, tx * 4, tx == 0, smem, acc, accb);
+      } else {
+        dma_gemm_tile<64, 64, 2, 4, XMAJ, XMAJ, EPI_F32, ACT_NONE, true, NS, GA, false, true>(
+            g.wg[j], smem, tx, ty, 0, nullptr, acc, accb);
+      }
       if (stp && threadIdx.x == 0) stp[1] = __builtin_amdgcn_s_memrealtime();
       if (upd) {
         // the updates; the transposed image through LDS as 16-byte pieces (8 rows of a column)
@@ -1614,11 +1712,37 @@ __global__ void __launch_bounds__(SLAB_THREADS) wgrad_small_kernel(WgradMultiPar
   }
 }
 
+// The image path (NNMPI_WGS_KIMG=0: the LDS-DMA tiles, A/B): whole 8-band groups, <= 2,048 rows
+static int g_wgs_kimg = -1;
+void set_wgs_kimg(int v) { g_wgs_kimg = v; }
+bool wgrad_kimg_ok(int rows) {
+  if (g_wgs_kimg < 0) {
+    const char* e = knob_env("NNMPI_WGS_KIMG");
+    g_wgs_kimg = (e && e[0] == '0') ? 0 : 1;
+  }
+  const int nb = (rows + 31) / 32;
+  return g_wgs_kimg == 1 && rows > 0 && nb % 8 == 0 && nb <= 64;
+}
+
 hipError_t wgrad_small(const WgradArgs* jobs, int nj, const WgOut* img, const SlabReduce* tail,
-                       hipStream_t s) {
+                       hipStream_t s, int kbands) {
   if (nj < 1 || nj > RB_MAXL) return hipErrorInvalidValue;
   WgradMultiParams g{};
   g.nj = nj;
+  // the image path when every job has both images and the bands split evenly over 8 waves
+  bool kimg = kbands > 0 && kbands % 8 == 0 && kbands <= 64 && img != nullptr;
+  for (int j = 0; kimg && j < nj; ++j) {
+    kimg = img[j].kA && img[j].kB && jobs[j].M % 64 == 0 && jobs[j].N % 64 == 0 &&
+           jobs[j].K <= kbands * 32 && jobs[j].K > (kbands - 1) * 32;
+    g.kA[j] = img[j].kA;
+    g.kB[j] = img[j].kB;
+  }
+  g.kbands = kbands;
+  static const int gm = [] {   // (NNMPI_WGS_GM 1 / 2 / 4, A/B)
+    const char* e = knob_env("NNMPI_WGS_GM");
+    return (e && (e[0] == '1' || e[0] == '2' || e[0] == '4')) ? e[0] - '0' : 2;
+  }();
+  g.gm = gm;
   int nb = 0;
   for (int j = 0; j < nj; ++j) {
     const WgradArgs& a = jobs[j];
@@ -1671,9 +1795,21 @@ hipError_t wgrad_small(const WgradArgs* jobs, int nj, const WgOut* img, const Sl
   static bool attr = false;
   if (!attr) {
     for (auto* k : {wgrad_small_kernel<2, 4>, wgrad_small_kernel<3, 4>, wgrad_small_kernel<4, 4>,
-                    wgrad_small_kernel<2, 6>, wgrad_small_kernel<2, 8>})
+                    wgrad_small_kernel<2, 6>, wgrad_small_kernel<2, 8>, wgrad_small_kernel<4, 4, 1>,
+                    wgrad_small_kernel<4, 4, 2>, wgrad_small_kernel<4, 4, 3>, wgrad_small_kernel<4, 4, 4>,
+                    wgrad_small_kernel<4, 4, 5>, wgrad_small_kernel<4, 4, 6>, wgrad_small_kernel<4, 4, 7>,
+                    wgrad_small_kernel<4, 4, 8>})
       (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
+  }
+  if (kimg) {
+    using Fn = void (*)(WgradMultiParams);
+    static const Fn kf[8] = {wgrad_small_kernel<4, 4, 1>, wgrad_small_kernel<4, 4, 2>, wgrad_small_kernel<4, 4, 3>,
+                             wgrad_small_kernel<4, 4, 4>, wgrad_small_kernel<4, 4, 5>, wgrad_small_kernel<4, 4, 6>,
+                             wgrad_small_kernel<4, 4, 7>, wgrad_small_kernel<4, 4, 8>};
+    hipLaunchKernelGGL(kf[kbands / 8 - 1], dim3(nb), dim3(SLAB_THREADS), std::max(WGS_KIMG_SMEM, SLAB_PART_BYTES),
+                       s, g);
+    return hipGetLastError();
   }
   hipLaunchKernelGGL(f, dim3(nb), dim3(SLAB_THREADS), smem, s, g);
   return hipGetLastError();

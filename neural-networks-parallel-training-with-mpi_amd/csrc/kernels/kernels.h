@@ -182,6 +182,13 @@ struct RowbandArgs {
   int rbs_bands = 0;   // (set by the launch) bands; rbs_map: XCD-grouped block map, grid padded
   int rbs_map = 0;     // to whole 8-band groups; rbs_local: plain hand-off stores for a band whose
   int rbs_local = 0;   // blocks all report one XCC id
+  // Small-batch weight gradients from K-major operand images (wgrad_small's image path, null:
+  // off): the split kernel also writes each band's 32-row x 16-column MFMA operand fragments of
+  // its share of X (ka[0]), a_{l-1} (ka[l], l >= 1) and dZ_l (kz[l]) -- fragment (g, band) at
+  // element (g * kbands + band) * 512, lane i's 8 rows of column 16 g + (i & 15) at i * 8
+  bf16* ka[RB_MAXL] = {};
+  bf16* kz[RB_MAXL] = {};
+  int kbands = 0;
 };
 // the column-split row-band kernel takes this batch (H = 512, in <= 512, rows below the
 // full-band threshold): 8 blocks per 32-row band, each one 64-column slice of every layer
@@ -242,6 +249,8 @@ hipError_t slab_reduce_multi(const SlabReduce* r, int nr, hipStream_t s);
 struct WgOut {
   bf16* pkf; bf16* pkd;   // with job.sg: the updated W's fragment-major images (null: none)
   int* cnt;               // in-launch fixup (experiments library): per-tile counter words, zero
+  const bf16* kA = nullptr;   // wgrad_small: K-major fragment images of dZ (A) and of the layer
+  const bf16* kB = nullptr;   // input (B), RowbandArgs::kz / ka (null: the LDS-DMA tiles)
 };
 #if NNMPI_EXPERIMENTS_BUILD
 int wgrad_fix_counters(int M, int N);
@@ -249,8 +258,12 @@ int wgrad_fix_counters(int M, int N);
 // Small-batch weight gradients of several layers in ONE launch: 64 x 64 tiles over the whole K
 // (no split), SGD-momentum + the row-band v2 images (img[j], may be null) in the epilogue when
 // jobs[j].sg is set (else the gradient), the head's combine `tail` (may be null) in extra blocks.
+// With img[j].kA / kB set for every job (kbands bands, a multiple of 8 up to 64) the operands
+// come from the K-major fragment images instead (each wave one eighth of K, summed in order).
 hipError_t wgrad_small(const WgradArgs* jobs, int nj, const WgOut* img, const SlabReduce* tail,
-                       hipStream_t s);
+                       hipStream_t s, int kbands = 0);
+bool wgrad_kimg_ok(int rows);   // the image path takes this batch (and NNMPI_WGS_KIMG allows it)
+void set_wgs_kimg(int v);       // A/B: 1 image path, 0 the LDS-DMA tiles, -1 re-read NNMPI_WGS_KIMG
 #if NNMPI_EXPERIMENTS_BUILD
 hipError_t wgrad_multi_fix(const WgradArgs* jobs, int nj, const int* splits, const WgOut* fix,
                            const SlabReduce* tail, hipStream_t s);

@@ -841,6 +841,25 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
       if (r < nvalid) st16(dst + (long long)(row0 + r) * H + k, v);
     }
   };
+  // K-major operand fragments for the small-batch weight gradients (p.kbands, wgrad_small's
+  // image path): fragment (g, band) of a [rows][*] matrix from its LDS image -- lane i holds rows
+  // 8 (i >> 4) .. + 7 of column 16 g + (i & 15), zero past the batch -- one 16-byte store
+  auto kfrag = [&](const char* img, bf16* dst, int g) {
+    const int k = 16 * g + (lane & 15), r0 = 8 * (lane >> 4);
+    bf16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      v[e] = r0 + e < nvalid ? *reinterpret_cast<const bf16*>(img + rb_off(r0 + e, k)) : (bf16)0.f;
+    *reinterpret_cast<bf16x8*>(dst + ((long long)g * p.kbands + band) * 512 + lane * 8) = v;
+  };
+  // ... of the wave's own column groups of an H-wide matrix (issued after a hand-off's arrival,
+  // so they wait in no hand-off's drain)
+  auto kown = [&](const char* img, bf16* dst) {
+    if (!dst) return;
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) kfrag(img, dst, n0 / 16 + j);
+  };
 
   // ---- startup: operands, the band's input rows, the ring's first D k-steps (band kernel) ----
   bf16x8 ring[D][NF];
@@ -904,6 +923,14 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
   }
   __syncthreads();
   stamp();
+  // the input's fragments (the block's share of its column groups), from slot 0: at the first
+  // hand-off (stores issued here would hold up the first main loop's counted ring waits), or
+  // after the forward pass when there is none (nh == 1: slot 0 keeps the input)
+  auto kinput = [&]() {
+    if (!p.ka[0]) return;
+    const int gpb = IN / 16 / C;
+    for (int gi = w; gi < gpb; gi += NW) kfrag(slot(0), p.ka[0], c * gpb + gi);
+  };
 
   f32x4 acc[2][NJ];
   // ---- forward: slot(l + 1) receives the whole band of a_l; the last layer's own columns go
@@ -937,11 +964,14 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
     cur = nxt;
     if (!last) {
       arrive(l);
+      if (l == 0) kinput();
+      kown(out, p.ka[l + 1]);
       wait(l);
       gather(p.a[l], out);
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
+      if (nh == 1) kinput();
     }
   }
   // ---- head: partial logits over the own columns, exchanged and summed in block order ----
@@ -1020,7 +1050,8 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
       }
     }
   }
-  // dZ_{nh-1} of the own columns = dl * w * act'(a), in place and to p.dz[nh-1]
+  // dZ_{nh-1} of the own columns = dl * w * act'(a), in place (the image fragments) and to
+  // p.dz[nh-1]
   {
     const int r = tid / TPR, g = tid % TPR;
     const float dl = q.dls[r];
@@ -1038,12 +1069,17 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
         o[4 + e] = (bf16)(dl * w1[e] * act_bwd_t<ACT>((float)v[4 + e]));
       }
       if (r < nvalid) st16(p.dz[nh - 1] + (long long)(row0 + r) * H + k, o);
+      if (p.kz[nh - 1]) *pz = o;
     }
   }
   if (nh >= 2) {
     arrive(nh);
+    kown(z, p.kz[nh - 1]);
     wait(nh);
     gather(p.dz[nh - 1], z);
+  } else if (p.kz[0]) {
+    __syncthreads();
+    kown(z, p.kz[0]);
   }
   // ---- activation gradients: the own columns of dZ_{l-1}, over a_{l-1} in slot(l) ----
   for (int l = nh - 1; l >= 1; --l) {
@@ -1076,8 +1112,11 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
     if (l >= 2) {
       const int ph = 2 * nh - l;
       arrive(ph);
+      kown(out, p.kz[l - 1]);
       wait(ph);
       gather(p.dz[l - 1], out);
+    } else {
+      kown(out, p.kz[0]);
     }
     z = out;
   }
@@ -1368,15 +1407,20 @@ static size_t rb_counters(int H, int in) { return rb_pad4((size_t)wgrad_fix_coun
 static size_t rb_counters(int, int) { return 0; }
 #endif
 
+// K-major operand images of the small-batch weight gradients (RowbandArgs::ka / kz): 2 nh of
+// them, each up to 64 bands (2,048 rows) x 32 rows x max(H, in) bf16 (floats)
+static size_t rb_kimg_floats(int H, int in) { return (size_t)64 * RB_ROWS * std::max(H, in) / 2; }
+
 // Workspace (floats): the column-split kernel's sync words (RBS_XS ints at a fixed place: they
 // must read zero between launches whatever the batch size), the head partials, the weight-
-// gradient slabs, the fixup counters, the split kernel's head exchange (G x 8 x 32).
+// gradient slabs, the fixup counters, the split kernel's head exchange (G x 8 x 32), the K-major
+// operand images.
 size_t rowband_workspace_bytes(int rows, int H, int in, int nh, int splits) {
   const size_t G = (size_t)rowband_blocks(rows);
   const int S = rb_max_splits(splits, nh, H, rows);
   const size_t head = G * H + rb_pad4(G) + rb_pad4(G);
   return (RBS_XS + head + (size_t)nh * S * ((size_t)H * std::max(H, in) + H) +
-          (size_t)nh * rb_counters(H, in) + G * 8 * RB_ROWS) *
+          (size_t)nh * rb_counters(H, in) + G * 8 * RB_ROWS + 2 * (size_t)nh * rb_kimg_floats(H, in)) *
          sizeof(float);
 }
 int rowband_error_word() { return 0; }   // int index into the workspace: a split-kernel wait timed out
@@ -1430,6 +1474,20 @@ hipError_t rowband_step(const RowbandStep& st0, hipStream_t s) {
     p.zero_words = cnt;
     p.n_zero = nh * (int)rb_counters(H, p.in);
   }
+  // the small-batch weight gradients' image path: the split kernel writes the operand images
+  const bool wgs = p.xsync && rb_wgsmall() && p.rows <= 2048 && rowband_split_ok(p.rows, H, p.in, nh, p.act);
+  const bool kimg = wgs && wgrad_kimg_ok(p.rows);
+  for (int l = 0; l < RB_MAXL; ++l) p.ka[l] = p.kz[l] = nullptr;
+  p.kbands = 0;
+  if (kimg) {
+    bf16* kb = reinterpret_cast<bf16*>(p.hx + G * 8 * RB_ROWS);
+    const size_t per_img = 2 * rb_kimg_floats(H, p.in);   // (bf16 elements)
+    for (int l = 0; l < nh; ++l) {
+      p.ka[l] = kb + (size_t)(2 * l) * per_img;
+      p.kz[l] = kb + (size_t)(2 * l + 1) * per_img;
+    }
+    p.kbands = (int)G;
+  }
   hipError_t e = hipSuccess;
   if (st.phase <= 1) {
     e = rowband_fwd_bwd(p, s);
@@ -1454,13 +1512,13 @@ hipError_t rowband_step(const RowbandStep& st0, hipStream_t s) {
   // (<= 2,048 rows: above, the un-split k loop -- ~0.35 us per 64 rows -- loses to the split-K
   // slabs + combine: 4,096 rows 31.3 vs 16.8 + 9.1 us, 3,000 rows 25.5 vs 14.7 + 9.1;
   // profiles/r5_wgrad_small_ab.txt)
-  if (nj > 0 && p.xsync && rb_wgsmall() && p.rows <= 2048 && rowband_split_ok(p.rows, H, p.in, nh, p.act)) {
+  if (nj > 0 && wgs) {
     WgOut im[RB_MAXL];
     const bool img = st.sg.g_base && p.Pf[0];
     for (int l = l0; l < l1; ++l)
       im[l - l0] = WgOut{img ? const_cast<bf16*>(p.Pf[l]) : nullptr,
-                              img && l >= 1 ? const_cast<bf16*>(p.Pd[l]) : nullptr, nullptr};
-    return wgrad_small(jobs, nj, im, head ? &head_red : nullptr, s);
+                         img && l >= 1 ? const_cast<bf16*>(p.Pd[l]) : nullptr, nullptr, p.kz[l], p.ka[l]};
+    return wgrad_small(jobs, nj, im, head ? &head_red : nullptr, s, p.kbands);
   }
 #if NNMPI_EXPERIMENTS_BUILD
   if (nj > 0 && rb_fixup()) {

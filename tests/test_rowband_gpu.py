@@ -81,7 +81,13 @@ _SPLIT_SHAPES = [([512, 512, 512, 512, 1], 1024, "relu", 0),
                  ([512, 512, 512, 512, 1], 777, "tanh", 0),
                  ([512, 512, 512, 512, 1], 1000, "relu", 4),
                  ([512, 512, 512, 512, 1], 1000, "relu", 2),
-                 ([512, 512, 512, 512, 1], 2048, "relu", 2)]
+                 ([512, 512, 512, 512, 1], 2048, "relu", 2),
+                 # the weight gradients' image path at other shapes (whole 8-band groups): one
+                 # hidden layer, input width 256, 3 / 6 k-blocks per wave, four hidden layers
+                 ([512, 512, 1], 256, "relu", 0),
+                 ([256, 512, 512, 512, 1], 1024, "relu", 0),
+                 ([512, 512, 512, 512, 1], 768, "tanh", 0),
+                 ([512] * 5 + [1], 1536, "relu", 0)]
 
 
 @pytest.mark.parametrize("widths,rows,act,groups", _SPLIT_SHAPES)
@@ -132,6 +138,43 @@ def test_rowband_small_wgrad_matches_the_slab_form(rows, monkeypatch):
             res.append((ar.master.double().cpu(), losses))
     finally:
         lib.set_rb_wgsmall(-1)
+    (p1, l1), (p2, l2) = res
+    assert float((p1 - p2).norm() / p2.norm()) < 1e-5
+    for a, b in zip(l1, l2):
+        assert a == pytest.approx(b, rel=1e-4)
+
+
+@pytest.mark.parametrize("widths,rows", [([512, 512, 512, 512, 1], 1024), ([512, 512, 512, 512, 1], 2048),
+                                         ([512, 512, 1], 256), ([256, 512, 512, 512, 1], 1000),
+                                         ([512] * 5 + [1], 1536)])
+def test_rowband_small_wgrad_image_path_matches_the_lds_tiles(widths, rows, monkeypatch):
+    """wgrad_small's image path (operands from the K-major fragments the split kernel writes,
+    K split over the 8 waves, partial tiles summed in wave order; gemm_bf16.hip wgs_kimg_tile)
+    against its LDS-DMA tiles (set_wgs_kimg(0)): three fused-update steps, parameters within
+    1e-5 relative (different summation order), losses within 1e-4; no wait timed out."""
+    from nnmpi_amd import native
+    from nnmpi_amd.ops.hip_ops import HipOps
+    lib = native.lib()
+    monkeypatch.setenv("NNMPI_ROWBAND_MIN_ROWS", "6144")
+    assert lib.wgrad_kimg_ok(rows)
+    X, Y = _data(rows, widths)
+    res = []
+    try:
+        for kimg in (1, 0):
+            assert lib.set_wgs_kimg(kimg)
+            _, ar, eng = _engine(widths, rows, "cuda", HipOps("cuda"), lr=1e-3, momentum=0.9,
+                                 rowband=True, monkeypatch=monkeypatch)
+            assert eng.uses_rowband_split(rows)
+            eng.load_batch(X, Y)
+            eng.set_scales(1.0 / rows, 1.0 / rows, 1.0)
+            losses = []
+            for _ in range(3):
+                eng.step()
+                losses.append(eng.loss())
+            eng.check_device_errors()
+            res.append((ar.master.double().cpu(), losses))
+    finally:
+        lib.set_wgs_kimg(-1)
     (p1, l1), (p2, l2) = res
     assert float((p1 - p2).norm() / p2.norm()) < 1e-5
     for a, b in zip(l1, l2):
