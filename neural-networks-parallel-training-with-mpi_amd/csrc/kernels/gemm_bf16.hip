@@ -1578,6 +1578,7 @@ __device__ __forceinline__ void wgs_kimg_tile(const bf16* __restrict__ za, const
   }
 }
 constexpr int WGS_KIMG_SMEM = 8 * 16 * 64 * 16 + 8 * 4 * 16 * 4;
+constexpr int WGS_KIMG_MAXB = 128;   // bands (4,096 rows): up to 16 k-blocks per wave
 
 template <int GA, int NS, int KPW = 0>
 __global__ void __launch_bounds__(SLAB_THREADS) wgrad_small_kernel(WgradMultiParams g) {
@@ -1712,7 +1713,7 @@ __global__ void __launch_bounds__(SLAB_THREADS) wgrad_small_kernel(WgradMultiPar
   }
 }
 
-// The image path (NNMPI_WGS_KIMG=0: the LDS-DMA tiles, A/B): whole 8-band groups, <= 2,048 rows
+// The image path (NNMPI_WGS_KIMG=0: the LDS-DMA tiles, A/B): whole 8-band groups, <= 4,096 rows
 static int g_wgs_kimg = -1;
 void set_wgs_kimg(int v) { g_wgs_kimg = v; }
 bool wgrad_kimg_ok(int rows) {
@@ -1721,7 +1722,7 @@ bool wgrad_kimg_ok(int rows) {
     g_wgs_kimg = (e && e[0] == '0') ? 0 : 1;
   }
   const int nb = (rows + 31) / 32;
-  return g_wgs_kimg == 1 && rows > 0 && nb % 8 == 0 && nb <= 64;
+  return g_wgs_kimg == 1 && rows > 0 && nb % 8 == 0 && nb <= WGS_KIMG_MAXB;
 }
 
 hipError_t wgrad_small(const WgradArgs* jobs, int nj, const WgOut* img, const SlabReduce* tail,
@@ -1730,7 +1731,7 @@ hipError_t wgrad_small(const WgradArgs* jobs, int nj, const WgOut* img, const Sl
   WgradMultiParams g{};
   g.nj = nj;
   // the image path when every job has both images and the bands split evenly over 8 waves
-  bool kimg = kbands > 0 && kbands % 8 == 0 && kbands <= 64 && img != nullptr;
+  bool kimg = kbands > 0 && kbands % 8 == 0 && kbands <= WGS_KIMG_MAXB && img != nullptr;
   for (int j = 0; kimg && j < nj; ++j) {
     kimg = img[j].kA && img[j].kB && jobs[j].M % 64 == 0 && jobs[j].N % 64 == 0 &&
            jobs[j].K <= kbands * 32 && jobs[j].K > (kbands - 1) * 32;
@@ -1795,18 +1796,23 @@ hipError_t wgrad_small(const WgradArgs* jobs, int nj, const WgOut* img, const Sl
   static bool attr = false;
   if (!attr) {
     for (auto* k : {wgrad_small_kernel<2, 4>, wgrad_small_kernel<3, 4>, wgrad_small_kernel<4, 4>,
-                    wgrad_small_kernel<2, 6>, wgrad_small_kernel<2, 8>, wgrad_small_kernel<4, 4, 1>,
-                    wgrad_small_kernel<4, 4, 2>, wgrad_small_kernel<4, 4, 3>, wgrad_small_kernel<4, 4, 4>,
-                    wgrad_small_kernel<4, 4, 5>, wgrad_small_kernel<4, 4, 6>, wgrad_small_kernel<4, 4, 7>,
-                    wgrad_small_kernel<4, 4, 8>})
+                    wgrad_small_kernel<2, 6>, wgrad_small_kernel<2, 8>})
       (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
     attr = true;
   }
   if (kimg) {
     using Fn = void (*)(WgradMultiParams);
-    static const Fn kf[8] = {wgrad_small_kernel<4, 4, 1>, wgrad_small_kernel<4, 4, 2>, wgrad_small_kernel<4, 4, 3>,
-                             wgrad_small_kernel<4, 4, 4>, wgrad_small_kernel<4, 4, 5>, wgrad_small_kernel<4, 4, 6>,
-                             wgrad_small_kernel<4, 4, 7>, wgrad_small_kernel<4, 4, 8>};
+    static const Fn kf[16] = {wgrad_small_kernel<4, 4, 1>,  wgrad_small_kernel<4, 4, 2>,  wgrad_small_kernel<4, 4, 3>,
+                              wgrad_small_kernel<4, 4, 4>,  wgrad_small_kernel<4, 4, 5>,  wgrad_small_kernel<4, 4, 6>,
+                              wgrad_small_kernel<4, 4, 7>,  wgrad_small_kernel<4, 4, 8>,  wgrad_small_kernel<4, 4, 9>,
+                              wgrad_small_kernel<4, 4, 10>, wgrad_small_kernel<4, 4, 11>, wgrad_small_kernel<4, 4, 12>,
+                              wgrad_small_kernel<4, 4, 13>, wgrad_small_kernel<4, 4, 14>, wgrad_small_kernel<4, 4, 15>,
+                              wgrad_small_kernel<4, 4, 16>};
+    static bool kattr = false;
+    if (!kattr) {
+      for (Fn k : kf) (void)hipFuncSetAttribute((const void*)k, hipFuncAttributeMaxDynamicSharedMemorySize, 160 * 1024);
+      kattr = true;
+    }
     hipLaunchKernelGGL(kf[kbands / 8 - 1], dim3(nb), dim3(SLAB_THREADS), std::max(WGS_KIMG_SMEM, SLAB_PART_BYTES),
                        s, g);
     return hipGetLastError();

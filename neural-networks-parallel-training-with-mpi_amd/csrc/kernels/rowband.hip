@@ -802,8 +802,29 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
     else
       asm volatile("global_store_dwordx4 %0, %1, off sc1\n s_nop 1" ::"v"(dst), "v"(d) : "memory");
   };
-  // the whole band of a handed-off [rows][H] matrix into an LDS image (padding rows zero)
-  auto gather = [&](const bf16* src, char* img) {
+  // K-major operand fragments for the small-batch weight gradients (p.kbands, wgrad_small's
+  // image path): fragment (g, band) of a [rows][*] matrix from its LDS image -- lane i holds rows
+  // 8 (i >> 4) .. + 7 of column 16 g + (i & 15), zero past the batch -- one 16-byte store
+  auto kfrag = [&](const char* img, bf16* dst, int g) {
+    const int k = 16 * g + (lane & 15), r0 = 8 * (lane >> 4);
+    bf16x8 v;
+#pragma unroll
+    for (int e = 0; e < 8; ++e)
+      v[e] = r0 + e < nvalid ? *reinterpret_cast<const bf16*>(img + rb_off(r0 + e, k)) : (bf16)0.f;
+    *reinterpret_cast<bf16x8*>(dst + ((long long)g * p.kbands + band) * 512 + lane * 8) = v;
+  };
+  // ... of the wave's own column groups of an H-wide matrix (NJ stores)
+  auto kown = [&](const char* img, bf16* dst) {
+    if (!dst) return;
+    asm volatile("" ::: "memory");
+#pragma unroll
+    for (int j = 0; j < NJ; ++j) kfrag(img, dst, n0 / 16 + j);
+  };
+  // the whole band of a handed-off [rows][H] matrix into an LDS image (padding rows zero).  With
+  // kdst, the own fragments of the matrix the image holds now (the band's own columns are the same
+  // bits in both) are written while the loads fly: their NJ stores, the youngest, stay out of the
+  // loads' wait -- issued before the loads, the wait would hold for their write acknowledgements
+  auto gather = [&](const bf16* src, char* img, bf16* kdst) {
     constexpr int IT = RB_ROWS * H / 8 / NT;
     bf16x8 v[IT];
 #pragma unroll
@@ -812,7 +833,12 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
       const int kb = id / (RB_ROWS * 8), r = (id >> 3) & (RB_ROWS - 1), k8 = id & 7;
       v[it] = ld_sc1_b16(src + (long long)(row0 + min(r, nvalid - 1)) * H + kb * 64 + k8 * 8);
     }
-    asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    if (kdst) {
+      kown(img, kdst);
+      asm volatile("s_waitcnt vmcnt(%0)" ::"n"(NJ) : "memory");
+    } else {
+      asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
+    }
 #pragma unroll
     for (int it = 0; it < IT; ++it) {
       asm volatile("" : "+v"(v[it]));
@@ -840,25 +866,6 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
       const bf16x8 v = *reinterpret_cast<const bf16x8*>(img + rb_off(r, k));
       if (r < nvalid) st16(dst + (long long)(row0 + r) * H + k, v);
     }
-  };
-  // K-major operand fragments for the small-batch weight gradients (p.kbands, wgrad_small's
-  // image path): fragment (g, band) of a [rows][*] matrix from its LDS image -- lane i holds rows
-  // 8 (i >> 4) .. + 7 of column 16 g + (i & 15), zero past the batch -- one 16-byte store
-  auto kfrag = [&](const char* img, bf16* dst, int g) {
-    const int k = 16 * g + (lane & 15), r0 = 8 * (lane >> 4);
-    bf16x8 v;
-#pragma unroll
-    for (int e = 0; e < 8; ++e)
-      v[e] = r0 + e < nvalid ? *reinterpret_cast<const bf16*>(img + rb_off(r0 + e, k)) : (bf16)0.f;
-    *reinterpret_cast<bf16x8*>(dst + ((long long)g * p.kbands + band) * 512 + lane * 8) = v;
-  };
-  // ... of the wave's own column groups of an H-wide matrix (issued after a hand-off's arrival,
-  // so they wait in no hand-off's drain)
-  auto kown = [&](const char* img, bf16* dst) {
-    if (!dst) return;
-    asm volatile("" ::: "memory");
-#pragma unroll
-    for (int j = 0; j < NJ; ++j) kfrag(img, dst, n0 / 16 + j);
   };
 
   // ---- startup: operands, the band's input rows, the ring's first D k-steps (band kernel) ----
@@ -965,9 +972,8 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
     if (!last) {
       arrive(l);
       if (l == 0) kinput();
-      kown(out, p.ka[l + 1]);
       wait(l);
-      gather(p.a[l], out);
+      gather(p.a[l], out, p.ka[l + 1]);
     } else {
       asm volatile("s_waitcnt vmcnt(0)" ::: "memory");
       __syncthreads();
@@ -1074,9 +1080,8 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
   }
   if (nh >= 2) {
     arrive(nh);
-    kown(z, p.kz[nh - 1]);
     wait(nh);
-    gather(p.dz[nh - 1], z);
+    gather(p.dz[nh - 1], z, p.kz[nh - 1]);
   } else if (p.kz[0]) {
     __syncthreads();
     kown(z, p.kz[0]);
@@ -1112,9 +1117,8 @@ __global__ void __launch_bounds__(64 * NW) rowband_split_kernel(RowbandArgs p) {
     if (l >= 2) {
       const int ph = 2 * nh - l;
       arrive(ph);
-      kown(out, p.kz[l - 1]);
       wait(ph);
-      gather(p.dz[l - 1], out);
+      gather(p.dz[l - 1], out, p.kz[l - 1]);
     } else {
       kown(out, p.kz[0]);
     }
@@ -1408,8 +1412,8 @@ static size_t rb_counters(int, int) { return 0; }
 #endif
 
 // K-major operand images of the small-batch weight gradients (RowbandArgs::ka / kz): 2 nh of
-// them, each up to 64 bands (2,048 rows) x 32 rows x max(H, in) bf16 (floats)
-static size_t rb_kimg_floats(int H, int in) { return (size_t)64 * RB_ROWS * std::max(H, in) / 2; }
+// them, each up to 128 bands (4,096 rows) x 32 rows x max(H, in) bf16 (floats)
+static size_t rb_kimg_floats(int H, int in) { return (size_t)128 * RB_ROWS * std::max(H, in) / 2; }
 
 // Workspace (floats): the column-split kernel's sync words (RBS_XS ints at a fixed place: they
 // must read zero between launches whatever the batch size), the head partials, the weight-
@@ -1475,8 +1479,11 @@ hipError_t rowband_step(const RowbandStep& st0, hipStream_t s) {
     p.n_zero = nh * (int)rb_counters(H, p.in);
   }
   // the small-batch weight gradients' image path: the split kernel writes the operand images
-  const bool wgs = p.xsync && rb_wgsmall() && p.rows <= 2048 && rowband_split_ok(p.rows, H, p.in, nh, p.act);
-  const bool kimg = wgs && wgrad_kimg_ok(p.rows);
+  // (<= 2,048 rows the LDS-DMA tiles, up to 4,096 the image path: above 2,048 rows the tiles' un-split
+  // k loop loses to the split-K slabs + combine, the image path does not: profiles/r6_wgrad_small_kimg.txt)
+  const bool split_ok = p.xsync && rb_wgsmall() && rowband_split_ok(p.rows, H, p.in, nh, p.act);
+  const bool kimg = split_ok && p.rows <= 4096 && wgrad_kimg_ok(p.rows);
+  const bool wgs = kimg || (split_ok && p.rows <= 2048);
   for (int l = 0; l < RB_MAXL; ++l) p.ka[l] = p.kz[l] = nullptr;
   p.kbands = 0;
   if (kimg) {

@@ -146,12 +146,14 @@ def test_rowband_small_wgrad_matches_the_slab_form(rows, monkeypatch):
 
 @pytest.mark.parametrize("widths,rows", [([512, 512, 512, 512, 1], 1024), ([512, 512, 512, 512, 1], 2048),
                                          ([512, 512, 1], 256), ([256, 512, 512, 512, 1], 1000),
-                                         ([512] * 5 + [1], 1536)])
+                                         ([512] * 5 + [1], 1536), ([512, 512, 512, 1], 3072),
+                                         ([512, 512, 512, 512, 1], 4096)])
 def test_rowband_small_wgrad_image_path_matches_the_lds_tiles(widths, rows, monkeypatch):
     """wgrad_small's image path (operands from the K-major fragments the split kernel writes,
     K split over the 8 waves, partial tiles summed in wave order; gemm_bf16.hip wgs_kimg_tile)
-    against its LDS-DMA tiles (set_wgs_kimg(0)): three fused-update steps, parameters within
-    1e-5 relative (different summation order), losses within 1e-4; no wait timed out."""
+    against what runs without it (set_wgs_kimg(0)): the LDS-DMA tiles up to 2,048 rows, the
+    split-K slabs + combine above: three fused-update steps, parameters within 1e-5 relative
+    (different summation order), losses within 1e-4; no wait timed out."""
     from nnmpi_amd import native
     from nnmpi_amd.ops.hip_ops import HipOps
     lib = native.lib()
