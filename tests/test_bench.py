@@ -199,7 +199,11 @@ def test_bench_tunes_the_bf16_reduction_algorithm():
     assert len(rccl) == 2 and all(k[:-5] in t for k in rccl), t
     assert d["config"]["bf16_reduce"] == ("rccl" if d["config"]["comm_mode"].endswith("+rccl")
                                           else "acc32")
-    if d["config"]["comm_mode"].startswith("overlap"):
+    if d["config"]["comm_mode"].startswith("overlap_c2"):
+        # (the 2-chunks-per-layer candidate, --chunk_tiles 512: 2 chunk buckets per 2048-wide
+        # layer's weight gradient)
+        assert d["config"]["n_buckets"] > 1
+    elif d["config"]["comm_mode"].startswith("overlap"):
         assert d["config"]["n_buckets"] > 5      # chunk buckets (inline replans to one bucket)
     assert d["replicas_bitwise_equal"] is True
 
