@@ -4,7 +4,7 @@
 # (its strong_scaling block runs the column-split row-band step).  Usage: r5_final.sh [part]
 cd "${GRAFT_REPO_ROOT:-$(dirname "$0")/..}" || exit 2
 export TMPDIR=/tmp
-O=gpurun_out/r6final; mkdir -p $O
+O=${R6OUT:-gpurun_out/r6final}; mkdir -p $O
 ( while true; do date > $O/heartbeat; sleep 50; done ) &
 HB=$!
 trap "kill $HB" EXIT
