@@ -33,11 +33,15 @@ __global__ void __launch_bounds__(256) sgd_kernel(float* __restrict__ p, TG* __r
                                                   long long n4, const float* __restrict__ hp,
                                                   int nesterov, int first, int zero_grad, SgdPack pk) {
   const float lr = hp[0], mom = hp[1], damp = hp[2], wd = hp[3], gs = hp[4];
+  // (the momentum load is gated by kernel arguments only, not by the hyper-parameters in device
+  // memory: gated by hp[1] it waited for that load's round trip before issuing -- two dependent
+  // round trips per element.  sgd_elem reads buf only when mom != 0 and not first: same bits)
+  const bool ldb = buf != nullptr && !first;
   const long long stride = (long long)gridDim.x * blockDim.x;
   for (long long i = (long long)blockIdx.x * blockDim.x + threadIdx.x; i < n4; i += stride) {
     f32x4 pv = reinterpret_cast<f32x4*>(p)[i];
     f32x4 gv = load_grad4(g, i);
-    f32x4 bv = (mom != 0.f && !first) ? reinterpret_cast<f32x4*>(buf)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
+    f32x4 bv = ldb ? reinterpret_cast<f32x4*>(buf)[i] : f32x4{0.f, 0.f, 0.f, 0.f};
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
       float bb = bv[r];
@@ -92,7 +96,8 @@ __global__ void __launch_bounds__(256) sgd_tiles_kernel(float* __restrict__ p, T
   // RT: 32-row groups per tile (a thread updates RT float4s, every load of the tile in flight
   // before the first update)
   const float lr = hp[0], mom = hp[1], damp = hp[2], wd = hp[3], gs = hp[4];
-  const bool useb = mom != 0.f && !first;
+  // (momentum loads gated by kernel arguments only, as in sgd_kernel: no wait for hp[1])
+  const bool useb = buf != nullptr && !first;
   auto apply = [&](long long i, f32x4 pv, f32x4 gv, f32x4 bv) -> f32x4 {
 #pragma unroll
     for (int r = 0; r < 4; ++r) {
