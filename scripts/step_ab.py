@@ -92,6 +92,10 @@ def main():
             apply(lib, knobs)
             for t, s in zip(state, snap):
                 t.copy_(s)
+            # (the weights changed outside an optimizer step: the row-band v2 weight images are
+            # rebuilt before the next step -- without this, every config after the first started
+            # from the previous config's images and no rowband config compared bitwise)
+            arena.version += 1
             eng._graphs.clear()
             eng.run_steps(a.chunk, a.chunk)          # capture + warm the new kernels
             eng.prepare_steps(a.steps, a.chunk)
